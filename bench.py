@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: layered int8 offset-min-sum decode of DVB-S2
+N=64800 r=1/2 at 50 iterations (BASELINE.json configs[2]: batch 4096 per GPU).
+
+A "step" = one pass of the hot path over one batch: frame-major int8 LLRs
+already resident in HBM -> interleave -> layered decode (50 it) -> hard
+decisions (frame-major) -> bit/frame error count.  Inputs come from the
+integer-exact AWGN generator on the device (synthetic, all-zero codeword, as
+the reference's CFakeEncoder + channel) and are generated before timing.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank decodes
+its own contiguous shard of codewords (first codeword = rank * batch) with no
+data-path collective ("scaling": "weak"); only the timing (max over ranks)
+and the 3 error counters are reduced after the timed region.
+
+Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--code", default="dvbs2_r1_2")
+    ap.add_argument("--batch", type=int, default=4096, help="codewords per GPU")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--ebn0", type=float, default=1.0, help="Eb/N0 (dB) of the synthetic channel")
+    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 generic, 2 windowed")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def hbm_peak_gbs():
+    # MI355X HBM3E peak (MI355X_MICROARCH.md "Chip-level parameters": 8.0 TB/s spec)
+    return 8000.0
+
+
+def cpu_baseline(code_name, iters, budget_s, threads, seed):
+    """Time the reference's own SSE decoder (oracle/_ref, kind "reference")
+    or, if it was not built, the oracle port, on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    from ldpcgputegra_amd import channel, load_table
+    t = load_table(code_name)
+    table = channel.i8_table(channel.sigma_from_ebn0(1.0, t.k_info / t.n))
+    kind = "reference" if O.ref_available(code_name) else "port"
+    blk = 16 * threads                     # one 16-frame decode() call per thread per round
+    llr = channel.awgn_i8_host(t.n, blk, seed, table)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        if kind == "reference":
+            O.ref_decode_mt(code_name, llr, iters, 1, threads)
+        else:
+            O.decode_i8_mt(t, llr, iters, 1, threads)
+        done += blk
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    mbps = done * t.n / el / 1e6
+    return dict(value=round(mbps, 3), unit="Mbit/s", cores=threads, kind=kind,
+                sample="%s %d it int8 OMS offset 1: %d codewords (%d threads x 16-frame decode() calls) in %.2f s"
+                       % (code_name, iters, done, threads, el))
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    from ldpcgputegra_amd import Code, Decoder, channel, default_params
+    code = Code(a.code)
+    dec = Decoder(code, device=local, max_batch=a.batch, kernel=a.kernel)
+    B, N = a.batch, code.n
+    sigma = channel.sigma_from_ebn0(a.ebn0, code.k_info / code.n)
+    table = channel.i8_table(sigma, 8, 31)
+    llr = torch.empty((B, N), dtype=torch.int8, device="cuda")
+    hard = torch.empty((B, N), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    dec.awgn_i8_device(llr, first_cw=rank * B, seed=a.seed, table=table, stream=stream)
+    params = default_params()
+
+    def step():
+        dec.decode_i8_device(llr, hard, a.iters, params=params, stream=stream)
+        dec.count_errors_device(hard, code.k_info, counts, stream=stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    counts.zero_()
+    dec.profile(True)
+    dec.kernel_time(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kms, launches = dec.kernel_time(reset=True)
+    dec.profile(False)
+
+    stats = torch.tensor([el, kms / max(launches, 1)], dtype=torch.float64, device="cuda")
+    cnt = counts.clone()
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    el, kernel_ms = stats.tolist()
+    be, fe = cnt.tolist()
+
+    if rank == 0:
+        frames = world * B * a.steps
+        value = frames * N / el / 1e6
+        E = code.e
+        alg_bytes = B * (4.0 * E * a.iters + 2.0 * N)     # SURVEY.md 8(d), per launch
+        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9     # GB/s
+        peak = hbm_peak_gbs()
+        traffic = None
+        try:
+            tr = json.load(open(a.traffic_file))
+            key = "%s_b%d_it%d_k%d" % (a.code, B, a.iters, dec.kernel)
+            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        out = {
+            "metric": "decoded Mbit/s + BER@SNR, DVB-S2 N=64800 r=1/2, 50 iters, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "Mbit/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8",
+            "data": "synthetic (device AWGN generator, all-zero codeword, Eb/N0 %.2f dB)" % a.ebn0,
+            "config": {
+                "workload": "DVB-S2 N=64800 r=1/2 layered int8 offset-min-sum (offset 1), %d iters, batch %d "
+                            "codewords per GPU" % (a.iters, B),
+                "code": a.code, "batch_per_gpu": B, "global_batch": B * world, "iters": a.iters,
+                "ebn0_db": a.ebn0, "kernel": ["auto", "generic", "windowed"][a.kernel],
+                "parallelism": "codeword shards x%d (no collective)" % world,
+            },
+            "ber": be / max(frames * code.k_info, 1),
+            "fer": fe / max(frames, 1),
+            "info_mbps": round(value * code.k_info / N, 3),
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 2), "peak": peak, "unit": "GB/s",
+                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": alg_bytes,
+            },
+        }
+        if world == 1 and a.cpu_seconds > 0:
+            thr = a.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(a.code, a.iters, a.cpu_seconds, thr, a.seed)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,171 @@
+/*
+ * ldpc_mi355x.h -- C-ABI of the MI355X layered min-sum LDPC decoder.
+ *
+ * This is the drop-in boundary for the reference's decode path
+ * (boiseHPSim/ldpcGpuTegra).  Plain C types only: no HIP or torch types in any
+ * signature (streams are passed as `void *` holding a hipStream_t).  Every
+ * function returns an int status (LDPC_OK == 0, negative on error) and never
+ * exits the process -- unlike the reference, which prints and calls exit(0)
+ * (code/x86/CDecoder/DecoderLibrary.h:37-41, code/gpu_fixed/custom_api/
+ * custom_cuda.cu:5-17).
+ *
+ * Entry point -> reference interface it replaces:
+ *   ldpc_code_create / ldpc_code_load / ldpc_code_from_dvbs2_table
+ *       -> the compile-time H table PosNoeudsVariable[] + DEG_k macros
+ *          (code/x86/Constantes/constantes_sse.h:1-2,
+ *           code/x86/Constantes/64800x32400.dvb-s2/constantes_sse.h:6-36)
+ *   ldpc_ctx_create(code, device, max_batch)
+ *       -> CGPUDecoder(nb_frames, n, k, m) + initialize()
+ *          (code/gpu_fixed/decoder_template/CGPUDecoder.h:20-37) and the
+ *          decoder constructors that allocate V / msg scratch
+ *          (code/x86/CDecoder/template/CDecoder_fixed_SSE.cpp:23-27)
+ *   ldpc_params {algo, offset, factor, var/msg range}
+ *       -> CreateDecoder(type, arch, format, p_decoder, vMin, vMax, mMin, mMax)
+ *          (code/x86/CDecoder/DecoderLibrary.h:44-134), setOffset
+ *          (OMS/CDecoder_OMS_fixed_SSE.cpp:104-112), setFactor
+ *          (NMS/CDecoder_NMS_fixed_SSE.cpp:107-111), setVarRange/setMsgRange
+ *          (template/CDecoder_fixed.h:40-41)
+ *   ldpc_decode_i8(ctx, llr, hard, batch, n_iter, params)
+ *       -> CDecoder::decode(char var_nodes[], char Rprime_fix[], int iters)
+ *          (code/x86/CDecoder/template/CDecoder.h:37), 16 frames per call
+ *          there, any batch here; same frame-major layout, same 0/1 output
+ *   ldpc_decode_f32(...)
+ *       -> CDecoder::decode(float var_nodes[], char Rprime_fix[], int)
+ *          (CDecoder.h:38; a no-op for the reference's fixed-point decoders)
+ *          and CGPUDecoder::decode(float[], int[], int) (CGPUDecoder.h:31)
+ *   ldpc_decode_i8_async / _f32_async
+ *       -> CGPU_Decoder_*_SIMD::decode_stream
+ *          (code/gpu_fixed/decoder_ms/CGPU_Decoder_MS_SIMD.cu:219-275),
+ *          device pointers, caller-owned stream, no hidden sync
+ *   ldpc_awgn_*  -> CChanelAWGN_MKL::configure/generate + CFastFixConversion
+ *          (code/x86/CChanel/CChanelAWGN_MKL.cpp:95-143,
+ *           code/x86/CFixPointConversion/CFastFixConversion.cpp:55-65) and the
+ *          on-GPU channel (code/gpu_fixed/awgn_channel/CChanel_AWGN_SIMD.cu:7-30)
+ *   ldpc_count_errors_async -> CErrorAnalyzer::generate
+ *          (code/x86/CErrorAnalyzer/CErrorAnalyzer.cpp:123-154)
+ *
+ * Threading: a ldpc_code is immutable and may be shared by any number of
+ * contexts/threads.  A ldpc_ctx owns device scratch and is not re-entrant
+ * (like the reference decoder objects); use one per host thread / stream.
+ */
+#ifndef LDPC_MI355X_H
+#define LDPC_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDPC_ABI_VERSION 1
+
+enum {
+    LDPC_OK = 0,
+    LDPC_EINVAL = -1,      /* bad argument, H table, or saturation ranges */
+    LDPC_EUNSUPPORTED = -2,/* valid request the reference would reject (exit) */
+    LDPC_EDEVICE = -3,     /* HIP error; see ldpc_last_error() */
+    LDPC_ENOMEM = -4,      /* host or device allocation failed */
+    LDPC_EIO = -5          /* file not found / malformed table file */
+};
+
+enum {
+    LDPC_ALGO_OMS = 0,     /* offset min-sum   (CDecoder_OMS_fixed_SSE) */
+    LDPC_ALGO_NMS = 1,     /* normalised min-sum (CDecoder_NMS_fixed_SSE) */
+    LDPC_ALGO_MS = 2       /* plain min-sum == OMS with offset 0 */
+};
+
+typedef struct ldpc_code ldpc_code;
+typedef struct ldpc_ctx ldpc_ctx;
+
+typedef struct {
+    int algo;        /* LDPC_ALGO_*                                  default OMS */
+    int offset;      /* int8 OMS offset (setOffset)                  default 1   */
+    int factor;      /* int8 NMS factor, scaled by 1/32 (setFactor)  default 29  */
+    float beta;      /* float path: OMS offset or NMS factor         default 0.15*/
+    int var_min;     /* setVarRange(min, max)                   default -127,127 */
+    int var_max;
+    int msg_min;     /* setMsgRange(min, max)                   default -31, 31  */
+    int msg_max;
+    int early_term;  /* stop a codeword once H*x == 0 (0 = exact n_iter) */
+} ldpc_params;
+
+/* ---- errors / version ------------------------------------------------ */
+void ldpc_params_default(ldpc_params *p);
+const char *ldpc_strerror(int status);
+const char *ldpc_last_error(void);          /* thread-local detail of the last error */
+int ldpc_abi_version(void);
+int ldpc_device_count(int *count);
+
+/* ---- code tables ----------------------------------------------------- */
+/* Layered H: checks in schedule order, in n_groups runs of equal degree
+ * (group g = group_cnt[g] checks of degree group_deg[g]); edge_var[E] lists
+ * each check's variables.  Group 0 vs later groups matters for bit-exactness
+ * (reference quirk). */
+int ldpc_code_create(int n, int m, int n_groups, const int *group_deg, const int *group_cnt,
+                     const uint32_t *edge_var, ldpc_code **out);
+/* DVB-S2 IRA code from its Annex-B address table: row r lists row_len[r]
+ * parity addresses (concatenated in row_addr).  Layered order as the
+ * reference tables: checks 1..M-1 (info vars ascending, K+i-1, K+i), then
+ * check 0 (info ascending, K). */
+int ldpc_code_from_dvbs2_table(int n, int k_info, int n_rows, const int *row_len,
+                               const int *row_addr, ldpc_code **out);
+/* Load a ".ldpc" binary table or a DVB-S2 ".txt" address table. */
+int ldpc_code_load(const char *path, ldpc_code **out);
+int ldpc_code_info(const ldpc_code *h, int *n, int *m, int *e, int *n_groups, int *max_deg);
+int ldpc_code_edges(const ldpc_code *h, uint32_t *edge_var, int *group_deg, int *group_cnt);
+/* 1 if the layered schedule has the DVB-S2 staircase chain (fast kernel). */
+int ldpc_code_plan_info(const ldpc_code *h, int *staircase, int *n_windows, int *min_hazard);
+void ldpc_code_destroy(ldpc_code *h);
+
+/* ---- decoder context --------------------------------------------------- */
+int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ldpc_ctx **out);
+void ldpc_ctx_destroy(ldpc_ctx *ctx);
+int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
+/* Select kernel family: 0 = auto, 1 = generic (per-edge messages),
+ * 2 = windowed layered kernel (compressed messages). */
+int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
+int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
+/* Kernel timing (bench / profiling): when enabled, every decode records HIP
+ * events around the decode kernel on the stream it is launched on;
+ * ldpc_ctx_kernel_time returns the summed kernel time and launch count since
+ * the last reset (it waits for the recorded events). */
+int ldpc_ctx_profile(ldpc_ctx *ctx, int enable);
+int ldpc_ctx_kernel_time(ldpc_ctx *ctx, double *total_ms, int *launches, int reset);
+
+/* Host buffers, synchronous, frame-major [batch][N]; hard = (V > 0). */
+int ldpc_decode_i8(ldpc_ctx *ctx, const int8_t *llr, uint8_t *hard, int batch, int n_iter,
+                   const ldpc_params *p);
+int ldpc_decode_f32(ldpc_ctx *ctx, const float *llr, uint8_t *hard, int batch, int n_iter,
+                    const ldpc_params *p);
+
+/* Device buffers, asynchronous on `hip_stream` (NULL = the context stream).
+ * soft (optional): final V per bit; iters_used (optional): per codeword. */
+int ldpc_decode_i8_async(ldpc_ctx *ctx, void *hip_stream, const int8_t *d_llr, uint8_t *d_hard,
+                         int8_t *d_soft, int32_t *d_iters_used, int batch, int n_iter,
+                         const ldpc_params *p);
+int ldpc_decode_f32_async(ldpc_ctx *ctx, void *hip_stream, const float *d_llr, uint8_t *d_hard,
+                          float *d_soft, int32_t *d_iters_used, int batch, int n_iter,
+                          const ldpc_params *p);
+
+/* ---- synthetic channel -------------------------------------------------- */
+/* sigma = sqrt(10^(-(EbN0 + 10 log10(rate))/10) / 2)  (CChanelAWGN_MKL.cpp:102-105) */
+double ldpc_awgn_sigma(double ebn0_db, double rate);
+/* Threshold table (63 entries) for the integer-exact quantised AWGN generator:
+ * q = clamp(trunc(factor*y), -sat, sat), y = -1 + sigma*z (bit 0). */
+int ldpc_awgn_i8_table(double sigma, int factor, int sat, uint32_t *table /*[64]*/);
+/* llr[b][i] for codewords first_cw .. first_cw+batch-1; codeword bits
+ * (0/1, [batch][N]) or NULL for the all-zero codeword. */
+int ldpc_awgn_i8_host(int n, int batch, uint64_t first_cw, uint64_t seed, const uint32_t *table,
+                      const uint8_t *codeword, int8_t *llr);
+int ldpc_awgn_i8_async(ldpc_ctx *ctx, void *hip_stream, int8_t *d_llr, int batch,
+                       uint64_t first_cw, uint64_t seed, const uint32_t *table,
+                       const uint8_t *d_codeword);
+/* Count bit errors over the first k positions of each codeword vs d_ref
+ * (NULL = all-zero); d_counts[0] += bit errors, d_counts[1] += frame errors. */
+int ldpc_count_errors_async(ldpc_ctx *ctx, void *hip_stream, const uint8_t *d_hard, int batch,
+                           int k, const uint8_t *d_ref, unsigned long long *d_counts);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDPC_MI355X_H */

@@ -1,0 +1,106 @@
+"""ctypes binding of the C-ABI in include/ldpc_mi355x.h.
+
+The shared library is built in-tree (``ldpcgputegra_amd/libldpc_mi355x.so``,
+see ``__graft_entry__.build``).  There is no fallback: if the library is
+missing, importing the decoder raises -- the product path never silently
+drops to a CPU implementation.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libldpc_mi355x.so")
+
+LDPC_OK, LDPC_EINVAL, LDPC_EUNSUPPORTED, LDPC_EDEVICE, LDPC_ENOMEM, LDPC_EIO = 0, -1, -2, -3, -4, -5
+ALGO_OMS, ALGO_NMS, ALGO_MS = 0, 1, 2
+
+
+class LdpcError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__("%s (%d): %s" % (_strerror(status), status, msg))
+        self.status = status
+
+
+class ldpc_params(C.Structure):
+    _fields_ = [
+        ("algo", C.c_int), ("offset", C.c_int), ("factor", C.c_int), ("beta", C.c_float),
+        ("var_min", C.c_int), ("var_max", C.c_int), ("msg_min", C.c_int), ("msg_max", C.c_int),
+        ("early_term", C.c_int),
+    ]
+
+
+# name -> (restype, argtypes); every exported symbol of include/ldpc_mi355x.h
+P = C.c_void_p
+I = C.c_int
+U64 = C.c_uint64
+SIGNATURES = {
+    "ldpc_params_default": (None, [C.POINTER(ldpc_params)]),
+    "ldpc_strerror": (C.c_char_p, [I]),
+    "ldpc_last_error": (C.c_char_p, []),
+    "ldpc_abi_version": (I, []),
+    "ldpc_device_count": (I, [C.POINTER(I)]),
+    "ldpc_code_create": (I, [I, I, I, P, P, P, C.POINTER(P)]),
+    "ldpc_code_from_dvbs2_table": (I, [I, I, I, P, P, C.POINTER(P)]),
+    "ldpc_code_load": (I, [C.c_char_p, C.POINTER(P)]),
+    "ldpc_code_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "ldpc_code_edges": (I, [P, P, P, P]),
+    "ldpc_code_plan_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "ldpc_code_destroy": (None, [P]),
+    "ldpc_ctx_create": (I, [P, I, I, C.POINTER(P)]),
+    "ldpc_ctx_destroy": (None, [P]),
+    "ldpc_ctx_stream": (I, [P, C.POINTER(P)]),
+    "ldpc_ctx_set_kernel": (I, [P, I]),
+    "ldpc_ctx_get_kernel": (I, [P, C.POINTER(I)]),
+    "ldpc_ctx_profile": (I, [P, I]),
+    "ldpc_ctx_kernel_time": (I, [P, C.POINTER(C.c_double), C.POINTER(I), I]),
+    "ldpc_decode_i8": (I, [P, P, P, I, I, C.POINTER(ldpc_params)]),
+    "ldpc_decode_f32": (I, [P, P, P, I, I, C.POINTER(ldpc_params)]),
+    "ldpc_decode_i8_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params)]),
+    "ldpc_decode_f32_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params)]),
+    "ldpc_awgn_sigma": (C.c_double, [C.c_double, C.c_double]),
+    "ldpc_awgn_i8_table": (I, [C.c_double, I, I, P]),
+    "ldpc_awgn_i8_host": (I, [I, I, U64, U64, P, P, P]),
+    "ldpc_awgn_i8_async": (I, [P, P, P, I, U64, U64, P, P]),
+    "ldpc_count_errors_async": (I, [P, P, P, I, I, P, P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libldpc_mi355x.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libldpc_mi355x.so not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
+                              " (expected at %s)" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _strerror(status):
+    try:
+        return lib().ldpc_strerror(status).decode()
+    except Exception:  # pragma: no cover
+        return "error"
+
+
+def check(status):
+    if status != LDPC_OK:
+        raise LdpcError(status, lib().ldpc_last_error().decode())
+    return status
+
+
+def default_params(**kw):
+    p = ldpc_params()
+    lib().ldpc_params_default(C.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise TypeError("unknown ldpc_params field %r" % k)
+        setattr(p, k, v)
+    return p

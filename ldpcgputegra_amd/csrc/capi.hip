@@ -1,0 +1,351 @@
+// capi.hip -- the C-ABI decoder context and decode entry points
+// (include/ldpc_mi355x.h).  Host code only; kernels live in generic.hip,
+// windowed.hip and layout.hip.
+//
+// A context mirrors the reference decoder objects: it owns the device scratch
+// (V and messages, allocated up front for max_batch codewords, as
+// CDecoder_fixed_SSE's constructor does, code/x86/CDecoder/template/
+// CDecoder_fixed_SSE.cpp:23-27, and CGPUDecoder(nb_frames, n, k, m),
+// code/gpu_fixed/decoder_template/CGPUDecoder.cpp:14-38) plus its own HIP
+// stream -- created once, not per call as the reference's decode_stream does
+// (code/gpu_fixed/decoder_ms/CGPU_Decoder_MS_SIMD.cu:223-224).
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+#include "kernels.h"
+#include "ldpc_internal.h"
+#include "windowed.h"
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return ldpc_set_error(LDPC_EDEVICE, "%s: %s", #expr, hipGetErrorString(_e));       \
+    } while (0)
+
+struct ldpc_ctx {
+    const ldpc_code *code = nullptr;
+    int device = 0;
+    int max_batch = 0;
+    int max_stride = 0;
+    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed
+    hipStream_t stream = nullptr;
+    // device copy of the code
+    uint32_t *d_edge_var = nullptr;
+    int *d_group_deg = nullptr, *d_group_cnt = nullptr;
+    WindowedCode wcode{};           // windowed-kernel tables (windowed.hip)
+    // scratch (lazily sized)
+    void *d_V = nullptr;
+    size_t V_bytes = 0;
+    void *d_msg = nullptr;
+    size_t msg_bytes = 0;
+    void *d_io = nullptr;           // staging for the host-buffer API
+    size_t io_bytes = 0;
+    // kernel timing (ldpc_ctx_profile)
+    bool profile = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+};
+
+static int ensure(void **p, size_t *have, size_t need)
+{
+    if (*have >= need) return LDPC_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    hipError_t e = hipMalloc(p, need);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return ldpc_set_error(LDPC_ENOMEM, "hipMalloc(%zu): %s", need, hipGetErrorString(e));
+    }
+    *have = need;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_device_count(int *count)
+{
+    if (!count) return ldpc_set_error(LDPC_EINVAL, "count is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *count = (e == hipSuccess) ? c : 0;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ldpc_ctx **out)
+{
+    if (!out) return ldpc_set_error(LDPC_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (!h || max_batch <= 0) return ldpc_set_error(LDPC_EINVAL, "NULL code or max_batch <= 0");
+    if (h->max_deg > 32) return ldpc_set_error(LDPC_EUNSUPPORTED, "check degree %d > 32", h->max_deg);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return ldpc_set_error(LDPC_EDEVICE, "no HIP device visible");
+    if (device < 0 || device >= ndev) return ldpc_set_error(LDPC_EINVAL, "device %d of %d", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+    auto *c = new ldpc_ctx();
+    c->code = h;
+    c->device = device;
+    c->max_batch = max_batch;
+    c->max_stride = (max_batch + 63) / 64 * 64;
+    int rc = LDPC_OK;
+    auto fail = [&](int r) {
+        ldpc_ctx_destroy(c);
+        return r;
+    };
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(ldpc_set_error(LDPC_EDEVICE, "hipStreamCreate"));
+    if (hipMalloc(&c->d_edge_var, 4ull * h->e) != hipSuccess ||
+        hipMalloc(&c->d_group_deg, sizeof(int) * h->n_groups) != hipSuccess ||
+        hipMalloc(&c->d_group_cnt, sizeof(int) * h->n_groups) != hipSuccess)
+        return fail(ldpc_set_error(LDPC_ENOMEM, "code tables"));
+    if (hipMemcpy(c->d_edge_var, h->edge_var.data(), 4ull * h->e, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_group_deg, h->group_deg.data(), sizeof(int) * h->n_groups, hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMemcpy(c->d_group_cnt, h->group_cnt.data(), sizeof(int) * h->n_groups, hipMemcpyHostToDevice) !=
+            hipSuccess)
+        return fail(ldpc_set_error(LDPC_EDEVICE, "code table upload"));
+    if ((rc = windowed_code_upload(h, &c->wcode)) != LDPC_OK) return fail(rc);
+    *out = c;
+    return LDPC_OK;
+}
+
+extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    windowed_code_free(&c->wcode);
+    for (auto &pr : c->events) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    (void)hipFree(c->d_edge_var);
+    (void)hipFree(c->d_group_deg);
+    (void)hipFree(c->d_group_cnt);
+    (void)hipFree(c->d_V);
+    (void)hipFree(c->d_msg);
+    (void)hipFree(c->d_io);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
+{
+    if (!c || !s) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/stream");
+    *s = (void *)c->stream;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
+{
+    if (!c || k < 0 || k > 2) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto), 1, 2");
+    if (k == 2 && !windowed_supported(c->code))
+        return ldpc_set_error(LDPC_EUNSUPPORTED, "windowed kernel cannot schedule this code");
+    c->kernel = k;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_ctx_profile(ldpc_ctx *c, int enable)
+{
+    if (!c) return ldpc_set_error(LDPC_EINVAL, "NULL ctx");
+    c->profile = enable != 0;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_ctx_kernel_time(ldpc_ctx *c, double *total_ms, int *launches, int reset)
+{
+    if (!c) return ldpc_set_error(LDPC_EINVAL, "NULL ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    double tot = 0.0;
+    for (auto &pr : c->events) {
+        HIP_TRY(hipEventSynchronize(pr.second));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+        tot += ms;
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = (int)c->events.size();
+    if (reset) {
+        for (auto &pr : c->events) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+        c->events.clear();
+    }
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_ctx_get_kernel(ldpc_ctx *c, int *k)
+{
+    if (!c || !k) return ldpc_set_error(LDPC_EINVAL, "NULL");
+    *k = c->kernel;
+    return LDPC_OK;
+}
+
+static int check_params(const ldpc_ctx *c, int batch, int n_iter, const ldpc_params *p, bool is_float)
+{
+    if (batch < 0 || batch > c->max_batch)
+        return ldpc_set_error(LDPC_EINVAL, "batch %d outside [0, max_batch=%d]", batch, c->max_batch);
+    if (n_iter < 0) return ldpc_set_error(LDPC_EINVAL, "n_iter < 0");
+    if (!p) return ldpc_set_error(LDPC_EINVAL, "params NULL");
+    if (p->algo < 0 || p->algo > 2) return ldpc_set_error(LDPC_EINVAL, "algo %d", p->algo);
+    if (!is_float) {
+        // CDecoder_OMS_fixed_SSE::decode / CDecoder_NMS_fixed_SSE::decode exit
+        // unless vSAT_POS_VAR == 127 (OMS .cpp:116-119, NMS .cpp:119-122)
+        if (p->var_max != 127)
+            return ldpc_set_error(LDPC_EUNSUPPORTED, "var_max must be 127 (reference decode_8bits only)");
+        if (p->var_min < -128 || p->var_min > 0) return ldpc_set_error(LDPC_EINVAL, "var_min %d", p->var_min);
+        if (p->msg_max < 0 || p->msg_max > 127) return ldpc_set_error(LDPC_EINVAL, "msg_max %d", p->msg_max);
+        if (p->algo == LDPC_ALGO_OMS && (p->offset < 0 || p->offset > 255))
+            return ldpc_set_error(LDPC_EINVAL, "offset %d", p->offset);
+    }
+    return LDPC_OK;
+}
+
+static bool use_windowed(const ldpc_ctx *c, const ldpc_params *p, bool is_float)
+{
+    if (c->kernel == 1) return false;
+    if (is_float || !windowed_supported(c->code)) return false;
+    if (!windowed_params_ok(p)) return false;
+    return true;   // kernel 0 (auto) or 2
+}
+
+static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t *d_hard, void *d_soft,
+                         int32_t *d_iters, int batch, int n_iter, const ldpc_params *p, bool is_float)
+{
+    int rc = check_params(c, batch, n_iter, p, is_float);
+    if (rc != LDPC_OK) return rc;
+    if (batch == 0) return LDPC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    if (!s) s = c->stream;
+    const ldpc_code *h = c->code;
+    const int stride = (batch + 63) / 64 * 64;
+    const size_t esz = is_float ? 4 : 1;
+    const bool win = use_windowed(c, p, is_float);
+    if (c->kernel == 2 && !win)
+        return ldpc_set_error(LDPC_EUNSUPPORTED, "windowed kernel selected but not applicable to these params");
+    const size_t msg_need = win ? windowed_msg_bytes(h, stride) : (size_t)h->e * stride * esz;
+    if ((rc = ensure(&c->d_V, &c->V_bytes, (size_t)h->n * stride * esz)) != LDPC_OK) return rc;
+    if ((rc = ensure(&c->d_msg, &c->msg_bytes, msg_need)) != LDPC_OK) return rc;
+    // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
+    // compressed word is the all-zero message set as well.
+    HIP_TRY(hipMemsetAsync(c->d_msg, 0, msg_need, s));
+    if (is_float) {
+        if (launch_interleave_f32((const float *)d_llr, (float *)c->d_V, h->n, batch, stride, s))
+            return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
+    } else {
+        if (launch_interleave_i8((const int8_t *)d_llr, (int8_t *)c->d_V, h->n, batch, stride, s))
+            return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
+    }
+    DecodeLaunch L{};
+    L.V = c->d_V;
+    L.msg = c->d_msg;
+    L.stride = stride;
+    L.batch = batch;
+    L.iters = n_iter;
+    L.is_float = is_float;
+    L.d_edge_var = c->d_edge_var;
+    L.d_group_deg = c->d_group_deg;
+    L.d_group_cnt = c->d_group_cnt;
+    L.n_groups = h->n_groups;
+    L.n = h->n;
+    L.m = h->m;
+    L.e = h->e;
+    L.algo = (p->algo == LDPC_ALGO_MS) ? LDPC_ALGO_OMS : p->algo;
+    L.param = (p->algo == LDPC_ALGO_NMS) ? p->factor : (p->algo == LDPC_ALGO_MS ? 0 : p->offset);
+    L.var_min = p->var_min;
+    L.msg_max = p->msg_max;
+    L.early = p->early_term;
+    L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
+    L.iters_used = d_iters;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (c->profile) {
+        HIP_TRY(hipEventCreate(&ev0));
+        HIP_TRY(hipEventCreate(&ev1));
+        HIP_TRY(hipEventRecord(ev0, s));
+    }
+    int lr = win ? launch_windowed(L, c->wcode, s) : launch_generic(L, s);
+    if (c->profile) {
+        HIP_TRY(hipEventRecord(ev1, s));
+        c->events.emplace_back(ev0, ev1);
+    }
+    if (lr) return ldpc_set_error(LDPC_EDEVICE, "decode launch: %s", hipGetErrorString(hipGetLastError()));
+    if (d_hard || d_soft) {
+        int r2 = is_float ? launch_deinterleave_f32((const float *)c->d_V, d_hard, (float *)d_soft, h->n, batch,
+                                                    stride, s)
+                          : launch_deinterleave_i8((const int8_t *)c->d_V, d_hard, (int8_t *)d_soft, h->n,
+                                                   batch, stride, s);
+        if (r2) return ldpc_set_error(LDPC_EDEVICE, "deinterleave: %s", hipGetErrorString(hipGetLastError()));
+    }
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_decode_i8_async(ldpc_ctx *c, void *s, const int8_t *d_llr, uint8_t *d_hard, int8_t *d_soft,
+                                    int32_t *d_iters, int batch, int n_iter, const ldpc_params *p)
+{
+    if (!c || (!d_llr && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr");
+    return decode_device(c, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, false);
+}
+
+extern "C" int ldpc_decode_f32_async(ldpc_ctx *c, void *s, const float *d_llr, uint8_t *d_hard, float *d_soft,
+                                     int32_t *d_iters, int batch, int n_iter, const ldpc_params *p)
+{
+    if (!c || (!d_llr && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr");
+    return decode_device(c, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, true);
+}
+
+static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, int n_iter, const ldpc_params *p,
+                       bool is_float)
+{
+    if (!c || ((!llr || !hard) && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr/hard");
+    int rc = check_params(c, batch, n_iter, p, is_float);
+    if (rc != LDPC_OK || batch == 0) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t in_bytes = (size_t)batch * c->code->n * (is_float ? 4 : 1);
+    const size_t out_bytes = (size_t)batch * c->code->n;
+    const size_t in_al = (in_bytes + 255) / 256 * 256;
+    if ((rc = ensure(&c->d_io, &c->io_bytes, in_al + out_bytes)) != LDPC_OK) return rc;
+    char *d_in = (char *)c->d_io, *d_out = d_in + in_al;
+    HIP_TRY(hipMemcpyAsync(d_in, llr, in_bytes, hipMemcpyHostToDevice, c->stream));
+    rc = decode_device(c, c->stream, d_in, (uint8_t *)d_out, nullptr, nullptr, batch, n_iter, p, is_float);
+    if (rc != LDPC_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(hard, d_out, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_decode_i8(ldpc_ctx *c, const int8_t *llr, uint8_t *hard, int batch, int n_iter,
+                              const ldpc_params *p)
+{
+    return decode_host(c, llr, hard, batch, n_iter, p, false);
+}
+
+extern "C" int ldpc_decode_f32(ldpc_ctx *c, const float *llr, uint8_t *hard, int batch, int n_iter,
+                               const ldpc_params *p)
+{
+    return decode_host(c, llr, hard, batch, n_iter, p, true);
+}
+
+extern "C" int ldpc_awgn_i8_async(ldpc_ctx *c, void *s, int8_t *d_llr, int batch, uint64_t first_cw, uint64_t seed,
+                                  const uint32_t *table, const uint8_t *d_codeword)
+{
+    if (!c || !d_llr || !table || batch < 0) return ldpc_set_error(LDPC_EINVAL, "awgn args");
+    if (table[63] < 1 || table[63] > 31) return ldpc_set_error(LDPC_EINVAL, "awgn table sat");
+    HIP_TRY(hipSetDevice(c->device));
+    AwgnTable t;
+    memcpy(t.t, table, sizeof(t.t));
+    if (launch_awgn_i8(d_llr, c->code->n, batch, first_cw, seed, t, d_codeword, s ? (hipStream_t)s : c->stream))
+        return ldpc_set_error(LDPC_EDEVICE, "awgn: %s", hipGetErrorString(hipGetLastError()));
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_count_errors_async(ldpc_ctx *c, void *s, const uint8_t *d_hard, int batch, int k,
+                                       const uint8_t *d_ref, unsigned long long *d_counts)
+{
+    if (!c || !d_hard || !d_counts || batch < 0 || k < 0 || k > c->code->n)
+        return ldpc_set_error(LDPC_EINVAL, "count_errors args");
+    HIP_TRY(hipSetDevice(c->device));
+    if (launch_count_errors(d_hard, c->code->n, batch, k, d_ref, d_counts, s ? (hipStream_t)s : c->stream))
+        return ldpc_set_error(LDPC_EDEVICE, "count_errors: %s", hipGetErrorString(hipGetLastError()));
+    return LDPC_OK;
+}

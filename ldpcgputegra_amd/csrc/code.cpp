@@ -1,0 +1,333 @@
+// code.cpp -- runtime H tables (replaces the reference's compile-time
+// PosNoeudsVariable[] headers, code/x86/Constantes/*/constantes_sse.h), table
+// loaders, the DVB-S2 Annex-B builder, error reporting and the host side of
+// the synthetic channel.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+#include "ldpc_internal.h"
+
+// ---------------------------------------------------------------- errors
+static thread_local std::string g_last_error;
+
+int ldpc_set_error(int status, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return status;
+}
+
+extern "C" const char *ldpc_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" const char *ldpc_strerror(int status)
+{
+    switch (status) {
+    case LDPC_OK: return "ok";
+    case LDPC_EINVAL: return "invalid argument";
+    case LDPC_EUNSUPPORTED: return "unsupported configuration";
+    case LDPC_EDEVICE: return "device (HIP) error";
+    case LDPC_ENOMEM: return "out of memory";
+    case LDPC_EIO: return "I/O or table format error";
+    default: return "unknown error";
+    }
+}
+
+extern "C" int ldpc_abi_version(void) { return LDPC_ABI_VERSION; }
+
+extern "C" void ldpc_params_default(ldpc_params *p)
+{
+    if (!p) return;
+    // defaults of code/x86/main_p.cpp:90-104,133-141 (offset 1, factor 29,
+    // VAR +-127, MSG +-31; float OMS offset 0.15)
+    p->algo = LDPC_ALGO_OMS;
+    p->offset = 1;
+    p->factor = 29;
+    p->beta = 0.15f;
+    p->var_min = -127;
+    p->var_max = 127;
+    p->msg_min = -31;
+    p->msg_max = 31;
+    p->early_term = 0;
+}
+
+// ---------------------------------------------------------------- codes
+int ldpc_code_finalize(ldpc_code *h)
+{
+    h->check_deg.clear();
+    h->check_start.clear();
+    h->check_group.clear();
+    h->max_deg = 0;
+    int start = 0;
+    for (int g = 0; g < h->n_groups; g++) {
+        for (int i = 0; i < h->group_cnt[g]; i++) {
+            h->check_deg.push_back(h->group_deg[g]);
+            h->check_start.push_back(start);
+            h->check_group.push_back(g);
+            start += h->group_deg[g];
+        }
+        h->max_deg = std::max(h->max_deg, h->group_deg[g]);
+    }
+    if (start != h->e || (int)h->check_deg.size() != h->m)
+        return ldpc_set_error(LDPC_EINVAL, "group table sums to %d edges / %zu checks, expected %d / %d",
+                              start, h->check_deg.size(), h->e, h->m);
+    for (int c = 0; c < h->m; c++) {
+        const uint32_t *ev = &h->edge_var[h->check_start[c]];
+        for (int j = 0; j < h->check_deg[c]; j++)
+            for (int k = 0; k < j; k++)
+                if (ev[j] == ev[k])
+                    return ldpc_set_error(LDPC_EINVAL, "check %d lists variable %u twice", c, ev[j]);
+    }
+    extern int ldpc_plan_build(ldpc_code * h);
+    return ldpc_plan_build(h);
+}
+
+extern "C" int ldpc_code_create(int n, int m, int n_groups, const int *group_deg, const int *group_cnt,
+                                const uint32_t *edge_var, ldpc_code **out)
+{
+    if (!out) return ldpc_set_error(LDPC_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (n <= 0 || m <= 0 || n_groups <= 0 || !group_deg || !group_cnt || !edge_var)
+        return ldpc_set_error(LDPC_EINVAL, "bad code dimensions / NULL table");
+    long e = 0, mm = 0;
+    for (int g = 0; g < n_groups; g++) {
+        if (group_deg[g] < 2 || group_deg[g] > 64 || group_cnt[g] <= 0)
+            return ldpc_set_error(LDPC_EUNSUPPORTED, "group %d: degree %d count %d (degree must be 2..64)",
+                                  g, group_deg[g], group_cnt[g]);
+        e += (long)group_deg[g] * group_cnt[g];
+        mm += group_cnt[g];
+    }
+    if (mm != m) return ldpc_set_error(LDPC_EINVAL, "groups hold %ld checks, m = %d", mm, m);
+    for (long i = 0; i < e; i++)
+        if (edge_var[i] >= (uint32_t)n)
+            return ldpc_set_error(LDPC_EINVAL, "edge %ld: variable %u >= n %d", i, edge_var[i], n);
+    auto *h = new (std::nothrow) ldpc_code();
+    if (!h) return ldpc_set_error(LDPC_ENOMEM, "host alloc");
+    h->n = n;
+    h->m = m;
+    h->e = (int)e;
+    h->n_groups = n_groups;
+    h->group_deg.assign(group_deg, group_deg + n_groups);
+    h->group_cnt.assign(group_cnt, group_cnt + n_groups);
+    h->edge_var.assign(edge_var, edge_var + e);
+    int rc = ldpc_code_finalize(h);
+    if (rc != LDPC_OK) {
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return LDPC_OK;
+}
+
+// DVB-S2 IRA structure: check r (0..M-1) is connected to info bit v = 360*g + k
+// when r == (x + k*q) mod M for an address x of row g (ETSI EN 302 307 Annex B;
+// encoder form in code/x86/CEncoder/GenericEncoder.cpp:55-69), plus the parity
+// staircase.  Layered order of the reference tables: checks 1..M-1, then 0.
+extern "C" int ldpc_code_from_dvbs2_table(int n, int k_info, int n_rows, const int *row_len,
+                                          const int *row_addr, ldpc_code **out)
+{
+    if (!out) return ldpc_set_error(LDPC_EINVAL, "out is NULL");
+    *out = nullptr;
+    const int m = n - k_info;
+    if (n <= 0 || k_info <= 0 || m <= 0 || k_info % 360 || m % 360 || n_rows != k_info / 360 || !row_len ||
+        !row_addr)
+        return ldpc_set_error(LDPC_EINVAL, "DVB-S2 table: n=%d k=%d rows=%d (need k/360 rows, 360 | k, m)", n,
+                              k_info, n_rows);
+    const int q = m / 360;
+    std::vector<std::vector<uint32_t>> info(m);
+    const int *a = row_addr;
+    for (int g = 0; g < n_rows; g++) {
+        for (int t = 0; t < row_len[g]; t++)
+            if (a[t] < 0 || a[t] >= m)
+                return ldpc_set_error(LDPC_EINVAL, "row %d: address %d out of range", g, a[t]);
+        for (int k = 0; k < 360; k++)
+            for (int t = 0; t < row_len[g]; t++) info[(a[t] + (long)k * q) % m].push_back(360 * g + k);
+        a += row_len[g];
+    }
+    std::vector<uint32_t> edges;
+    std::vector<int> gdeg, gcnt;
+    for (int idx = 0; idx < m; idx++) {
+        const int r = (idx + 1) % m;   // 1, 2, ..., m-1, 0
+        auto &lst = info[r];
+        std::sort(lst.begin(), lst.end());
+        int d = (int)lst.size();
+        edges.insert(edges.end(), lst.begin(), lst.end());
+        if (r > 0) {
+            edges.push_back(k_info + r - 1);
+            edges.push_back(k_info + r);
+            d += 2;
+        } else {
+            edges.push_back(k_info);
+            d += 1;
+        }
+        if (!gdeg.empty() && gdeg.back() == d)
+            gcnt.back()++;
+        else {
+            gdeg.push_back(d);
+            gcnt.push_back(1);
+        }
+    }
+    return ldpc_code_create(n, m, (int)gdeg.size(), gdeg.data(), gcnt.data(), edges.data(), out);
+}
+
+static int load_ldpc_binary(const std::string &data, ldpc_code **out)
+{
+    auto rd32 = [&](size_t off) {
+        uint32_t v;
+        memcpy(&v, data.data() + off, 4);
+        return v;
+    };
+    if (data.size() < 24 || memcmp(data.data(), "LDPCH001", 8) != 0)
+        return ldpc_set_error(LDPC_EIO, "not a LDPCH001 table");
+    uint32_t n = rd32(8), m = rd32(12), e = rd32(16), ng = rd32(20);
+    if (ng == 0 || ng > 1024 || data.size() != 24 + 8ull * ng + 4ull * e)
+        return ldpc_set_error(LDPC_EIO, "truncated LDPCH001 table");
+    std::vector<int> gd(ng), gc(ng);
+    for (uint32_t g = 0; g < ng; g++) {
+        gd[g] = (int)rd32(24 + 8 * g);
+        gc[g] = (int)rd32(28 + 8 * g);
+    }
+    std::vector<uint32_t> ev(e);
+    memcpy(ev.data(), data.data() + 24 + 8ull * ng, 4ull * e);
+    return ldpc_code_create((int)n, (int)m, (int)ng, gd.data(), gc.data(), ev.data(), out);
+}
+
+static int load_dvbs2_text(const std::string &data, ldpc_code **out)
+{
+    std::istringstream in(data);
+    std::string line;
+    int n = -1, k = -1;
+    std::vector<int> len, addr;
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        if (line[0] == '#') {
+            const char *p = strstr(line.c_str(), "N=");
+            const char *q = strstr(line.c_str(), "K=");
+            if (p && q) {
+                n = atoi(p + 2);
+                k = atoi(q + 2);
+            }
+            continue;
+        }
+        std::istringstream ls(line);
+        int v, c = 0;
+        while (ls >> v) {
+            addr.push_back(v);
+            c++;
+        }
+        if (c) len.push_back(c);
+    }
+    if (n <= 0 || k <= 0) return ldpc_set_error(LDPC_EIO, "DVB-S2 table without '# N=.. K=..' header");
+    return ldpc_code_from_dvbs2_table(n, k, (int)len.size(), len.data(), addr.data(), out);
+}
+
+extern "C" int ldpc_code_load(const char *path, ldpc_code **out)
+{
+    if (!path || !out) return ldpc_set_error(LDPC_EINVAL, "NULL path/out");
+    *out = nullptr;
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return ldpc_set_error(LDPC_EIO, "cannot open %s", path);
+    std::string data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (data.size() >= 8 && memcmp(data.data(), "LDPCH001", 8) == 0) return load_ldpc_binary(data, out);
+    return load_dvbs2_text(data, out);
+}
+
+extern "C" int ldpc_code_info(const ldpc_code *h, int *n, int *m, int *e, int *n_groups, int *max_deg)
+{
+    if (!h) return ldpc_set_error(LDPC_EINVAL, "NULL code");
+    if (n) *n = h->n;
+    if (m) *m = h->m;
+    if (e) *e = h->e;
+    if (n_groups) *n_groups = h->n_groups;
+    if (max_deg) *max_deg = h->max_deg;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_code_edges(const ldpc_code *h, uint32_t *edge_var, int *group_deg, int *group_cnt)
+{
+    if (!h) return ldpc_set_error(LDPC_EINVAL, "NULL code");
+    if (edge_var) memcpy(edge_var, h->edge_var.data(), 4ull * h->e);
+    if (group_deg) memcpy(group_deg, h->group_deg.data(), sizeof(int) * h->n_groups);
+    if (group_cnt) memcpy(group_cnt, h->group_cnt.data(), sizeof(int) * h->n_groups);
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_code_plan_info(const ldpc_code *h, int *staircase, int *n_windows, int *min_hazard)
+{
+    if (!h) return ldpc_set_error(LDPC_EINVAL, "NULL code");
+    if (staircase) *staircase = h->staircase ? 1 : 0;
+    if (n_windows) *n_windows = (int)h->windows.size();
+    if (min_hazard) *min_hazard = h->min_hazard;
+    return LDPC_OK;
+}
+
+extern "C" void ldpc_code_destroy(ldpc_code *h) { delete h; }
+
+// ---------------------------------------------------------------- channel
+extern "C" double ldpc_awgn_sigma(double ebn0_db, double rate)
+{
+    // CChanelAWGN_MKL::configure, code/x86/CChanel/CChanelAWGN_MKL.cpp:102-105
+    double interm = -0.1 * (ebn0_db + 10.0 * std::log10(rate));
+    return std::sqrt(std::pow(10.0, interm) / 2.0);
+}
+
+// P(q <= v) for q = clamp(trunc(factor*y), -sat, sat), y = -1 + sigma*z.
+// trunc(f*y) <= v  <=>  y < (v+1)/f  (v >= 0)   or   y <= v/f  (v < 0).
+extern "C" int ldpc_awgn_i8_table(double sigma, int factor, int sat, uint32_t *table)
+{
+    if (!table || sigma <= 0.0 || factor <= 0 || sat < 1 || sat > 31)
+        return ldpc_set_error(LDPC_EINVAL, "awgn table: sigma>0, factor>0, 1<=sat<=31");
+    // 2*sat+1 levels -sat..sat need 2*sat thresholds; table[63] holds sat.
+    for (int k = 0; k < 63; k++) table[k] = 0xFFFFFFFFu;
+    table[63] = (uint32_t)sat;
+    for (int k = 0; k < 2 * sat; k++) {
+        int v = -sat + k;
+        double t = (v >= 0) ? (double)(v + 1) / factor : (double)v / factor;
+        double p = 0.5 * std::erfc(-((t + 1.0) / sigma) / std::sqrt(2.0));
+        double u = std::floor(p * 4294967296.0);
+        if (u < 0) u = 0;
+        if (u > 4294967295.0) u = 4294967295.0;
+        table[k] = (uint32_t)u;
+    }
+    return LDPC_OK;
+}
+
+static inline uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// Generator definition (also implemented by the HIP kernel in decode.hip and
+// by tests/golden/gen_golden.py): element idx = cw*N + i,
+//   u = splitmix64(idx ^ (seed * 0xD1B54A32D192ED03)) >> 32
+//   q0 = -sat + #{k < 2*sat : u >= table[k]}  (bit 0 sent as -1; sat = table[63])
+//   q  = bit ? -q0 : q0
+extern "C" int ldpc_awgn_i8_host(int n, int batch, uint64_t first_cw, uint64_t seed, const uint32_t *table,
+                                 const uint8_t *codeword, int8_t *llr)
+{
+    if (n <= 0 || batch < 0 || !table || !llr) return ldpc_set_error(LDPC_EINVAL, "awgn host args");
+    const int sat = (int)table[63];
+    if (sat < 1 || sat > 31) return ldpc_set_error(LDPC_EINVAL, "awgn table: bad sat %d", sat);
+    const uint64_t key = seed * 0xD1B54A32D192ED03ull;
+    for (int b = 0; b < batch; b++)
+        for (int i = 0; i < n; i++) {
+            uint64_t idx = (first_cw + b) * (uint64_t)n + i;
+            uint32_t u = (uint32_t)(splitmix64(idx ^ key) >> 32);
+            int cnt = 0;
+            for (int k = 0; k < 2 * sat; k++) cnt += (u >= table[k]);
+            int q = cnt - sat;
+            if (codeword && codeword[(size_t)b * n + i]) q = -q;
+            llr[(size_t)b * n + i] = (int8_t)q;
+        }
+    return LDPC_OK;
+}

@@ -1,0 +1,38 @@
+// kernels.h -- launch descriptors shared between the C-ABI (capi.hip) and the
+// kernel translation units.
+#pragma once
+#include "kernels_common.h"
+
+struct DecodeLaunch {
+    // state, codeword-fastest layout: V[N][stride], messages per kernel family
+    void *V;
+    void *msg;
+    int stride;          // row stride in codewords (multiple of 64)
+    int batch;
+    int iters;
+    int is_float;
+    // code (device copies)
+    const uint32_t *d_edge_var;
+    const int *d_group_deg;
+    const int *d_group_cnt;
+    int n_groups, n, m, e;
+    // parameters
+    int algo, param, var_min, msg_max, early;
+    float beta;
+    int32_t *iters_used;
+};
+
+int launch_generic(const DecodeLaunch &L, hipStream_t s);
+
+// frame-major [batch][N] <-> node-major V[N][stride] (+ hard decision x > 0)
+int launch_interleave_i8(const int8_t *llr, int8_t *V, int n, int batch, int stride, hipStream_t s);
+int launch_interleave_f32(const float *llr, float *V, int n, int batch, int stride, hipStream_t s);
+int launch_deinterleave_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, int stride,
+                           hipStream_t s);
+int launch_deinterleave_f32(const float *V, uint8_t *hard, float *soft, int n, int batch, int stride,
+                            hipStream_t s);
+
+int launch_awgn_i8(int8_t *llr, int n, int batch, uint64_t first_cw, uint64_t seed, const AwgnTable &t,
+                   const uint8_t *codeword, hipStream_t s);
+int launch_count_errors(const uint8_t *hard, int n, int batch, int k, const uint8_t *ref,
+                        unsigned long long *counts, hipStream_t s);

@@ -1,0 +1,148 @@
+// layout.hip -- frame-major <-> node-major transposes, hard decision, the
+// synthetic AWGN channel and the error counter.
+//
+// Reference counterparts: Interleaver_uint8 / InvInterleaver_uint8
+// (code/gpu_fixed/transpose/GPU_Transpose_uint8.cu:9-130; the inverse applies
+// the hard decision x > 0 as code/x86/CTools/CTools.cpp:370 does), the GPU
+// channel (code/gpu_fixed/awgn_channel/CChanel_AWGN_SIMD.cu:7-30) and
+// CErrorAnalyzer::generate (code/x86/CErrorAnalyzer/CErrorAnalyzer.cpp:123-154).
+//
+// Transposes move 64x64 tiles through LDS: global reads are 64 contiguous
+// elements per row of the source, writes 64 contiguous codewords per node row.
+#include "kernels.h"
+
+namespace {
+
+template <typename T>
+__global__ void __launch_bounds__(256) interleave_k(const T *__restrict__ src, T *__restrict__ dst, int n,
+                                                    int batch, int stride)
+{
+    __shared__ T tile[64][65];
+    const int n0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int b = b0 + ty + 4 * r, i = n0 + tx;
+        tile[ty + 4 * r][tx] = (b < batch && i < n) ? src[(size_t)b * n + i] : (T)0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int i = n0 + ty + 4 * r, b = b0 + tx;
+        if (i < n && b < stride) dst[(size_t)i * stride + b] = tile[tx][ty + 4 * r];
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) deinterleave_k(const T *__restrict__ V, uint8_t *__restrict__ hard,
+                                                      T *__restrict__ soft, int n, int batch, int stride)
+{
+    __shared__ T tile[64][65];
+    const int n0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int i = n0 + ty + 4 * r, b = b0 + tx;
+        tile[ty + 4 * r][tx] = (i < n && b < batch) ? V[(size_t)i * stride + b] : (T)0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int b = b0 + ty + 4 * r, i = n0 + tx;
+        if (b < batch && i < n) {
+            const T x = tile[tx][ty + 4 * r];
+            if (hard) hard[(size_t)b * n + i] = (x > (T)0) ? 1 : 0;
+            if (soft) soft[(size_t)b * n + i] = x;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) awgn_i8_k(int8_t *__restrict__ llr, int n, int batch, uint64_t first_cw,
+                                                 uint64_t seed, AwgnTable t, const uint8_t *__restrict__ cw)
+{
+    __shared__ uint32_t th[64];
+    if (threadIdx.x < 64) th[threadIdx.x] = t.t[threadIdx.x];
+    __syncthreads();
+    const int sat = (int)th[63];
+    const uint64_t key = seed * 0xD1B54A32D192ED03ull;
+    const size_t total = (size_t)n * batch;
+    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (size_t)gridDim.x * 256) {
+        const size_t b = e / n, i = e - b * n;
+        const uint64_t idx = (first_cw + b) * (uint64_t)n + i;
+        const uint32_t u = (uint32_t)(splitmix64(idx ^ key) >> 32);
+        int cnt = 0;
+        for (int k = 0; k < 2 * sat; k++) cnt += (u >= th[k]);
+        int q = cnt - sat;
+        if (cw && cw[e]) q = -q;
+        llr[e] = (int8_t)q;
+    }
+}
+
+__global__ void __launch_bounds__(256) count_errors_k(const uint8_t *__restrict__ hard, int n, int k,
+                                                      const uint8_t *__restrict__ ref,
+                                                      unsigned long long *counts)
+{
+    const int b = blockIdx.x;
+    const uint8_t *h = hard + (size_t)b * n;
+    const uint8_t *r = ref ? ref + (size_t)b * n : nullptr;
+    int errs = 0;
+    for (int i = threadIdx.x; i < k; i += 256) errs += (h[i] != (r ? r[i] : 0));
+    __shared__ int red[256];
+    red[threadIdx.x] = errs;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && red[0]) {
+        atomicAdd(&counts[0], (unsigned long long)red[0]);
+        atomicAdd(&counts[1], 1ull);
+    }
+}
+
+inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -1; }
+
+}  // namespace
+
+int launch_interleave_i8(const int8_t *llr, int8_t *V, int n, int batch, int stride, hipStream_t s)
+{
+    dim3 g((n + 63) / 64, (stride + 63) / 64);
+    hipLaunchKernelGGL(interleave_k<int8_t>, g, dim3(256), 0, s, llr, V, n, batch, stride);
+    return ok();
+}
+int launch_interleave_f32(const float *llr, float *V, int n, int batch, int stride, hipStream_t s)
+{
+    dim3 g((n + 63) / 64, (stride + 63) / 64);
+    hipLaunchKernelGGL(interleave_k<float>, g, dim3(256), 0, s, llr, V, n, batch, stride);
+    return ok();
+}
+int launch_deinterleave_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, int stride,
+                           hipStream_t s)
+{
+    dim3 g((n + 63) / 64, (batch + 63) / 64);
+    hipLaunchKernelGGL(deinterleave_k<int8_t>, g, dim3(256), 0, s, V, hard, soft, n, batch, stride);
+    return ok();
+}
+int launch_deinterleave_f32(const float *V, uint8_t *hard, float *soft, int n, int batch, int stride,
+                            hipStream_t s)
+{
+    dim3 g((n + 63) / 64, (batch + 63) / 64);
+    hipLaunchKernelGGL(deinterleave_k<float>, g, dim3(256), 0, s, V, hard, soft, n, batch, stride);
+    return ok();
+}
+int launch_awgn_i8(int8_t *llr, int n, int batch, uint64_t first_cw, uint64_t seed, const AwgnTable &t,
+                   const uint8_t *codeword, hipStream_t s)
+{
+    size_t total = (size_t)n * batch;
+    int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(awgn_i8_k, dim3(blocks), dim3(256), 0, s, llr, n, batch, first_cw, seed, t, codeword);
+    return ok();
+}
+int launch_count_errors(const uint8_t *hard, int n, int batch, int k, const uint8_t *ref,
+                        unsigned long long *counts, hipStream_t s)
+{
+    if (batch <= 0) return 0;
+    hipLaunchKernelGGL(count_errors_k, dim3(batch), dim3(256), 0, s, hard, n, k, ref, counts);
+    return ok();
+}

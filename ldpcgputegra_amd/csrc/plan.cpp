@@ -1,0 +1,92 @@
+// plan.cpp -- static analysis of the layered schedule (host, once per code).
+//
+// The reference processes checks strictly in table order
+// (code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:172,262,334,...): every
+// check sees the V values left by all earlier checks.  To run many checks of
+// one codeword in parallel and stay bit-exact we need to know which checks
+// touch a variable that an earlier, not-yet-finished check writes:
+//
+//  * chain links: check i+1 shares exactly one variable with check i (the
+//    DVB-S2 parity staircase: check i writes K+i, check i+1 reads it).  The
+//    kernel forwards that value in registers, in schedule order.
+//  * hazards: any other variable shared by two checks at cyclic schedule
+//    distance < min_hazard.  The windowed kernel needs
+//    min_hazard >= kMinHazardWindowed (see decode.hip).
+#include <algorithm>
+#include <unordered_map>
+
+#include "ldpc_internal.h"
+
+static constexpr int kPlanSlots = 16;   // checks per window (lanes per codeword)
+
+int ldpc_plan_build(ldpc_code *h)
+{
+    const int m = h->m;
+    h->chain_in.assign(m, -1);
+    h->chain_out.assign(m, -1);
+    h->windows.clear();
+    h->win_slots = 0;
+
+    // --- chain links between cyclically consecutive checks
+    bool stair = (m > 1);
+    int links = 0;
+    for (int i = 0; i < m; i++) {
+        const int nx = (i + 1) % m;
+        const uint32_t *a = &h->edge_var[h->check_start[i]];
+        const uint32_t *b = &h->edge_var[h->check_start[nx]];
+        const int da = h->check_deg[i], db = h->check_deg[nx];
+        int shared = 0, sa = -1, sb = -1;
+        for (int x = 0; x < da; x++)
+            for (int y = 0; y < db; y++)
+                if (a[x] == b[y]) {
+                    shared++;
+                    sa = x;
+                    sb = y;
+                }
+        if (shared == 0) continue;
+        if (shared > 1 || sa != da - 1 || sb != db - 2) {
+            stair = false;
+            continue;
+        }
+        h->chain_out[i] = (int8_t)sa;
+        h->chain_in[nx] = (int8_t)sb;
+        links++;
+    }
+    h->staircase = stair && links > 0;
+    if (!h->staircase) {
+        std::fill(h->chain_in.begin(), h->chain_in.end(), (int8_t)-1);
+        std::fill(h->chain_out.begin(), h->chain_out.end(), (int8_t)-1);
+    }
+
+    // --- hazard distance (two passes over the cyclic schedule)
+    std::vector<int> last(h->n, -1);
+    int min_hz = 1 << 30;
+    for (int pass = 0; pass < 2; pass++)
+        for (int i = 0; i < m; i++) {
+            const uint32_t *ev = &h->edge_var[h->check_start[i]];
+            for (int j = 0; j < h->check_deg[i]; j++) {
+                const uint32_t v = ev[j];
+                if (pass == 1 && last[v] >= 0 && last[v] != i) {
+                    int d = i - last[v];
+                    if (d <= 0) d += m;
+                    const bool chain = (h->chain_in[i] == j);   // value arrives via the chain
+                    if (!chain) min_hz = std::min(min_hz, d);
+                }
+                last[v] = i;
+            }
+        }
+    h->min_hazard = (min_hz == (1 << 30)) ? m : min_hz;
+
+    // --- windows: consecutive runs of <= kPlanSlots checks of one degree group
+    if (h->staircase) {
+        h->win_slots = kPlanSlots;
+        int c = 0;
+        while (c < m) {
+            int g = h->check_group[c], cnt = 0;
+            while (c + cnt < m && cnt < kPlanSlots && h->check_group[c + cnt] == g) cnt++;
+            h->windows.push_back({c, cnt});
+            c += cnt;
+        }
+    }
+    return LDPC_OK;
+}

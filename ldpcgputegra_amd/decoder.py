@@ -1,0 +1,238 @@
+"""Host-side mirror of the reference decoder interface, on the MI355X C-ABI.
+
+Reference interface (code/x86/CDecoder/template/CDecoder.h:28-40,
+CDecoder_fixed.h:30-44, OMS/CDecoder_OMS_fixed_SSE.h, NMS/...,
+DecoderLibrary.h:44-134)::
+
+    CDecoder*  CreateDecoder(type, arch, format, p_decoder, vMin, vMax, mMin, mMax)
+    decoder->setOffset(k) / setFactor(k) / setVarRange / setMsgRange
+    decoder->decode(char llr[16*N], char hard[16*N], int iterations)
+
+Here ``CreateDecoder(..., arch="mi355x")`` returns an object with the same
+methods and argument meaning; ``decode`` fills ``hard`` in place (0/1 per bit,
+frame-major) like the reference.  Errors the reference handles with
+``printf + exit(0)`` raise ``LdpcError`` instead.
+
+``Decoder`` is the batch API used by tests and bench.py: any batch size,
+host numpy arrays or device tensors (``*_device`` methods take torch tensors
+on the GPU and enqueue on the current stream without synchronising).
+"""
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .codes import Code
+
+
+class Decoder:
+    """One C-ABI decoder context (device scratch for ``max_batch`` codewords)."""
+
+    def __init__(self, code, device=0, max_batch=4096, kernel=0):
+        self.code = code if isinstance(code, Code) else Code(code)
+        self.device = device
+        self.max_batch = max_batch
+        h = C.c_void_p()
+        _lib.check(_lib.lib().ldpc_ctx_create(self.code.handle, device, max_batch, C.byref(h)))
+        self._ctx = h
+        if kernel:
+            self.set_kernel(kernel)
+
+    # -- configuration
+    def set_kernel(self, kernel):
+        """0 = auto, 1 = generic (per-edge messages), 2 = windowed."""
+        _lib.check(_lib.lib().ldpc_ctx_set_kernel(self._ctx, int(kernel)))
+
+    @property
+    def kernel(self):
+        k = C.c_int()
+        _lib.check(_lib.lib().ldpc_ctx_get_kernel(self._ctx, C.byref(k)))
+        return k.value
+
+    def profile(self, enable=True):
+        """Record HIP events around every decode kernel launch."""
+        _lib.check(_lib.lib().ldpc_ctx_profile(self._ctx, int(enable)))
+
+    def kernel_time(self, reset=True):
+        """(summed decode-kernel ms, launches) since the last reset."""
+        ms, n = C.c_double(), C.c_int()
+        _lib.check(_lib.lib().ldpc_ctx_kernel_time(self._ctx, C.byref(ms), C.byref(n), int(reset)))
+        return ms.value, n.value
+
+    @property
+    def stream(self):
+        s = C.c_void_p()
+        _lib.check(_lib.lib().ldpc_ctx_stream(self._ctx, C.byref(s)))
+        return s.value
+
+    # -- host buffers (synchronous)
+    def decode_i8(self, llr, n_iter, params=None, out=None):
+        llr = np.ascontiguousarray(llr, dtype=np.int8)
+        B = llr.shape[0] if llr.ndim == 2 else 1
+        assert llr.size == B * self.code.n, "llr must be [batch, N]"
+        hard = out if out is not None else np.empty((B, self.code.n), dtype=np.uint8)
+        p = params or _lib.default_params()
+        _lib.check(_lib.lib().ldpc_decode_i8(self._ctx, llr.ctypes.data, hard.ctypes.data, B, n_iter, C.byref(p)))
+        return hard
+
+    def decode_f32(self, llr, n_iter, params=None, out=None):
+        llr = np.ascontiguousarray(llr, dtype=np.float32)
+        B = llr.shape[0] if llr.ndim == 2 else 1
+        assert llr.size == B * self.code.n
+        hard = out if out is not None else np.empty((B, self.code.n), dtype=np.uint8)
+        p = params or _lib.default_params(algo=_lib.ALGO_MS)
+        _lib.check(_lib.lib().ldpc_decode_f32(self._ctx, llr.ctypes.data, hard.ctypes.data, B, n_iter, C.byref(p)))
+        return hard
+
+    # -- device tensors (asynchronous on `stream`, default: torch current stream)
+    @staticmethod
+    def _ptr(t):
+        return None if t is None else C.c_void_p(t.data_ptr())
+
+    @staticmethod
+    def _torch_stream(stream):
+        if stream is not None:
+            return C.c_void_p(stream)
+        import torch
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def decode_i8_device(self, llr, hard, n_iter, params=None, soft=None, iters_used=None, stream=None):
+        B = llr.shape[0]
+        assert llr.numel() == B * self.code.n and llr.is_contiguous()
+        p = params or _lib.default_params()
+        _lib.check(_lib.lib().ldpc_decode_i8_async(self._ctx, self._torch_stream(stream), self._ptr(llr),
+                                                   self._ptr(hard), self._ptr(soft), self._ptr(iters_used),
+                                                   B, n_iter, C.byref(p)))
+
+    def decode_f32_device(self, llr, hard, n_iter, params=None, soft=None, iters_used=None, stream=None):
+        B = llr.shape[0]
+        assert llr.numel() == B * self.code.n and llr.is_contiguous()
+        p = params or _lib.default_params(algo=_lib.ALGO_MS)
+        _lib.check(_lib.lib().ldpc_decode_f32_async(self._ctx, self._torch_stream(stream), self._ptr(llr),
+                                                    self._ptr(hard), self._ptr(soft), self._ptr(iters_used),
+                                                    B, n_iter, C.byref(p)))
+
+    def awgn_i8_device(self, llr, first_cw, seed, table, codeword=None, stream=None):
+        t = np.ascontiguousarray(table, dtype=np.uint32)
+        _lib.check(_lib.lib().ldpc_awgn_i8_async(self._ctx, self._torch_stream(stream), self._ptr(llr),
+                                                 llr.shape[0], first_cw, seed, t.ctypes.data,
+                                                 self._ptr(codeword)))
+
+    def count_errors_device(self, hard, k, counts, ref=None, stream=None):
+        _lib.check(_lib.lib().ldpc_count_errors_async(self._ctx, self._torch_stream(stream), self._ptr(hard),
+                                                      hard.shape[0], k, self._ptr(ref), self._ptr(counts)))
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and _lib._lib is not None:
+            _lib._lib.ldpc_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+
+# ---------------------------------------------------------------------------
+# Reference-shaped mirror (CDecoder hierarchy + CreateDecoder factory)
+
+@dataclass
+class param_decoder:
+    """code/x86/main_p.cpp:133-141 defaults."""
+    nb_iters: int = 30
+    nms_factor_fixed: int = 29
+    nms_factor_float: float = 0.75
+    oms_offset_fixed: int = 1
+    oms_offset_float: float = 0.15
+
+
+class CDecoder:
+    """code/x86/CDecoder/template/CDecoder.h:28-40."""
+
+    def __init__(self, code, nb_frames=16, device=0):
+        self._dec = Decoder(code, device=device, max_batch=nb_frames)
+        self.nb_frames = nb_frames
+        self.sigB = 0.0
+        self.nb_iters = 0
+        self._p = _lib.default_params()
+
+    def setSigmaChannel(self, sigB):
+        self.sigB = float(sigB)
+
+    def setNumberOfIterations(self, value):
+        self.nb_iters = int(value)
+
+    def decode(self, var_nodes, Rprime_fix, nombre_iterations):
+        """decode(char llr[], char hard[], int it): int8 in, 0/1 out, in place.
+        A float llr array selects the float decoder (the reference's
+        fixed-point decoders ignore that overload, CDecoder_fixed_SSE.cpp:35-40;
+        here it runs the float layered min-sum)."""
+        n = self._dec.code.n
+        arr = np.asarray(var_nodes)
+        frames = arr.size // n
+        out = np.asarray(Rprime_fix).reshape(frames, n) if isinstance(Rprime_fix, np.ndarray) else None
+        if arr.dtype == np.float32 or arr.dtype == np.float64:
+            res = self._dec.decode_f32(arr.reshape(frames, n), nombre_iterations, self._float_params())
+        else:
+            res = self._dec.decode_i8(arr.reshape(frames, n), nombre_iterations, self._p)
+        if out is not None:
+            out[...] = res
+        return res
+
+    def _float_params(self):
+        return _lib.default_params(algo=_lib.ALGO_MS)
+
+
+class CDecoder_fixed(CDecoder):
+    """code/x86/CDecoder/template/CDecoder_fixed.h:30-44."""
+
+    def setVarRange(self, vmin, vmax):
+        self._p.var_min, self._p.var_max = int(vmin), int(vmax)
+
+    def setMsgRange(self, mmin, mmax):
+        self._p.msg_min, self._p.msg_max = int(mmin), int(mmax)
+
+
+class CDecoder_OMS_fixed_MI355X(CDecoder_fixed):
+    """Offset min-sum (code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.h)."""
+
+    def __init__(self, code, nb_frames=16, device=0):
+        super().__init__(code, nb_frames, device)
+        self._p.algo = _lib.ALGO_OMS
+        self._offset_set = False
+
+    def setOffset(self, offset):
+        # single assignment, as CDecoder_OMS_fixed_SSE::setOffset (:104-112)
+        if self._offset_set:
+            raise _lib.LdpcError(_lib.LDPC_EINVAL, "Offset value was already configured (%d)" % self._p.offset)
+        self._p.offset = int(offset)
+        self._offset_set = True
+
+
+class CDecoder_NMS_fixed_MI355X(CDecoder_fixed):
+    """Normalised min-sum (code/x86/CDecoder/NMS/CDecoder_NMS_fixed_SSE.h)."""
+
+    def __init__(self, code, nb_frames=16, device=0):
+        super().__init__(code, nb_frames, device)
+        self._p.algo = _lib.ALGO_NMS
+
+    def setFactor(self, factor):
+        self._p.factor = int(factor)
+
+
+def CreateDecoder(type, arch, format, p_decoder, vMin, vMax, mMin, mMax, code="576x288", nb_frames=16, device=0):
+    """code/x86/CDecoder/DecoderLibrary.h:44-134 (arch "mi355x" instead of "sse")."""
+    if arch not in ("mi355x", "gpu", "sse"):
+        raise _lib.LdpcError(_lib.LDPC_EUNSUPPORTED, "decoder unavailable: arch %s" % arch)
+    if format != "fixed":
+        raise _lib.LdpcError(_lib.LDPC_EUNSUPPORTED, "decoder unavailable: format %s" % format)
+    if type == "OMS":
+        d = CDecoder_OMS_fixed_MI355X(code, nb_frames, device)
+        d.setOffset(p_decoder.oms_offset_fixed)
+    elif type == "NMS":
+        d = CDecoder_NMS_fixed_MI355X(code, nb_frames, device)
+        d.setFactor(p_decoder.nms_factor_fixed)
+    else:
+        raise _lib.LdpcError(_lib.LDPC_EUNSUPPORTED, "Requested LDPC decoder does not exist (%s:%s)" % (arch, type))
+    d.setVarRange(vMin, vMax)
+    d.setMsgRange(mMin, mMax)
+    return d

@@ -1,0 +1,73 @@
+"""Code tables: numpy reader, C-ABI loader and DVB-S2 Annex-B builder agree,
+and reproduce the reference's PosNoeudsVariable tables (sha256 recorded by
+tools/extract_codes.py in codes/manifest.json)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ldpcgputegra_amd import Code, available, codes, load_table
+
+MANIFEST = json.load(open(os.path.join(codes.CODE_DIR, "manifest.json")))
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_table_matches_reference_hash(name):
+    t = load_table(name)
+    m = MANIFEST[name]
+    assert (t.n, t.m, t.e) == (m["n"], m["m"], m["e"])
+    assert [list(g) for g in t.groups] == m["groups"]
+    assert hashlib.sha256(t.edge_var.astype("<u4").tobytes()).hexdigest() == m["edge_var_sha256"]
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_c_loader_matches_numpy_reader(name):
+    t = load_table(name)
+    c = Code(name)
+    t2 = c.table()
+    assert (c.n, c.m, c.e) == (t.n, t.m, t.e)
+    assert t2.groups == t.groups
+    assert np.array_equal(t2.edge_var, t.edge_var)
+
+
+def test_dvbs2_structure():
+    t = load_table("dvbs2_r1_2")
+    assert (t.n, t.m, t.e) == (64800, 32400, 226799)
+    assert t.groups == [(7, 32399), (6, 1)]
+    c = Code("dvbs2_r1_2")
+    info = c.plan_info()
+    assert info["staircase"]
+    assert info["min_hazard"] >= 60          # measured: 62 (SURVEY / plan.cpp)
+
+
+def test_generic_codes_have_no_staircase():
+    assert not Code("576x288").plan_info()["staircase"]
+
+
+def test_code_from_table_object_roundtrip():
+    t = load_table("576x288")
+    c = Code(t)
+    assert np.array_equal(c.table().edge_var, t.edge_var)
+
+
+def test_available_lists_shipped_codes():
+    names = available()
+    for n in ("576x288", "1944x972", "dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r8_9", "dvbs2_r9_10"):
+        assert n in names
+
+
+def test_bad_tables_rejected():
+    from ldpcgputegra_amd import LdpcError, Table
+    t = load_table("576x288")
+    bad = t.edge_var.copy()
+    bad[1] = bad[0]                                   # repeated variable in one check
+    with pytest.raises(LdpcError):
+        Code(Table(t.n, t.m, t.groups, bad))
+    bad2 = t.edge_var.copy()
+    bad2[5] = t.n                                     # out of range
+    with pytest.raises(LdpcError):
+        Code(Table(t.n, t.m, t.groups, bad2))
+    with pytest.raises(FileNotFoundError):
+        Code("no_such_code")

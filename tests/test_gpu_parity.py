@@ -1,0 +1,190 @@
+"""GPU parity: the HIP decoder (through the C-ABI) against the reference's
+golden vectors and the CPU oracle.
+
+int8 paths: bit-exact hard decisions AND bit-exact final V (soft) vs the
+oracle.  Float path: the north star allows 1e-6 LLR; the kernels use the same
+exact IEEE ops (sub/add/min/max/abs, no FMA) as the oracle, so the test
+tolerance is FLOAT_TOL = 1e-6 absolute and in practice the results are
+bit-identical.
+"""
+import numpy as np
+import pytest
+from conftest import golden_cases, golden_inputs
+
+import oracle as O
+from ldpcgputegra_amd import ALGO_MS, ALGO_NMS, ALGO_OMS, Code, Decoder, channel, default_params, load_table
+
+pytestmark = pytest.mark.gpu
+FLOAT_TOL = 1e-6
+CASES = golden_cases()
+_decoders = {}
+
+
+def decoder(code, kernel=0, max_batch=4096):
+    key = (code, kernel, max_batch)
+    if key not in _decoders:
+        _decoders[key] = Decoder(Code(code), max_batch=max_batch, kernel=kernel)
+    return _decoders[key]
+
+
+def kernels_for(code):
+    ks = [1]
+    if Code(code).plan_info()["staircase"]:
+        ks.append(2)
+    return ks
+
+
+def params_of(case):
+    algo = ALGO_NMS if case["algo"] == 1 else ALGO_OMS
+    return default_params(algo=algo, offset=case["param"], factor=case["param"], var_min=case["var_min"],
+                          msg_max=case["msg_max"], msg_min=-case["msg_max"])
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_gpu_matches_reference_golden(case):
+    llr, expected = golden_inputs(case)
+    for k in kernels_for(case["code"]):
+        dec = decoder(case["code"], k, max_batch=64)
+        try:
+            got = dec.decode_i8(llr, case["iters"], params_of(case))
+        except Exception as e:   # windowed kernel may not support exotic params
+            if k == 2 and "not applicable" in str(e):
+                continue
+            raise
+        assert np.array_equal(got, expected), "kernel %d: %d bits differ" % (k, int((got != expected).sum()))
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+@pytest.mark.parametrize("code", ["576x288", "1944x972", "2048x384", "1024x518", "1200x600", "200x100",
+                                  "dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r9_10", "16200x7560"])
+@pytest.mark.parametrize("batch", [1, 37, 64])
+def test_soft_output_bit_exact_vs_oracle(code, batch):
+    torch = _torch()
+    t = load_table(code)
+    iters = 6 if t.n > 10000 else 15
+    sigma = channel.sigma_from_ebn0(1.5, t.k_info / t.n)
+    llr = channel.awgn_i8_host(t.n, batch, seed=batch, table=channel.i8_table(sigma))
+    ref_hard, ref_soft, _ = O.decode_i8(t, llr, iters, O.OMS, 1, return_soft=True)
+    for k in kernels_for(code):
+        dec = decoder(code, k, max_batch=64)
+        d_llr = torch.from_numpy(llr).cuda()
+        d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+        d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
+        dec.decode_i8_device(d_llr, d_hard, iters, soft=d_soft)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_soft.cpu().numpy(), ref_soft), "kernel %d" % k
+        assert np.array_equal(d_hard.cpu().numpy(), ref_hard), "kernel %d" % k
+
+
+@pytest.mark.parametrize("algo,param", [(ALGO_OMS, 0), (ALGO_OMS, 3), (ALGO_NMS, 24), (ALGO_MS, 0)])
+def test_algorithms_vs_oracle(algo, param):
+    t = load_table("1944x972")
+    llr = channel.awgn_i8_host(t.n, 40, seed=7, table=channel.i8_table(0.75))
+    o_algo = O.NMS if algo == ALGO_NMS else O.OMS
+    o_param = param if algo != ALGO_MS else 0
+    exp = O.decode_i8(t, llr, 12, o_algo, o_param)
+    p = default_params(algo=algo, offset=param, factor=param)
+    got = decoder("1944x972", 1, 64).decode_i8(llr, 12, p)
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("code", ["576x288", "dvbs2_r1_2"])
+def test_early_termination_vs_oracle(code):
+    torch = _torch()
+    t = load_table(code)
+    batch = 24
+    sigma = channel.sigma_from_ebn0(1.0 if t.n > 10000 else 2.0, t.k_info / t.n)
+    llr = channel.awgn_i8_host(t.n, batch, seed=3, table=channel.i8_table(sigma))
+    ref_hard, ref_soft, ref_its = O.decode_i8(t, llr, 30, O.OMS, 1, early_term=True, return_soft=True)
+    assert ref_its.min() < 30                                # some codewords stop early
+    for k in kernels_for(code):
+        dec = decoder(code, k, max_batch=64)
+        d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+        d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
+        d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
+        dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, 30, params=default_params(early_term=1),
+                             soft=d_soft, iters_used=d_its)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_its.cpu().numpy(), ref_its), "kernel %d" % k
+        assert np.array_equal(d_soft.cpu().numpy(), ref_soft), "kernel %d" % k
+
+
+@pytest.mark.parametrize("code,algo,beta", [("1944x972", ALGO_MS, 0.0), ("576x288", ALGO_OMS, 0.15),
+                                            ("576x288", ALGO_NMS, 0.75), ("dvbs2_r1_2", ALGO_MS, 0.0)])
+def test_float_decoder_vs_oracle(code, algo, beta):
+    torch = _torch()
+    t = load_table(code)
+    rng = np.random.default_rng(5)
+    batch = 33
+    sigma = channel.sigma_from_ebn0(1.2, t.k_info / t.n)
+    llr = (-1.0 + sigma * rng.standard_normal((batch, t.n))).astype(np.float32)
+    iters = 5 if t.n > 10000 else 20
+    o_algo = O.NMS if algo == ALGO_NMS else O.OMS
+    ref_hard, ref_soft, _ = O.decode_f32(t, llr, iters, o_algo, beta)
+    dec = decoder(code, 0, 64)
+    d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+    d_soft = torch.empty((batch, t.n), dtype=torch.float32, device="cuda")
+    dec.decode_f32_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=default_params(algo=algo, beta=beta),
+                          soft=d_soft)
+    torch.cuda.synchronize()
+    soft = d_soft.cpu().numpy()
+    assert np.max(np.abs(soft - ref_soft)) <= FLOAT_TOL
+    assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
+
+
+def test_device_channel_matches_host_generator():
+    torch = _torch()
+    t = load_table("dvbs2_r1_2")
+    table = channel.i8_table(0.87)
+    dec = decoder("dvbs2_r1_2", 0, 64)
+    d = torch.empty((7, t.n), dtype=torch.int8, device="cuda")
+    dec.awgn_i8_device(d, first_cw=123, seed=42, table=table)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), channel.awgn_i8_host(t.n, 7, 42, table, first_cw=123))
+
+
+def test_error_counter():
+    torch = _torch()
+    dec = decoder("576x288", 1, 64)
+    hard = np.zeros((5, 576), np.uint8)
+    hard[1, 3] = 1
+    hard[1, 100] = 1
+    hard[3, 287] = 1
+    hard[4, 300] = 1            # beyond k = 288: not counted (CErrorAnalyzer counts N-M bits)
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    dec.count_errors_device(torch.from_numpy(hard).cuda(), 288, counts)
+    torch.cuda.synchronize()
+    assert counts.cpu().tolist() == [3, 2]
+
+
+def test_dvbs2_full_batch_properties():
+    """BASELINE configs[2] size (4096 codewords, 50 it): shard invariance,
+    determinism and convergence at high SNR (size-independent properties)."""
+    torch = _torch()
+    t = load_table("dvbs2_r1_2")
+    B = 4096
+    dec = decoder("dvbs2_r1_2", 0, B)
+    table = channel.i8_table(channel.sigma_from_ebn0(1.2, 0.5))
+    llr = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
+    dec.awgn_i8_device(llr, 0, 77, table)
+    h1 = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+    h2 = torch.empty_like(h1)
+    dec.decode_i8_device(llr, h1, 50)
+    dec.decode_i8_device(llr[:1000], h2[:1000], 50)           # ragged shard
+    dec.decode_i8_device(llr[1000:], h2[1000:], 50)
+    torch.cuda.synchronize()
+    assert torch.equal(h1, h2)
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    dec.count_errors_device(h1, t.k_info, counts)
+    torch.cuda.synchronize()
+    be, fe = counts.cpu().tolist()
+    assert fe <= 2, (be, fe)                                   # 1.2 dB: past the waterfall
+    # spot-check 16 codewords against the oracle at full iterations
+    sel = llr[::256].cpu().numpy()
+    exp = O.decode_i8(t, sel, 50)
+    assert np.array_equal(h1[::256].cpu().numpy(), exp)
