@@ -71,6 +71,15 @@ def lib():
     """Load libldpc_mi355x.so (raises if it was not built)."""
     global _lib
     if _lib is None:
+        # One process holds one HIP runtime: libamdhip64.so.7 is resolved by
+        # soname, so whichever copy loads first (ROCm's, or the one bundled in
+        # PyTorch's wheel) serves everybody.  When PyTorch is installed we let
+        # it load first, so the device tensors handed to us and our kernels
+        # share its runtime (loading ours first leaves torch.cuda unusable).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError("libldpc_mi355x.so not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
                               " (expected at %s)" % LIB_PATH)

@@ -180,7 +180,7 @@ class Code:
     def plan_info(self):
         s, w, hz = C.c_int(), C.c_int(), C.c_int()
         _lib.check(_lib.lib().ldpc_code_plan_info(self._h, C.byref(s), C.byref(w), C.byref(hz)))
-        return dict(staircase=bool(s.value), n_windows=w.value, min_hazard=hz.value)
+        return dict(staircase=bool(s.value), n_windows=w.value, min_hazard=hz.value, windowed=w.value > 0)
 
     def __del__(self):
         h = getattr(self, "_h", None)

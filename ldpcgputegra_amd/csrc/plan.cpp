@@ -78,7 +78,8 @@ int ldpc_plan_build(ldpc_code *h)
     h->min_hazard = (min_hz == (1 << 30)) ? m : min_hz;
 
     // --- windows: consecutive runs of <= kPlanSlots checks of one degree group
-    if (h->staircase) {
+    extern bool windowed_kernel_available();
+    if (h->staircase && windowed_kernel_available()) {
         h->win_slots = kPlanSlots;
         int c = 0;
         while (c < m) {

@@ -29,7 +29,7 @@ def decoder(code, kernel=0, max_batch=4096):
 
 def kernels_for(code):
     ks = [1]
-    if Code(code).plan_info()["staircase"]:
+    if Code(code).plan_info()["windowed"]:
         ks.append(2)
     return ks
 

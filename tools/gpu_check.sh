@@ -1,0 +1,23 @@
+#!/bin/bash
+# One GPU-box session: smoke, GPU parity tests, short bench.  Each GPU step has
+# its own time limit; a crash/abort/timeout (rc >= 124) stops the script, an
+# ordinary test failure (rc 1) does not.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() {  # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name" >&2
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" >&2
+    tail -5 "gpurun_out/$name.log" >&2
+    if [ $rc -ge 124 ] || [ $rc -gt 1 -a $rc -ne 5 ]; then exit $rc; fi
+    return 0
+}
+STEPS=${STEPS:-smoke,pytest,bench}
+[[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+[[ $STEPS == *pytest* ]] && run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 ${PYTEST_ARGS}
+[[ $STEPS == *bench* ]] && run bench 600 python bench.py ${BENCH_ARGS}
+exit 0
