@@ -11,6 +11,9 @@
 
 #include "ldpc_internal.h"
 
+bool windowed_supported(const ldpc_code *h);   // windowed.hip
+int ldpc_plan_build(ldpc_code *h);             // plan.cpp
+
 // ---------------------------------------------------------------- errors
 static thread_local std::string g_last_error;
 
@@ -85,7 +88,6 @@ int ldpc_code_finalize(ldpc_code *h)
                 if (ev[j] == ev[k])
                     return ldpc_set_error(LDPC_EINVAL, "check %d lists variable %u twice", c, ev[j]);
     }
-    extern int ldpc_plan_build(ldpc_code * h);
     return ldpc_plan_build(h);
 }
 
@@ -263,7 +265,7 @@ extern "C" int ldpc_code_plan_info(const ldpc_code *h, int *staircase, int *n_wi
 {
     if (!h) return ldpc_set_error(LDPC_EINVAL, "NULL code");
     if (staircase) *staircase = h->staircase ? 1 : 0;
-    if (n_windows) *n_windows = (int)h->windows.size();
+    if (n_windows) *n_windows = windowed_supported(h) ? (int)h->windows.size() : 0;
     if (min_hazard) *min_hazard = h->min_hazard;
     return LDPC_OK;
 }

@@ -88,6 +88,46 @@ int ldpc_plan_build(ldpc_code *h)
             h->windows.push_back({c, cnt});
             c += cnt;
         }
+        // Verify the windowed kernel's read-ahead (windowed.hip): inside one
+        // degree group the V of window u is loaded before windows u-1 and u-2
+        // store, and all checks of a window read V before any of them stores.
+        // So a variable read by window u (chain-in edges excepted: their value
+        // arrives through the chain) must not be written by windows u-2..u.
+        // Group boundaries drain the pipeline.
+        constexpr int kLookahead = 2;
+        std::vector<int> writer_win(h->n, -1);   // last window (this group pass) writing var
+        bool ok = true;
+        int gstart = 0;
+        for (int wi = 0; wi < (int)h->windows.size() && ok; wi++) {
+            const ldpc_window &win = h->windows[wi];
+            if (wi > 0 && h->check_group[win.first] != h->check_group[h->windows[wi - 1].first]) gstart = wi;
+            for (int k = 0; k < win.count && ok; k++) {
+                const int ci = win.first + k;
+                const uint32_t *ev = &h->edge_var[h->check_start[ci]];
+                for (int j = 0; j < h->check_deg[ci]; j++) {
+                    if (h->chain_in[ci] == j) continue;
+                    const int lw = writer_win[ev[j]];
+                    if (lw >= gstart && wi - lw <= kLookahead) ok = false;
+                }
+            }
+            // inside a window only the chain link may share a variable
+            std::unordered_map<uint32_t, int> seen;
+            for (int k = 0; k < win.count && ok; k++) {
+                const int ci = win.first + k;
+                const uint32_t *ev = &h->edge_var[h->check_start[ci]];
+                for (int j = 0; j < h->check_deg[ci]; j++) {
+                    auto it = seen.find(ev[j]);
+                    if (it != seen.end() && !(it->second == k - 1 && h->chain_in[ci] == j)) ok = false;
+                    seen[ev[j]] = k;
+                }
+            }
+            for (int k = 0; k < win.count; k++) {
+                const int ci = win.first + k;
+                const uint32_t *ev = &h->edge_var[h->check_start[ci]];
+                for (int j = 0; j < h->check_deg[ci]; j++) writer_win[ev[j]] = wi;
+            }
+        }
+        if (!ok) h->windows.clear();
     }
     return LDPC_OK;
 }

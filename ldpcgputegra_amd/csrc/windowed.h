@@ -5,13 +5,18 @@
 
 struct WindowedCode {
     int valid;
+    int d0;                 // degree of group 0 (group 1 has d0 - 1)
     int max_deg;
-    int words;             // 32-bit words per compressed check message (1 or 2)
     int n_windows;
-    int *d_win;            // [n_windows] packed (first | count << 24) ... see windowed.hip
-    uint32_t *d_slot;      // per check slot descriptors
+    int g0_end;             // first window of group 1
+    uint32_t *d_slotvar;    // per window [D][16] variable indices
+    uint32_t *d_slotoff;    // [n_windows]
+    uint8_t *d_flags;       // [n_windows][16]
+    int *d_first;           // [n_windows]
+    int *d_cnt;             // [n_windows]
 };
 
+bool windowed_kernel_available();
 bool windowed_supported(const ldpc_code *h);
 bool windowed_params_ok(const ldpc_params *p);
 int windowed_code_upload(const ldpc_code *h, WindowedCode *w);
