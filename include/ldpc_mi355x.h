@@ -115,6 +115,11 @@ int ldpc_code_info(const ldpc_code *h, int *n, int *m, int *e, int *n_groups, in
 int ldpc_code_edges(const ldpc_code *h, uint32_t *edge_var, int *group_deg, int *group_cnt);
 /* 1 if the layered schedule has the DVB-S2 staircase chain (fast kernel). */
 int ldpc_code_plan_info(const ldpc_code *h, int *staircase, int *n_windows, int *min_hazard);
+/* Window schedule of the windowed2 kernel for S checks per window and
+ * read-ahead P: writes up to max_windows (first check, count) pairs and the
+ * total count (0 when the code has no staircase schedule). */
+int ldpc_code_window_plan(const ldpc_code *h, int S, int P, int *first, int *count, int max_windows,
+                          int *n_windows);
 void ldpc_code_destroy(ldpc_code *h);
 
 /* ---- decoder context --------------------------------------------------- */

@@ -182,6 +182,17 @@ class Code:
         _lib.check(_lib.lib().ldpc_code_plan_info(self._h, C.byref(s), C.byref(w), C.byref(hz)))
         return dict(staircase=bool(s.value), n_windows=w.value, min_hazard=hz.value, windowed=w.value > 0)
 
+    def window_plan(self, S, P):
+        """[(first check, count)] of the windowed2 schedule (empty if none)."""
+        L = _lib.lib()
+        n = C.c_int()
+        _lib.check(L.ldpc_code_window_plan(self._h, S, P, None, None, 0, C.byref(n)))
+        first = np.empty(max(n.value, 1), dtype=np.int32)
+        count = np.empty(max(n.value, 1), dtype=np.int32)
+        _lib.check(L.ldpc_code_window_plan(self._h, S, P, first.ctypes.data, count.ctypes.data, n.value,
+                                           C.byref(n)))
+        return list(zip(first[:n.value].tolist(), count[:n.value].tolist()))
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and _lib._lib is not None:

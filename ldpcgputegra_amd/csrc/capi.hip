@@ -35,6 +35,7 @@ struct ldpc_ctx {
     uint32_t *d_edge_var = nullptr;
     int *d_group_deg = nullptr, *d_group_cnt = nullptr;
     WindowedCode wcode{};           // windowed-kernel tables (windowed.hip)
+    Windowed2Code w16{}, w32{};     // windowed2.hip tables, S = 16 and S = 32
     // scratch (lazily sized)
     void *d_V = nullptr;
     size_t V_bytes = 0;
@@ -105,6 +106,8 @@ extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ld
             hipSuccess)
         return fail(ldpc_set_error(LDPC_EDEVICE, "code table upload"));
     if ((rc = windowed_code_upload(h, &c->wcode)) != LDPC_OK) return fail(rc);
+    if ((rc = windowed2_upload(h, 16, 2, &c->w16)) != LDPC_OK) return fail(rc);
+    if ((rc = windowed2_upload(h, 32, 1, &c->w32)) != LDPC_OK) return fail(rc);
     *out = c;
     return LDPC_OK;
 }
@@ -115,6 +118,8 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     windowed_code_free(&c->wcode);
+    windowed2_free(&c->w16);
+    windowed2_free(&c->w32);
     for (auto &pr : c->events) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -138,9 +143,9 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 2) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto), 1, 2");
-    if (k == 2 && !windowed_supported(c->code))
-        return ldpc_set_error(LDPC_EUNSUPPORTED, "windowed kernel cannot schedule this code");
+    if (!c || k < 0 || k > 4) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 4");
+    if ((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid))
+        return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
     c->kernel = k;
     return LDPC_OK;
 }
@@ -202,12 +207,22 @@ static int check_params(const ldpc_ctx *c, int batch, int n_iter, const ldpc_par
     return LDPC_OK;
 }
 
-static bool use_windowed(const ldpc_ctx *c, const ldpc_params *p, bool is_float)
+// kernel family for this call: 1 generic, 2 windowed, 3 windowed2/S16, 4 windowed2/S32
+static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float)
 {
-    if (c->kernel == 1) return false;
-    if (is_float || !windowed_supported(c->code)) return false;
-    if (!windowed_params_ok(p)) return false;
-    return true;   // kernel 0 (auto) or 2
+    if (is_float) return 1;
+    const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
+    const bool w2 = windowed2_params_ok(p);
+    switch (c->kernel) {
+    case 1: return 1;
+    case 2: return w1 ? 2 : -1;
+    case 3: return (w2 && c->w16.valid) ? 3 : -1;
+    case 4: return (w2 && c->w32.valid) ? 4 : -1;
+    default:
+        if (w2 && c->w32.valid) return 4;
+        if (w1) return 2;
+        return 1;
+    }
 }
 
 static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t *d_hard, void *d_soft,
@@ -221,9 +236,10 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     const ldpc_code *h = c->code;
     const int stride = (batch + 63) / 64 * 64;
     const size_t esz = is_float ? 4 : 1;
-    const bool win = use_windowed(c, p, is_float);
-    if (c->kernel == 2 && !win)
-        return ldpc_set_error(LDPC_EUNSUPPORTED, "windowed kernel selected but not applicable to these params");
+    const int kern = pick_kernel(c, p, is_float);
+    if (kern < 0)
+        return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d selected but not applicable to these params", c->kernel);
+    const bool win = kern >= 2;
     const size_t msg_need = win ? windowed_msg_bytes(h, stride) : (size_t)h->e * stride * esz;
     if ((rc = ensure(&c->d_V, &c->V_bytes, (size_t)h->n * stride * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&c->d_msg, &c->msg_bytes, msg_need)) != LDPC_OK) return rc;
@@ -264,7 +280,10 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
         HIP_TRY(hipEventCreate(&ev1));
         HIP_TRY(hipEventRecord(ev0, s));
     }
-    int lr = win ? launch_windowed(L, c->wcode, s) : launch_generic(L, s);
+    int lr = kern == 4   ? launch_windowed2(L, c->w32, s)
+             : kern == 3 ? launch_windowed2(L, c->w16, s)
+             : kern == 2 ? launch_windowed(L, c->wcode, s)
+                         : launch_generic(L, s);
     if (c->profile) {
         HIP_TRY(hipEventRecord(ev1, s));
         c->events.emplace_back(ev0, ev1);

@@ -270,6 +270,23 @@ extern "C" int ldpc_code_plan_info(const ldpc_code *h, int *staircase, int *n_wi
     return LDPC_OK;
 }
 
+int ldpc_plan_windows(const ldpc_code *h, int S, int P, std::vector<ldpc_window> &out);   // plan.cpp
+
+extern "C" int ldpc_code_window_plan(const ldpc_code *h, int S, int P, int *first, int *count, int max_windows,
+                                     int *n_windows)
+{
+    if (!h || S < 1 || S > 64 || P < 0 || !n_windows) return ldpc_set_error(LDPC_EINVAL, "window plan args");
+    std::vector<ldpc_window> w;
+    int rc = ldpc_plan_windows(h, S, P, w);
+    if (rc != LDPC_OK) return rc;
+    *n_windows = (int)w.size();
+    for (int i = 0; i < (int)w.size() && i < max_windows; i++) {
+        if (first) first[i] = w[i].first;
+        if (count) count[i] = w[i].count;
+    }
+    return LDPC_OK;
+}
+
 extern "C" void ldpc_code_destroy(ldpc_code *h) { delete h; }
 
 // ---------------------------------------------------------------- channel

@@ -19,6 +19,55 @@
 
 static constexpr int kPlanSlots = 16;   // checks per window (lanes per codeword)
 
+// Windows for windowed2.hip: greedy runs of <= S consecutive checks of one
+// degree group such that (1) only slot 0 may lack a chain input, (2) inside
+// a window only the chain link shares a variable, and (3) no variable read by
+// window u (chain input excepted) was written by windows u-P..u-1 of the same
+// group (the kernel loads window u's V before those windows store).
+int ldpc_plan_windows(const ldpc_code *h, int S, int P, std::vector<ldpc_window> &out)
+{
+    out.clear();
+    if (!h->staircase) return LDPC_OK;
+    std::vector<int> writer(h->n, -1);        // last window index writing the variable
+    std::vector<int> in_win(h->n, -1);        // window index that touched it (this window)
+    int gstart = 0;
+    int c = 0;
+    while (c < h->m) {
+        const int u = (int)out.size();
+        const int g = h->check_group[c];
+        if (u > 0 && h->check_group[out.back().first] != g) gstart = u;
+        int cnt = 0;
+        while (c + cnt < h->m && cnt < S) {
+            const int ci = c + cnt;
+            if (h->check_group[ci] != g) break;
+            if (cnt > 0 && h->chain_in[ci] < 0) break;          // chain break: start a new window
+            const uint32_t *ev = &h->edge_var[h->check_start[ci]];
+            bool ok = true;
+            for (int j = 0; j < h->check_deg[ci] && ok; j++) {
+                // the chain input arrives in registers from check ci-1 (the
+                // previous slot, or the carry of the previous window)
+                if (h->chain_in[ci] == j) continue;
+                if (in_win[ev[j]] == u) ok = false;               // shared inside the window
+                const int lw = writer[ev[j]];
+                if (lw >= gstart && lw >= u - P) ok = false;      // written by the read-ahead span
+            }
+            if (!ok) {
+                if (cnt == 0) return ldpc_set_error(LDPC_EINVAL, "plan: check %d cannot start a window", ci);
+                break;
+            }
+            for (int j = 0; j < h->check_deg[ci]; j++) in_win[ev[j]] = u;
+            cnt++;
+        }
+        for (int k = 0; k < cnt; k++) {
+            const uint32_t *ev = &h->edge_var[h->check_start[c + k]];
+            for (int j = 0; j < h->check_deg[c + k]; j++) writer[ev[j]] = u;
+        }
+        out.push_back({c, cnt});
+        c += cnt;
+    }
+    return LDPC_OK;
+}
+
 int ldpc_plan_build(ldpc_code *h)
 {
     const int m = h->m;

@@ -16,6 +16,23 @@ struct WindowedCode {
     int *d_cnt;             // [n_windows]
 };
 
+// windowed2.hip: z-domain chain, S = 16 (P = 2) or S = 32 (P = 1) checks per window
+struct Windowed2Code {
+    int valid;
+    int S, P, d0;
+    int n_windows;
+    int g0_end;
+    uint32_t *d_slotvar;
+    uint32_t *d_slotoff;
+    uint8_t *d_flags;
+    int *d_first;
+    int *d_cnt;
+};
+bool windowed2_params_ok(const ldpc_params *p);
+int windowed2_upload(const ldpc_code *h, int S, int P, Windowed2Code *w);
+void windowed2_free(Windowed2Code *w);
+int launch_windowed2(const DecodeLaunch &L, const Windowed2Code &w, hipStream_t s);
+
 bool windowed_kernel_available();
 bool windowed_supported(const ldpc_code *h);
 bool windowed_params_ok(const ldpc_params *p);

@@ -1,0 +1,514 @@
+// windowed2.hip -- second-generation windowed layered kernel for staircase
+// (DVB-S2 IRA) codes, int8 offset-min-sum fast path.
+//
+// Same decomposition as windowed.hip (pre / serial staircase chain / post per
+// window of consecutive checks, bit-exact with
+// code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:172-546), with three
+// changes that cut the per-check VALU work:
+//
+// 1. Sign-normalised ("z-domain") chain.  Check k maps the new value y of the
+//    staircase variable it reads to the new value of the one it writes:
+//        y_k = co_k + eps_k * dz(y_{k-1} - mx_k),
+//        dz(u) = sign(u) * clamp(|u| - offset, 0, T_k) = med3(u - med3(u, -off, off), -T, T)
+//    (eps_k = -1 iff the other edges' sign parity is odd, T_k = cst(min over
+//    the info edges)).  With rho_k = eps_k rho_{k-1} and z_k = rho_k y_k every
+//    step is   u_k = dz(u_{k-1}) + Dprev_k   -- med3, sub, med3, and one
+//    DPP add (row_shr:1) that also moves the value to the next lane.
+//    Lanes run the recurrence systolically (no per-step select): after s
+//    steps lanes 0..s are final.  Chain values stay unclamped; that never
+//    changes a dz input that matters because |y - mx| >= 127 - msg_max >
+//    T + offset whenever y would have been clamped (needs msg_max <= 63 and
+//    var range [-127, 127]; other parameters use windowed.hip).
+// 2. S = 32 checks per window and G = 2 codewords per wave (S = 16 / G = 4
+//    also built): 2 waves per SIMD at batch 4096, so the SIMD issues every 2
+//    cycles instead of every 4.  A 32-lane chain step crosses 16-lane DPP
+//    rows with row_bcast:15.
+// 3. Cheaper per-edge arithmetic: a = med3(c, -c, msg_max), running min2 =
+//    med3(a, min1, min2), sign parity accumulated as XOR of whole words,
+//    negation by (r ^ s) + (s & 1).
+//
+// Read-ahead: V / messages of window t+P are loaded before window t's
+// stores.  plan.cpp builds windows so that no variable read by window u
+// (chain input excepted) is written by windows u-P..u-1 of the same group,
+// and breaks windows where the chain breaks (only slot 0 may lack a chain
+// input).  The single check of the later degree group (DVB-S2 check 0) uses
+// the exact general step (its |min(c, max_msg)| quirk).
+//
+// Layout: V[N][stride] int8 (codeword fastest), Mc[check][stride] u32:
+// cst1 | cst2 << 7 | jmin << 14 | sign_j << (19 + j).
+#include <vector>
+
+#include "windowed.h"
+
+namespace {
+
+constexpr int F_ACT = 1, F_XIN = 2, F_ODEAD = 4;
+
+struct W2Args {
+    int8_t *V;
+    uint32_t *Mc;
+    int stride;
+    int iters;
+    const uint32_t *slotvar;   // per window [D][S]
+    const uint32_t *slotoff;   // [n_windows]
+    const uint8_t *flags;      // [n_windows][S]
+    const int *win_first;
+    const int *win_cnt;
+    int g0_end, n_windows;
+    int off, msg_max, early;
+    int32_t *iters_used;
+};
+
+// ---- lane shifts inside an S-lane row (S = 16: DPP row; S = 32: two rows)
+template <int S>
+LDPC_DEV int shift1(int old, int v)
+{
+    if constexpr (S == 32) {
+        // rows 1, 3 <- lane 15 of rows 0, 2 ; then lanes 1..15 of every 16-row
+        const int t = __builtin_amdgcn_update_dpp(old, v, 0x142, 0xA, 0xF, false);
+        return __builtin_amdgcn_update_dpp(t, v, 0x111, 0xF, 0xF, false);
+    } else {
+        return __builtin_amdgcn_update_dpp(old, v, 0x111, 0xF, 0xF, false);
+    }
+}
+
+// inclusive XOR scan over the S lanes of a row
+template <int S>
+LDPC_DEV int xor_scan(int p)
+{
+    p ^= __builtin_amdgcn_update_dpp(0, p, 0x111, 0xF, 0xF, false);
+    p ^= __builtin_amdgcn_update_dpp(0, p, 0x112, 0xF, 0xF, false);
+    p ^= __builtin_amdgcn_update_dpp(0, p, 0x114, 0xF, 0xF, false);
+    p ^= __builtin_amdgcn_update_dpp(0, p, 0x118, 0xF, 0xF, false);
+    if constexpr (S == 32) p ^= __builtin_amdgcn_update_dpp(0, p, 0x142, 0xA, 0xF, false);
+    return p;
+}
+
+LDPC_DEV int med3(int x, int lo, int hi)
+{
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
+}
+
+// S-1 systolic chain steps: u <- dz(u) + dprev, shifted one lane.
+template <int S>
+LDPC_DEV int chain_steps(int u, int dprev, int off, int T)
+{
+    const int noff = -off, nT = -T;
+#pragma unroll
+    for (int s = 0; s < S - 1; s++) {
+        int s1, s2, s3;
+        if constexpr (S == 32) {
+            asm("v_med3_i32 %1, %0, %5, %6\n\t"
+                "v_sub_u32 %2, %0, %1\n\t"
+                "v_med3_i32 %3, %2, %7, %8\n\t"
+                "s_nop 1\n\t"
+                "v_add_u32_dpp %0, %3, %4 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                "v_add_u32_dpp %0, %3, %4 row_shr:1 row_mask:0xf bank_mask:0xf"
+                : "+v"(u), "=&v"(s1), "=&v"(s2), "=&v"(s3)
+                : "v"(dprev), "v"(noff), "v"(off), "v"(nT), "v"(T));
+        } else {
+            asm("v_med3_i32 %1, %0, %5, %6\n\t"
+                "v_sub_u32 %2, %0, %1\n\t"
+                "v_med3_i32 %3, %2, %7, %8\n\t"
+                "s_nop 1\n\t"
+                "v_add_u32_dpp %0, %3, %4 row_shr:1 row_mask:0xf bank_mask:0xf"
+                : "+v"(u), "=&v"(s1), "=&v"(s2), "=&v"(s3)
+                : "v"(dprev), "v"(noff), "v"(off), "v"(nT), "v"(T));
+        }
+    }
+    return u;
+}
+
+template <int D>
+struct Tab {
+    uint32_t var[D];
+};
+
+template <int D>
+struct Buf {
+    int v[D];
+    uint32_t addr[D];
+    uint32_t m;
+};
+
+template <int D, int S>
+LDPC_DEV void load_tab(Tab<D> &t, const W2Args &a, int w, int slot)
+{
+    const uint32_t *p = a.slotvar + a.slotoff[w] + slot;
+#pragma unroll
+    for (int j = 0; j < D; j++) t.var[j] = p[j * S];
+}
+
+template <int D, int S>
+LDPC_DEV void load_buf(Buf<D> &bf, const Tab<D> &t, const W2Args &a, int w, int slot, int b)
+{
+#pragma unroll
+    for (int j = 0; j < D; j++) bf.addr[j] = t.var[j] * (uint32_t)a.stride + (uint32_t)b;
+    if (a.flags[w * S + slot] & F_ACT) {
+#pragma unroll
+        for (int j = 0; j < D; j++) bf.v[j] = a.V[bf.addr[j]];
+        bf.m = a.Mc[(size_t)(a.win_first[w] + slot) * a.stride + b];
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; j++) bf.v[j] = 0;
+        bf.m = 0;
+    }
+}
+
+LDPC_DEV int decode_msg(uint32_t word, int j, int c1o, int c2o, int jmo)
+{
+    const int mag = (jmo == j) ? c1o : c2o;
+    const int sm = ((int)(word << (12 - j))) >> 31;   // bit 19 + j, sign-extended
+    return (mag ^ sm) - sm;
+}
+
+// post: new messages and V for all D edges; returns nothing.
+template <int D>
+LDPC_DEV void post_store(const W2Args &a, const Buf<D> &bf, const int (&c)[D], const int (&av)[D], int min1,
+                         int min2, int sacc, int off, int cst_hi_fn_dummy, bool act, bool odead, size_t mc_idx,
+                         int cst1, int cst2)
+{
+    (void)cst_hi_fn_dummy;
+    (void)min2;
+    const int P = sacc ^ ((D & 1) ? (int)0x80000000 : 0);
+    uint32_t nw = (uint32_t)cst1 | ((uint32_t)cst2 << 7);
+    int jmin = 0;
+#pragma unroll
+    for (int j = 0; j < D; j++) {
+        const bool eq = av[j] == min1;
+        const int r = eq ? cst1 : cst2;
+        jmin = eq ? j : jmin;
+        const int t = c[j] ^ P;
+        const int sm = t >> 31;
+        const int lsb = (int)((uint32_t)t >> 31);
+        nw |= (uint32_t)lsb << (19 + j);
+        const int vn = med3(c[j] + (r ^ sm) + lsb, -127, 127);
+        if (act && (j != D - 1 || !odead)) a.V[bf.addr[j]] = (int8_t)vn;
+    }
+    nw |= (uint32_t)jmin << 14;
+    if (act) a.Mc[mc_idx] = nw;
+    (void)off;
+}
+
+// ---- one window of the first degree group (fast OMS path)
+template <int D, int S>
+LDPC_DEV int win_fast(const Buf<D> &bf, const W2Args &a, int w, int slot, int b, int carry, bool live)
+{
+    constexpr int X = D - 2, O = D - 1;
+    const int fl = a.flags[w * S + slot];
+    const bool act = (fl & F_ACT) && live;
+    const int off = a.off, mm = a.msg_max;
+    const int cnt = a.win_cnt[w];
+    const uint32_t word = bf.m;
+    const int c1o = (int)(word & 127), c2o = (int)((word >> 7) & 127), jmo = (int)((word >> 14) & 31);
+    int c[D], av[D];
+    int min1 = 127, min2 = 127, sacc = 0;
+#pragma unroll
+    for (int j = 0; j < X; j++) {   // info edges
+        const int cj = med3(bf.v[j] - decode_msg(word, j, c1o, c2o, jmo), -127, 127);
+        const int aj = med3(cj, -cj, mm);
+        c[j] = cj;
+        av[j] = aj;
+        sacc ^= cj;
+        min2 = med3(aj, min1, min2);
+        min1 = min(aj, min1);
+    }
+    const int T = max(min1 - off, 0);                    // cst(min over info edges)
+    const int kbit = (int)(((uint32_t)sacc >> 31) ^ (D & 1));   // eps = -1 when set
+    {
+        const int co = med3(bf.v[O] - decode_msg(word, O, c1o, c2o, jmo), -127, 127);
+        const int ao = med3(co, -co, mm);
+        c[O] = co;
+        av[O] = ao;
+        sacc ^= co;
+        min2 = med3(ao, min1, min2);
+        min1 = min(ao, min1);
+    }
+    const int mx = decode_msg(word, X, c1o, c2o, jmo);
+    // rho_k = eps_k * rho_{k-1}, rho_{-1} = +1 (the carry enters as a plain V value)
+    const int rbit = xor_scan<S>(kbit);
+    const int rho = 1 - 2 * rbit, rho_prev = 1 - 2 * (rbit ^ kbit);
+    const int tau = -rho_prev * mx;
+    const int C = rho * c[O];
+    const int dprev = shift1<S>(0, C) + tau;
+    const int y0 = (fl & F_XIN) ? carry : bf.v[X];       // slot 0's chain input
+    int u = rho_prev * y0 + tau;                         // only lane 0's value matters
+    u = chain_steps<S>(u, dprev, off, T);
+    // carry out: y of the window's last check (clamped: a plain V value)
+    const int zk = C + med3(u - med3(u, -off, off), -T, T);
+    const int ylast = med3(rho * zk, -127, 127);
+    const int new_carry = __shfl(ylast, (int)(threadIdx.x & (64 - S)) + cnt - 1, 64);
+    // post: the chain input of this check, then all edges
+    {
+        const int yin = med3(rho_prev * (u - tau), -127, 127);
+        const int cx = med3(yin - mx, -127, 127);
+        const int ax = med3(cx, -cx, mm);
+        c[X] = cx;
+        av[X] = ax;
+        sacc ^= cx;
+        min2 = med3(ax, min1, min2);
+        min1 = min(ax, min1);
+    }
+    const int cst1 = max(min2 - off, 0), cst2 = max(min1 - off, 0);
+    post_store<D>(a, bf, c, av, min1, min2, sacc, off, 0, act, fl & F_ODEAD,
+                  (size_t)(a.win_first[w] + slot) * a.stride + b, cst1, cst2);
+    return new_carry;
+}
+
+// ---- exact general step (later degree group: |min(c, msg_max)| quirk);
+// serial over the window's slots with a per-step commit.
+template <int D, int S>
+LDPC_DEV int win_exact_later(const Buf<D> &bf, const W2Args &a, int w, int slot, int b, int carry, bool live)
+{
+    constexpr int X = D - 2, O = D - 1;
+    const int fl = a.flags[w * S + slot];
+    const bool act = (fl & F_ACT) && live;
+    const int off = a.off, mm = a.msg_max;
+    const int cnt = a.win_cnt[w];
+    const uint32_t word = bf.m;
+    const int c1o = (int)(word & 127), c2o = (int)((word >> 7) & 127), jmo = (int)((word >> 14) & 31);
+    int c[D], av[D];
+    int min1 = 127, min2 = 127, sacc = 0;
+    auto cst = [&](int v) { return min(max(v - off, 0), mm); };
+#pragma unroll
+    for (int j = 0; j < D; j++) {
+        if (j == X) continue;
+        const int cj = med3(bf.v[j] - decode_msg(word, j, c1o, c2o, jmo), -127, 127);
+        const int aj = abs(min(cj, mm));
+        c[j] = cj;
+        av[j] = aj;
+        sacc ^= cj;
+        min2 = med3(aj, min1, min2);
+        min1 = min(aj, min1);
+    }
+    int i1 = 127, s2 = 0;
+#pragma unroll
+    for (int j = 0; j < X; j++) {
+        i1 = min(i1, av[j]);
+        s2 ^= c[j];
+    }
+    const int T = cst(i1);
+    const int kpar = (int)(((uint32_t)s2 >> 31) ^ (D & 1));
+    const int mx = decode_msg(word, X, c1o, c2o, jmo);
+    const int co = c[O];
+    const int vx = bf.v[X];
+    const bool has_x = fl & F_XIN;
+    int y = 0;
+    for (int k = 0; k < cnt; k++) {
+        const int t = shift1<S>(carry, y);
+        const int cx = med3((has_x ? t : vx) - mx, -127, 127);
+        const int r = min(max(abs(min(cx, mm)) - off, 0), T);
+        const int neg = (cx < 0) ^ kpar;
+        const int yn = med3(co + (neg ? -r : r), -127, 127);
+        y = (slot == k) ? yn : y;
+    }
+    const int t = shift1<S>(carry, y);
+    const int new_carry = __shfl(y, (int)(threadIdx.x & (64 - S)) + cnt - 1, 64);
+    {
+        const int cx = med3((has_x ? t : vx) - mx, -127, 127);
+        const int ax = abs(min(cx, mm));
+        c[X] = cx;
+        av[X] = ax;
+        sacc ^= cx;
+        min2 = med3(ax, min1, min2);
+        min1 = min(ax, min1);
+    }
+    post_store<D>(a, bf, c, av, min1, min2, sacc, off, 0, act, fl & F_ODEAD,
+                  (size_t)(a.win_first[w] + slot) * a.stride + b, cst(min2), cst(min1));
+    return new_carry;
+}
+
+// windows [wb, we) of one degree group, software-pipelined with read-ahead P
+template <int D, int S, int P, bool FAST>
+LDPC_DEV int run_group(const W2Args &a, int wb, int we, int slot, int b, int carry, bool live)
+{
+    Tab<D> T[2];
+    Buf<D> B[P + 1];
+    // prologue: tables for wb..wb+P, buffers for wb..wb+P-1
+#pragma unroll
+    for (int i = 0; i < P; i++)
+        if (wb + i < we) {
+            load_tab<D, S>(T[i % 2], a, wb + i, slot);
+            load_buf<D, S>(B[i], T[i % 2], a, wb + i, slot, b);
+        }
+    if (wb + P < we) load_tab<D, S>(T[P % 2], a, wb + P, slot);
+    auto step = [&](auto sc, int t) {
+        constexpr int s = decltype(sc)::value;
+        if (t + P + 1 < we) load_tab<D, S>(T[(s + P + 1) % 2], a, t + P + 1, slot);
+        if (t + P < we) load_buf<D, S>(B[(s + P) % (P + 1)], T[(s + P) % 2], a, t + P, slot, b);
+        if constexpr (FAST)
+            carry = win_fast<D, S>(B[s % (P + 1)], a, t, slot, b, carry, live);
+        else
+            carry = win_exact_later<D, S>(B[s % (P + 1)], a, t, slot, b, carry, live);
+    };
+    constexpr int U = (P == 1) ? 2 : 6;   // lcm(2, P + 1)
+    for (int t = wb; t < we; t += U) {
+        step(std::integral_constant<int, 0>{}, t);
+        if (t + 1 < we) step(std::integral_constant<int, 1>{}, t + 1);
+        if constexpr (U == 6) {
+            if (t + 2 < we) step(std::integral_constant<int, 2>{}, t + 2);
+            if (t + 3 < we) step(std::integral_constant<int, 3>{}, t + 3);
+            if (t + 4 < we) step(std::integral_constant<int, 4>{}, t + 4);
+            if (t + 5 < we) step(std::integral_constant<int, 5>{}, t + 5);
+        }
+    }
+    return carry;
+}
+
+template <int D, int S>
+LDPC_DEV int syndrome_part(const W2Args &a, int wb, int we, int slot, int b)
+{
+    int bad = 0;
+    for (int w = wb; w < we; w++) {
+        if (!(a.flags[w * S + slot] & F_ACT)) continue;
+        const uint32_t *p = a.slotvar + a.slotoff[w] + slot;
+        int par = 0;
+#pragma unroll
+        for (int j = 0; j < D; j++) par ^= (a.V[p[j * S] * (uint32_t)a.stride + b] > 0);
+        bad |= par;
+    }
+    return bad;
+}
+
+template <int D0, int S, int P>
+__global__ void __launch_bounds__(64) windowed2_decode(W2Args a)
+{
+    constexpr int G = 64 / S;
+    const int nb = gridDim.x, id = blockIdx.x;
+    const int wave = (id % 8) * (nb / 8) + id / 8;   // XCD-aware: neighbours share an XCD
+    const int slot = threadIdx.x & (S - 1), row = threadIdx.x / S;
+    const int b = wave * G + row;
+    int carry = a.V[a.slotvar[a.slotoff[0] + (D0 - 2) * S] * (uint32_t)a.stride + b];
+    bool live = true;
+    int it = 0;
+    while (it < a.iters) {
+        carry = run_group<D0, S, P, true>(a, 0, a.g0_end, slot, b, carry, live);
+        carry = run_group<D0 - 1, S, 1, false>(a, a.g0_end, a.n_windows, slot, b, carry, live);
+        it++;
+        if (a.early) {
+            if (live) {
+                int bad = syndrome_part<D0, S>(a, 0, a.g0_end, slot, b) |
+                          syndrome_part<D0 - 1, S>(a, a.g0_end, a.n_windows, slot, b);
+                for (int m = 1; m < S; m <<= 1) bad |= __shfl_xor(bad, m, 64);
+                if (!bad) {
+                    live = false;
+                    if (slot == 0 && a.iters_used) a.iters_used[b] = it;
+                }
+            }
+            if (!__any(live)) break;
+        }
+    }
+    if (live && slot == 0 && a.iters_used) a.iters_used[b] = it;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host side
+
+bool windowed2_params_ok(const ldpc_params *p)
+{
+    return (p->algo == LDPC_ALGO_OMS || p->algo == LDPC_ALGO_MS) && p->var_min == -127 && p->var_max == 127 &&
+           p->msg_max >= 0 && p->msg_max <= 63 && (p->algo == LDPC_ALGO_MS || (p->offset >= 0 && p->offset <= 63));
+}
+
+int windowed2_upload(const ldpc_code *h, int S, int P, Windowed2Code *w)
+{
+    *w = Windowed2Code{};
+    std::vector<ldpc_window> wins;
+    if (!(h->staircase && h->n_groups == 2 && h->group_deg[1] == h->group_deg[0] - 1 &&
+          (h->group_deg[0] == 7 || h->group_deg[0] == 10)))
+        return LDPC_OK;
+    extern int ldpc_plan_windows(const ldpc_code *h, int S, int P, std::vector<ldpc_window> &out);
+    if (ldpc_plan_windows(h, S, P, wins) != LDPC_OK || wins.empty()) return LDPC_OK;
+    const int nw = (int)wins.size();
+    std::vector<uint32_t> slotvar, slotoff(nw);
+    std::vector<uint8_t> flags((size_t)nw * S, 0);
+    std::vector<int> first(nw), cnt(nw);
+    int g0_end = nw;
+    for (int i = 0; i < nw; i++) {
+        const int c0 = wins[i].first;
+        const int d = h->check_deg[c0];
+        if (h->check_group[c0] != 0 && g0_end == nw) g0_end = i;
+        first[i] = c0;
+        cnt[i] = wins[i].count;
+        slotoff[i] = (uint32_t)slotvar.size();
+        slotvar.resize(slotvar.size() + (size_t)d * S, 0u);
+        for (int k = 0; k < wins[i].count; k++) {
+            const int c = c0 + k;
+            const uint32_t *ev = &h->edge_var[h->check_start[c]];
+            for (int j = 0; j < d; j++) slotvar[slotoff[i] + j * S + k] = ev[j];
+            uint8_t f = F_ACT;
+            if (h->chain_in[c] >= 0) f |= F_XIN;
+            if (h->chain_out[c] >= 0 && c + 1 < h->m) f |= F_ODEAD;
+            flags[(size_t)i * S + k] = f;
+        }
+    }
+    auto up = [&](void **dst, const void *src, size_t bytes) {
+        if (hipMalloc(dst, bytes) != hipSuccess) return false;
+        return hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+    };
+    if (!up((void **)&w->d_slotvar, slotvar.data(), slotvar.size() * 4) ||
+        !up((void **)&w->d_slotoff, slotoff.data(), slotoff.size() * 4) ||
+        !up((void **)&w->d_flags, flags.data(), flags.size()) || !up((void **)&w->d_first, first.data(), nw * 4) ||
+        !up((void **)&w->d_cnt, cnt.data(), nw * 4)) {
+        windowed2_free(w);
+        return ldpc_set_error(LDPC_ENOMEM, "windowed2 tables");
+    }
+    w->valid = 1;
+    w->S = S;
+    w->P = P;
+    w->d0 = h->group_deg[0];
+    w->n_windows = nw;
+    w->g0_end = g0_end;
+    return LDPC_OK;
+}
+
+void windowed2_free(Windowed2Code *w)
+{
+    (void)hipFree(w->d_slotvar);
+    (void)hipFree(w->d_slotoff);
+    (void)hipFree(w->d_flags);
+    (void)hipFree(w->d_first);
+    (void)hipFree(w->d_cnt);
+    *w = Windowed2Code{};
+}
+
+template <int D0, int S, int P>
+static int launch3(const W2Args &a, int grid, hipStream_t s)
+{
+    hipLaunchKernelGGL((windowed2_decode<D0, S, P>), dim3(grid), dim3(64), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_windowed2(const DecodeLaunch &L, const Windowed2Code &w, hipStream_t s)
+{
+    if (!w.valid) return -1;
+    W2Args a;
+    a.V = (int8_t *)L.V;
+    a.Mc = (uint32_t *)L.msg;
+    a.stride = L.stride;
+    a.iters = L.iters;
+    a.slotvar = w.d_slotvar;
+    a.slotoff = w.d_slotoff;
+    a.flags = w.d_flags;
+    a.win_first = w.d_first;
+    a.win_cnt = w.d_cnt;
+    a.g0_end = w.g0_end;
+    a.n_windows = w.n_windows;
+    a.off = L.param;
+    a.msg_max = L.msg_max;
+    a.early = L.early;
+    a.iters_used = L.iters_used;
+    const int G = 64 / w.S;
+    const int grid = L.stride / G;   // stride % 64 == 0 -> grid % 8 == 0
+    if (w.S == 32) {
+        if (w.d0 == 7) return launch3<7, 32, 1>(a, grid, s);
+        if (w.d0 == 10) return launch3<10, 32, 1>(a, grid, s);
+    } else {
+        if (w.d0 == 7) return launch3<7, 16, 2>(a, grid, s);
+        if (w.d0 == 10) return launch3<10, 16, 2>(a, grid, s);
+    }
+    return -1;
+}

@@ -80,6 +80,9 @@ def decode(table, llr, iters, offset=1, vmin=-127, mm=31):
                 T = cst(i1)
                 has_x = np.array([table_has_chain_in(table, ev, starts, degs, first + k) for k in range(n)])
                 ys = np.zeros((B, n), np.int64)
+                carry_in = carry
+                m_x0 = m_old[:, :, X].copy()
+                co0 = c[:, :, O].copy()
                 for k in range(n):
                     yin = carry if (has_x[k] and carry is not None) else vv[:, k, X]
                     cx = clamp(yin - m_old[:, k, X], vmin, 127)
@@ -89,7 +92,9 @@ def decode(table, llr, iters, offset=1, vmin=-127, mm=31):
                     ys[:, k] = clamp(c[:, k, O] + np.where(neg == 1, -r, r), vmin, 127)
                     carry = ys[:, k]
                     c[:, k, X] = cx
-                a = np.abs(np.minimum(c, mm)) if later else np.minimum(np.abs(c), mm)
+                if not later and vmin == -127 and mm <= 63:
+                    check_zchain(vv[:, :, X], m_x0, co0, T, s2, has_x, carry_in, ys, offset, n)
+                a =np.abs(np.minimum(c, mm)) if later else np.minimum(np.abs(c), mm)
                 # post
                 m1 = a.min(axis=2)
                 srt = np.sort(a, axis=2)
@@ -106,6 +111,37 @@ def decode(table, llr, iters, offset=1, vmin=-127, mm=31):
                 c1[chk], c2[chk], jm[chk] = k1.T, k2.T, jmin.T
                 sg[chk, :, :D] = neg.transpose(1, 0, 2)
     return (V > 0).astype(np.uint8), V.astype(np.int8)
+
+
+def dz(u, off, T):
+    """sign(u) * clamp(|u| - off, 0, T) == med3(u - med3(u, -off, off), -T, T)."""
+    s = u - clamp(u, -off, off)
+    return clamp(s, -T, T)
+
+
+def check_zchain(vx, mx, co, T, s2, has_x, carry_in, ys, off, n):
+    """The kernel's sign-normalised chain (windowed.hip, "z-domain"):
+    y_k = co_k + eps_k dz(y_{k-1} - mx_k), eps_k = -1 if kpar_k else +1.
+    With rho_k = eps_k rho_{k-1} and z_k = rho_k y_k:
+      z_k = C_k + dz(u_k),  u_k = z_{k-1} + tau_k,
+      C_k = rho_k co_k,  tau_k = -rho_{k-1} mx_k,
+    so every step is med3 / sub / med3 / add.  Chain values are left
+    unclamped (|y| <= 127 + T); clamping would not change any dz input that
+    matters because |y - mx| >= 127 - msg_max > T + off there."""
+    B = vx.shape[0]
+    eps = np.where(s2 == 1, -1, 1)                  # [B, n]
+    y_in = np.where(has_x[0] and carry_in is not None, carry_in if carry_in is not None else 0, vx[:, 0])
+    rho_prev = np.ones(B, np.int64)
+    z_prev = y_in * rho_prev
+    for k in range(n):
+        rho = eps[:, k] * rho_prev
+        tau = -rho_prev * mx[:, k]
+        u = z_prev + tau
+        z = rho * co[:, k] + dz(u, off, T[:, k])
+        y = rho * z
+        assert np.array_equal(clamp(y, -127, 127), ys[:, k]), "z-domain chain mismatch at slot %d" % k
+        # the kernel recovers the chain input of slot k from u: y_{k-1} = rho_{k-1} (u_k - tau_k)
+        z_prev, rho_prev = z, rho
 
 
 def table_has_chain_in(table, ev, starts, degs, ci):
