@@ -34,7 +34,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="codewords per GPU")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--ebn0", type=float, default=1.0, help="Eb/N0 (dB) of the synthetic channel")
-    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 generic, 2 windowed")
+    ap.add_argument("--kernel", type=int, default=0,
+                    help="0 auto, 1 generic, 2 windowed, 3 windowed2 S=16, 4 windowed2 S=32")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
@@ -90,6 +91,7 @@ def main():
     torch.cuda.set_device(local)
 
     from ldpcgputegra_amd import Code, Decoder, channel, default_params
+    from ldpcgputegra_amd.shard import reduce_results, shard_range
     code = Code(a.code)
     dec = Decoder(code, device=local, max_batch=a.batch, kernel=a.kernel)
     B, N = a.batch, code.n
@@ -99,7 +101,8 @@ def main():
     hard = torch.empty((B, N), dtype=torch.uint8, device="cuda")
     counts = torch.zeros(2, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
-    dec.awgn_i8_device(llr, first_cw=rank * B, seed=a.seed, table=table, stream=stream)
+    first_cw, _ = shard_range(rank, world, B * world)      # contiguous shard per rank
+    dec.awgn_i8_device(llr, first_cw=first_cw, seed=a.seed, table=table, stream=stream)
     params = default_params()
 
     def step():
@@ -125,13 +128,9 @@ def main():
     kms, launches = dec.kernel_time(reset=True)
     dec.profile(False)
 
-    stats = torch.tensor([el, kms / max(launches, 1)], dtype=torch.float64, device="cuda")
-    cnt = counts.clone()
-    if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-    el, kernel_ms = stats.tolist()
-    be, fe = cnt.tolist()
+    be_l, fe_l = counts.tolist()
+    el, be, fe, _ = reduce_results(el, be_l, fe_l, B * a.steps, device="cuda")
+    kernel_ms, _, _, _ = reduce_results(kms / max(launches, 1), 0, 0, 0, device="cuda")
 
     if rank == 0:
         frames = world * B * a.steps
@@ -143,7 +142,7 @@ def main():
         traffic = None
         try:
             tr = json.load(open(a.traffic_file))
-            key = "%s_b%d_it%d_k%d" % (a.code, B, a.iters, dec.kernel)
+            key = "%s_b%d_it%d_%s" % (a.code, B, a.iters, dec.last_kernel)
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -164,7 +163,7 @@ def main():
                 "workload": "DVB-S2 N=64800 r=1/2 layered int8 offset-min-sum (offset 1), %d iters, batch %d "
                             "codewords per GPU" % (a.iters, B),
                 "code": a.code, "batch_per_gpu": B, "global_batch": B * world, "iters": a.iters,
-                "ebn0_db": a.ebn0, "kernel": ["auto", "generic", "windowed"][a.kernel],
+                "ebn0_db": a.ebn0, "kernel": dec.last_kernel,
                 "parallelism": "codeword shards x%d (no collective)" % world,
             },
             "ber": be / max(frames * code.k_info, 1),

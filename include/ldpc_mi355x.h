@@ -130,6 +130,9 @@ int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
  * 2 = windowed layered kernel (compressed messages). */
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
+/* Kernel family the last decode actually ran (1 generic, 2 windowed,
+ * 3 windowed2 S=16, 4 windowed2 S=32; 0 before the first decode). */
+int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel timing (bench / profiling): when enabled, every decode records HIP
  * events around the decode kernel on the stream it is launched on;
  * ldpc_ctx_kernel_time returns the summed kernel time and launch count since

@@ -52,6 +52,7 @@ SIGNATURES = {
     "ldpc_ctx_stream": (I, [P, C.POINTER(P)]),
     "ldpc_ctx_set_kernel": (I, [P, I]),
     "ldpc_ctx_get_kernel": (I, [P, C.POINTER(I)]),
+    "ldpc_ctx_last_kernel": (I, [P, C.POINTER(I)]),
     "ldpc_ctx_profile": (I, [P, I]),
     "ldpc_ctx_kernel_time": (I, [P, C.POINTER(C.c_double), C.POINTER(I), I]),
     "ldpc_decode_i8": (I, [P, P, P, I, I, C.POINTER(ldpc_params)]),

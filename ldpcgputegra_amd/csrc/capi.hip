@@ -29,7 +29,8 @@ struct ldpc_ctx {
     int device = 0;
     int max_batch = 0;
     int max_stride = 0;
-    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed
+    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32
+    int last_kernel = 0;
     hipStream_t stream = nullptr;
     // device copy of the code
     uint32_t *d_edge_var = nullptr;
@@ -180,6 +181,13 @@ extern "C" int ldpc_ctx_kernel_time(ldpc_ctx *c, double *total_ms, int *launches
     return LDPC_OK;
 }
 
+extern "C" int ldpc_ctx_last_kernel(ldpc_ctx *c, int *k)
+{
+    if (!c || !k) return ldpc_set_error(LDPC_EINVAL, "NULL");
+    *k = c->last_kernel;
+    return LDPC_OK;
+}
+
 extern "C" int ldpc_ctx_get_kernel(ldpc_ctx *c, int *k)
 {
     if (!c || !k) return ldpc_set_error(LDPC_EINVAL, "NULL");
@@ -240,6 +248,7 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     if (kern < 0)
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d selected but not applicable to these params", c->kernel);
     const bool win = kern >= 2;
+    c->last_kernel = kern;
     const size_t msg_need = win ? windowed_msg_bytes(h, stride) : (size_t)h->e * stride * esz;
     if ((rc = ensure(&c->d_V, &c->V_bytes, (size_t)h->n * stride * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&c->d_msg, &c->msg_bytes, msg_need)) != LDPC_OK) return rc;

@@ -60,6 +60,14 @@ class Decoder:
         _lib.check(_lib.lib().ldpc_ctx_kernel_time(self._ctx, C.byref(ms), C.byref(n), int(reset)))
         return ms.value, n.value
 
+    KERNEL_NAMES = {0: "none", 1: "generic", 2: "windowed", 3: "windowed2_s16", 4: "windowed2_s32"}
+
+    @property
+    def last_kernel(self):
+        k = C.c_int()
+        _lib.check(_lib.lib().ldpc_ctx_last_kernel(self._ctx, C.byref(k)))
+        return self.KERNEL_NAMES.get(k.value, str(k.value))
+
     @property
     def stream(self):
         s = C.c_void_p()

@@ -1,0 +1,78 @@
+"""N > 1 path on the CPU: world_size-2 gloo processes shard a batch of
+codewords exactly as bench.py does (contiguous shards, inputs regenerated from
+(seed, first codeword)), decode their shard (CPU oracle standing in for the
+GPU here), and reduce only counters and time.  Shard invariance: the union of
+the shards equals the single-process decode bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from ldpcgputegra_amd.shard import reduce_results, shard_range
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch.distributed as dist
+    import oracle as O
+    from ldpcgputegra_amd import channel, load_table
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = load_table("576x288")
+    table = channel.i8_table(channel.sigma_from_ebn0(1.5, 0.5))
+    first, count = shard_range(rank, world, total)
+    llr = channel.awgn_i8_host(t.n, count, seed=9, table=table, first_cw=first)
+    hard = O.decode_i8(t, llr, 10)
+    be = int(hard[:, :t.k_info].sum())
+    fe = int((hard[:, :t.k_info].sum(axis=1) > 0).sum())
+    el, BE, FE, FR = reduce_results(0.1 * (rank + 1), be, fe, count)
+    np.save(os.path.join(out_dir, "hard_%d.npy" % rank), hard)
+    np.save(os.path.join(out_dir, "red_%d.npy" % rank), np.array([el, BE, FE, FR]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range_covers_batch():
+    for total in (1, 7, 4096, 32768):
+        for world in (1, 2, 3, 8):
+            got = [shard_range(r, world, total) for r in range(world)]
+            assert got[0][0] == 0
+            for (f, c), (f2, _) in zip(got, got[1:]):
+                assert f + c == f2
+            assert sum(c for _, c in got) == total
+            assert max(c for _, c in got) - min(c for _, c in got) <= 1
+
+
+def test_two_rank_gloo_shards_match_single_process(tmp_path):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import oracle as O
+    from ldpcgputegra_amd import channel, load_table
+    total = 10
+    mp.start_processes(_worker, args=(2, _free_port(), total, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    hard = np.concatenate([np.load(tmp_path / ("hard_%d.npy" % r)) for r in range(2)])
+    t = load_table("576x288")
+    table = channel.i8_table(channel.sigma_from_ebn0(1.5, 0.5))
+    ref = O.decode_i8(t, channel.awgn_i8_host(t.n, total, seed=9, table=table), 10)
+    assert np.array_equal(hard, ref)
+    red = [np.load(tmp_path / ("red_%d.npy" % r)) for r in range(2)]
+    assert np.array_equal(red[0], red[1])                   # every rank sees the reduced values
+    el, be, fe, fr = red[0]
+    assert el == pytest.approx(0.2)                         # max over ranks
+    assert fr == total and be == ref[:, :t.k_info].sum()
