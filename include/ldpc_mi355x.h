@@ -155,6 +155,11 @@ int ldpc_decode_f32_async(ldpc_ctx *ctx, void *hip_stream, const float *d_llr, u
                           float *d_soft, int32_t *d_iters_used, int batch, int n_iter,
                           const ldpc_params *p);
 
+/* DVB-S2 IRA encoder (codes built from an Annex-B table), as the
+ * reference's GenericEncoder::encode (code/x86/CEncoder/GenericEncoder.cpp:38-78):
+ * info [batch][K] 0/1 -> codeword [batch][N] = [info, parity]. */
+int ldpc_dvbs2_encode(const ldpc_code *h, const uint8_t *info, uint8_t *codeword, int batch);
+
 /* ---- synthetic channel -------------------------------------------------- */
 /* sigma = sqrt(10^(-(EbN0 + 10 log10(rate))/10) / 2)  (CChanelAWGN_MKL.cpp:102-105) */
 double ldpc_awgn_sigma(double ebn0_db, double rate);

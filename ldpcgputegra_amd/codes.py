@@ -182,6 +182,13 @@ class Code:
         _lib.check(_lib.lib().ldpc_code_plan_info(self._h, C.byref(s), C.byref(w), C.byref(hz)))
         return dict(staircase=bool(s.value), n_windows=w.value, min_hazard=hz.value, windowed=w.value > 0)
 
+    def encode(self, info):
+        """DVB-S2 IRA encoding of info bits [batch, K] -> codewords [batch, N]."""
+        info = np.ascontiguousarray(info, dtype=np.uint8).reshape(-1, self.k_info)
+        cw = np.empty((info.shape[0], self.n), dtype=np.uint8)
+        _lib.check(_lib.lib().ldpc_dvbs2_encode(self._h, info.ctypes.data, cw.ctypes.data, info.shape[0]))
+        return cw
+
     def window_plan(self, S, P):
         """[(first check, count)] of the windowed2 schedule (empty if none)."""
         L = _lib.lib()

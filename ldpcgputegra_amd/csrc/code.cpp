@@ -176,7 +176,47 @@ extern "C" int ldpc_code_from_dvbs2_table(int n, int k_info, int n_rows, const i
             gcnt.push_back(1);
         }
     }
-    return ldpc_code_create(n, m, (int)gdeg.size(), gdeg.data(), gcnt.data(), edges.data(), out);
+    int rc = ldpc_code_create(n, m, (int)gdeg.size(), gdeg.data(), gcnt.data(), edges.data(), out);
+    if (rc == LDPC_OK) {
+        (*out)->dvbs2_q = q;
+        (*out)->dvbs2_row_len.assign(row_len, row_len + n_rows);
+        long tot = 0;
+        for (int g = 0; g < n_rows; g++) tot += row_len[g];
+        (*out)->dvbs2_row_addr.assign(row_addr, row_addr + tot);
+    }
+    return rc;
+}
+
+// DVB-S2 IRA encoder, as the reference's GenericEncoder::encode
+// (code/x86/CEncoder/GenericEncoder.cpp:38-78): accumulate the Annex-B
+// parity addresses of every set information bit, then the staircase
+// p[j] ^= p[j-1].  codeword = [info (K bits), parity (M bits)].
+extern "C" int ldpc_dvbs2_encode(const ldpc_code *h, const uint8_t *info, uint8_t *codeword, int batch)
+{
+    if (!h || (!info && batch > 0) || (!codeword && batch > 0) || batch < 0)
+        return ldpc_set_error(LDPC_EINVAL, "encode args");
+    if (h->dvbs2_q <= 0) return ldpc_set_error(LDPC_EUNSUPPORTED, "code was not built from a DVB-S2 table");
+    const int n = h->n, m = h->m, k = n - m, q = h->dvbs2_q;
+    for (int b = 0; b < batch; b++) {
+        const uint8_t *in = info + (size_t)b * k;
+        uint8_t *cw = codeword + (size_t)b * n;
+        uint8_t *p = cw + k;
+        memset(p, 0, (size_t)m);
+        const int *addr = h->dvbs2_row_addr.data();
+        for (size_t g = 0; g < h->dvbs2_row_len.size(); g++) {
+            const int len = h->dvbs2_row_len[g];
+            for (int kk = 0; kk < 360; kk++) {
+                const int v = (int)g * 360 + kk;
+                const uint8_t bit = in[v] & 1;
+                cw[v] = bit;
+                if (bit)
+                    for (int t = 0; t < len; t++) p[(addr[t] + (long)kk * q) % m] ^= 1;
+            }
+            addr += len;
+        }
+        for (int j = 1; j < m; j++) p[j] ^= p[j - 1];
+    }
+    return LDPC_OK;
 }
 
 static int load_ldpc_binary(const std::string &data, ldpc_code **out)

@@ -21,6 +21,10 @@ struct ldpc_code {
     // per-check (layered order)
     std::vector<int> check_deg, check_start, check_group;
 
+    // DVB-S2 Annex-B rows when the code was built from a table (encoder)
+    int dvbs2_q = 0;
+    std::vector<int> dvbs2_row_len, dvbs2_row_addr;
+
     // ---- schedule plan for the windowed kernel (plan.cpp) ----
     bool staircase = false;       // check i+1 reads the var check i wrote last (DVB-S2 chain)
     int min_hazard = 0;           // min distance between two touches of one non-chain var

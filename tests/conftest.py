@@ -24,13 +24,14 @@ def golden_cases():
 
 def golden_inputs(case):
     """(llr int8 [B, N], expected hard uint8 [B, N]) for a golden case."""
-    from golden.gen_golden import awgn_i8
+    from golden.gen_golden import awgn_i8, random_codewords
     from ldpcgputegra_amd import load_table
     n = load_table(case["code"]).n
     if "llr_file" in case:
         llr = np.load(os.path.join(GOLDEN, case["llr_file"]))
     else:
-        llr = awgn_i8(n, case["batch"], case["seed"], np.array(case["table"], dtype=np.uint32))
+        cw = random_codewords(case["code"], case["batch"], case["info_seed"]) if "info_seed" in case else None
+        llr = awgn_i8(n, case["batch"], case["seed"], np.array(case["table"], dtype=np.uint32), codeword=cw)
     packed = np.load(os.path.join(GOLDEN, case["name"] + ".npz"))["hard_packed"]
     hard = np.unpackbits(packed, axis=-1, count=n)
     return llr, hard

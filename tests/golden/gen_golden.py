@@ -40,8 +40,16 @@ def splitmix64(x):
     return x ^ (x >> np.uint64(31))
 
 
-def awgn_i8(n, batch, seed, table, first_cw=0):
-    """numpy restatement of ldpc_awgn_i8_host (all-zero codeword)."""
+def random_codewords(code, batch, info_seed):
+    """Random info bits (numpy PCG64, seed info_seed) DVB-S2-encoded by the product encoder."""
+    from ldpcgputegra_amd import Code
+    c = Code(code)
+    info = np.random.default_rng(info_seed).integers(0, 2, size=(batch, c.k_info), dtype=np.uint8)
+    return c.encode(info)
+
+
+def awgn_i8(n, batch, seed, table, first_cw=0, codeword=None):
+    """numpy restatement of ldpc_awgn_i8_host (codeword None = all-zero)."""
     sat = int(table[63])
     idx = (np.arange(batch, dtype=np.uint64)[:, None] + np.uint64(first_cw)) * np.uint64(n) + \
         np.arange(n, dtype=np.uint64)[None, :]
@@ -49,7 +57,10 @@ def awgn_i8(n, batch, seed, table, first_cw=0):
     u = (splitmix64(idx ^ key) >> np.uint64(32)).astype(np.uint64)
     th = np.asarray(table[:2 * sat], dtype=np.uint64)
     cnt = (u[..., None] >= th).sum(axis=-1)
-    return (cnt - sat).astype(np.int8)
+    q = (cnt - sat).astype(np.int8)
+    if codeword is not None:
+        q = np.where(codeword.astype(bool), -q, q).astype(np.int8)
+    return q
 
 
 def sha(a):
@@ -62,11 +73,11 @@ def main():
 
     cases = []
 
-    def add(name, code, llr, iters, algo, param, vmin=-127, mmax=31, store_llr=True, gen=None):
+    def add(name, code, llr, iters, algo, param, vmin=-127, mmax=31, store_llr=True, gen=None, cw=None):
         hard = O.ref_decode(code, llr, iters, algo, param, vmin=vmin, mmax=mmax, mmin=-mmax)
         rec = dict(name=name, code=code, iters=iters, algo=algo, param=param, var_min=vmin, msg_max=mmax,
                    batch=int(llr.shape[0]), llr_sha256=sha(llr), hard_sha256=sha(hard),
-                   bit_errors=int(hard.sum()))
+                   bit_errors=int((hard != (0 if cw is None else cw)).sum()))
         arrays = dict(hard_packed=np.packbits(hard, axis=-1))
         if store_llr:
             rec["llr_file"] = "llr_%s.npy" % rec["llr_sha256"][:16]
@@ -113,6 +124,18 @@ def main():
             gen=gen)
     llr, gen = gen_llr("dvbs2_r1_2", 0.9, 16, seed=5009)
     add("dvbs2_r1_2_eb09_nms29_it20", "dvbs2_r1_2", llr, 20, O.NMS, 29, store_llr=False, gen=gen)
+    # random (non-zero) codewords through the DVB-S2 encoder: sign handling
+    # with both bit values (the reference's -encoder mode, GenericEncoder)
+    for code, ebn0, it in (("dvbs2_r1_2", 0.9, 50), ("dvbs2_r8_9", 4.0, 30)):
+        t = load_table(code)
+        sigma = channel.sigma_from_ebn0(ebn0, t.k_info / t.n)
+        table = channel.i8_table(sigma, 8, 31)
+        cw = random_codewords(code, 16, info_seed=77)
+        llr = awgn_i8(t.n, 16, 7001, table, codeword=cw)
+        assert np.array_equal(llr, channel.awgn_i8_host(t.n, 16, 7001, table, codeword=cw))
+        gen = dict(seed=7001, ebn0=ebn0, sigma=sigma, table=[int(x) for x in table], info_seed=77)
+        add("%s_eb%02d_randcw_oms1_it%d" % (code, int(ebn0 * 10), it), code, llr, it, O.OMS, 1, store_llr=False,
+            gen=gen, cw=cw)
     for code, ebn0 in (("dvbs2_r8_9", 4.0), ("dvbs2_r9_10", 4.4)):
         llr, gen = gen_llr(code, ebn0, 16, seed=6000)
         add("%s_eb%02d_oms1_it30" % (code, int(ebn0 * 10)), code, llr, 30, O.OMS, 1, store_llr=False, gen=gen)

@@ -71,3 +71,21 @@ def test_bad_tables_rejected():
         Code(Table(t.n, t.m, t.groups, bad2))
     with pytest.raises(FileNotFoundError):
         Code("no_such_code")
+
+
+@pytest.mark.parametrize("name", ["dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r8_9", "dvbs2_r9_10"])
+def test_dvbs2_encoder_codewords_satisfy_h(name):
+    c = Code(name)
+    t = load_table(name)
+    rng = np.random.default_rng(3)
+    info = rng.integers(0, 2, size=(3, c.k_info), dtype=np.uint8)
+    cw = c.encode(info)
+    assert np.array_equal(cw[:, :c.k_info], info)
+    assert (t.syndrome(cw) == 0).all()
+    assert cw[:, c.k_info:].any()
+
+
+def test_encoder_requires_dvbs2_table():
+    from ldpcgputegra_amd import LdpcError
+    with pytest.raises(LdpcError):
+        Code("576x288").encode(np.zeros((1, 288), np.uint8))
