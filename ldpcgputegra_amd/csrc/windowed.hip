@@ -390,7 +390,11 @@ void windowed_code_free(WindowedCode *w)
     *w = WindowedCode{};
 }
 
-size_t windowed_msg_bytes(const ldpc_code *h, int stride) { return (size_t)h->m * stride * 4; }
+size_t windowed_msg_bytes(const ldpc_code *h, int stride)
+{
+    // one compressed word per check: 19 header bits + one sign bit per edge
+    return (size_t)h->m * stride * (h->max_deg + 19 <= 32 ? 4 : 8);
+}
 
 int launch_windowed(const DecodeLaunch &L, const WindowedCode &w, hipStream_t s)
 {

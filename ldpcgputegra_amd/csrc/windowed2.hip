@@ -126,11 +126,15 @@ struct Tab {
     uint32_t var[D];
 };
 
+// compressed message word: 19 header bits + one sign bit per edge
+template <int D>
+using MsgT = typename std::conditional<(D + 19 <= 32), uint32_t, uint64_t>::type;
+
 template <int D>
 struct Buf {
     int v[D];
     uint32_t addr[D];
-    uint32_t m;
+    MsgT<D> m;
 };
 
 template <int D, int S>
@@ -149,7 +153,7 @@ LDPC_DEV void load_buf(Buf<D> &bf, const Tab<D> &t, const W2Args &a, int w, int 
     if (a.flags[w * S + slot] & F_ACT) {
 #pragma unroll
         for (int j = 0; j < D; j++) bf.v[j] = a.V[bf.addr[j]];
-        bf.m = a.Mc[(size_t)(a.win_first[w] + slot) * a.stride + b];
+        bf.m = reinterpret_cast<const MsgT<D> *>(a.Mc)[(size_t)(a.win_first[w] + slot) * a.stride + b];
     } else {
 #pragma unroll
         for (int j = 0; j < D; j++) bf.v[j] = 0;
@@ -164,16 +168,22 @@ LDPC_DEV int decode_msg(uint32_t word, int j, int c1o, int c2o, int jmo)
     return (mag ^ sm) - sm;
 }
 
-// post: new messages and V for all D edges; returns nothing.
+LDPC_DEV int decode_msg(uint64_t word, int j, int c1o, int c2o, int jmo)
+{
+    const int mag = (jmo == j) ? c1o : c2o;
+    const int sm = j < 13 ? ((int)((uint32_t)word << (12 - j))) >> 31
+                          : ((int)((uint32_t)(word >> 32) << (44 - j))) >> 31;   // bit 19 + j
+    return (mag ^ sm) - sm;
+}
+
+// post: new messages and V for all D edges
 template <int D>
 LDPC_DEV void post_store(const W2Args &a, const Buf<D> &bf, const int (&c)[D], const int (&av)[D], int min1,
-                         int min2, int sacc, int off, int cst_hi_fn_dummy, bool act, bool odead, size_t mc_idx,
-                         int cst1, int cst2)
+                         int sacc, bool act, bool odead, size_t mc_idx, int cst1, int cst2)
 {
-    (void)cst_hi_fn_dummy;
-    (void)min2;
+    using W = MsgT<D>;
     const int P = sacc ^ ((D & 1) ? (int)0x80000000 : 0);
-    uint32_t nw = (uint32_t)cst1 | ((uint32_t)cst2 << 7);
+    W nw = (W)cst1 | ((W)cst2 << 7);
     int jmin = 0;
 #pragma unroll
     for (int j = 0; j < D; j++) {
@@ -183,13 +193,12 @@ LDPC_DEV void post_store(const W2Args &a, const Buf<D> &bf, const int (&c)[D], c
         const int t = c[j] ^ P;
         const int sm = t >> 31;
         const int lsb = (int)((uint32_t)t >> 31);
-        nw |= (uint32_t)lsb << (19 + j);
+        nw |= (W)lsb << (19 + j);
         const int vn = med3(c[j] + (r ^ sm) + lsb, -127, 127);
         if (act && (j != D - 1 || !odead)) a.V[bf.addr[j]] = (int8_t)vn;
     }
-    nw |= (uint32_t)jmin << 14;
-    if (act) a.Mc[mc_idx] = nw;
-    (void)off;
+    nw |= (W)jmin << 14;
+    if (act) reinterpret_cast<W *>(a.Mc)[mc_idx] = nw;
 }
 
 // ---- one window of the first degree group (fast OMS path)
@@ -201,7 +210,7 @@ LDPC_DEV int win_fast(const Buf<D> &bf, const W2Args &a, int w, int slot, int b,
     const bool act = (fl & F_ACT) && live;
     const int off = a.off, mm = a.msg_max;
     const int cnt = a.win_cnt[w];
-    const uint32_t word = bf.m;
+    const auto word = bf.m;
     const int c1o = (int)(word & 127), c2o = (int)((word >> 7) & 127), jmo = (int)((word >> 14) & 31);
     int c[D], av[D];
     int min1 = 127, min2 = 127, sacc = 0;
@@ -252,8 +261,8 @@ LDPC_DEV int win_fast(const Buf<D> &bf, const W2Args &a, int w, int slot, int b,
         min1 = min(ax, min1);
     }
     const int cst1 = max(min2 - off, 0), cst2 = max(min1 - off, 0);
-    post_store<D>(a, bf, c, av, min1, min2, sacc, off, 0, act, fl & F_ODEAD,
-                  (size_t)(a.win_first[w] + slot) * a.stride + b, cst1, cst2);
+    post_store<D>(a, bf, c, av, min1, sacc, act, fl & F_ODEAD, (size_t)(a.win_first[w] + slot) * a.stride + b,
+                  cst1, cst2);
     return new_carry;
 }
 
@@ -267,7 +276,7 @@ LDPC_DEV int win_exact_later(const Buf<D> &bf, const W2Args &a, int w, int slot,
     const bool act = (fl & F_ACT) && live;
     const int off = a.off, mm = a.msg_max;
     const int cnt = a.win_cnt[w];
-    const uint32_t word = bf.m;
+    const auto word = bf.m;
     const int c1o = (int)(word & 127), c2o = (int)((word >> 7) & 127), jmo = (int)((word >> 14) & 31);
     int c[D], av[D];
     int min1 = 127, min2 = 127, sacc = 0;
@@ -315,8 +324,8 @@ LDPC_DEV int win_exact_later(const Buf<D> &bf, const W2Args &a, int w, int slot,
         min2 = med3(ax, min1, min2);
         min1 = min(ax, min1);
     }
-    post_store<D>(a, bf, c, av, min1, min2, sacc, off, 0, act, fl & F_ODEAD,
-                  (size_t)(a.win_first[w] + slot) * a.stride + b, cst(min2), cst(min1));
+    post_store<D>(a, bf, c, av, min1, sacc, act, fl & F_ODEAD, (size_t)(a.win_first[w] + slot) * a.stride + b,
+                  cst(min2), cst(min1));
     return new_carry;
 }
 
@@ -418,7 +427,7 @@ int windowed2_upload(const ldpc_code *h, int S, int P, Windowed2Code *w)
     *w = Windowed2Code{};
     std::vector<ldpc_window> wins;
     if (!(h->staircase && h->n_groups == 2 && h->group_deg[1] == h->group_deg[0] - 1 &&
-          (h->group_deg[0] == 7 || h->group_deg[0] == 10)))
+          (h->group_deg[0] == 7 || h->group_deg[0] == 10 || h->group_deg[0] == 27 || h->group_deg[0] == 30)))
         return LDPC_OK;
     extern int ldpc_plan_windows(const ldpc_code *h, int S, int P, std::vector<ldpc_window> &out);
     if (ldpc_plan_windows(h, S, P, wins) != LDPC_OK || wins.empty()) return LDPC_OK;
@@ -506,9 +515,13 @@ int launch_windowed2(const DecodeLaunch &L, const Windowed2Code &w, hipStream_t 
     if (w.S == 32) {
         if (w.d0 == 7) return launch3<7, 32, 1>(a, grid, s);
         if (w.d0 == 10) return launch3<10, 32, 1>(a, grid, s);
+        if (w.d0 == 27) return launch3<27, 32, 1>(a, grid, s);
+        if (w.d0 == 30) return launch3<30, 32, 1>(a, grid, s);
     } else {
         if (w.d0 == 7) return launch3<7, 16, 2>(a, grid, s);
         if (w.d0 == 10) return launch3<10, 16, 2>(a, grid, s);
+        if (w.d0 == 27) return launch3<27, 16, 2>(a, grid, s);
+        if (w.d0 == 30) return launch3<30, 16, 2>(a, grid, s);
     }
     return -1;
 }
