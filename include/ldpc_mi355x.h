@@ -155,6 +155,21 @@ int ldpc_decode_f32_async(ldpc_ctx *ctx, void *hip_stream, const float *d_llr, u
                           float *d_soft, int32_t *d_iters_used, int batch, int n_iter,
                           const ldpc_params *p);
 
+/* ---- mixed-rate batches (BASELINE config 5) ---------------------------- */
+/* A batch whose codewords use different codes of equal length N (e.g. the
+ * DVB-S2 normal-frame rates).  One decoder context per code; a decode groups
+ * the codewords by code id, runs the per-code decodes concurrently on their
+ * own streams (forked from / joined back to the caller's stream) and writes
+ * hard decisions (and iterations used) back in batch order.  The reference
+ * has one compile-time code per binary (code/x86/Constantes/constantes_sse.h). */
+typedef struct ldpc_mixed ldpc_mixed;
+int ldpc_mixed_create(const ldpc_code *const *codes, int n_codes, int device, int max_batch, ldpc_mixed **out);
+void ldpc_mixed_destroy(ldpc_mixed *mx);
+/* code_id: HOST array [batch] of indices into `codes`; d_llr/d_hard [batch][N]. */
+int ldpc_decode_i8_mixed_async(ldpc_mixed *mx, void *hip_stream, const int8_t *d_llr, uint8_t *d_hard,
+                               int32_t *d_iters_used, const int32_t *code_id, int batch, int n_iter,
+                               const ldpc_params *p);
+
 /* DVB-S2 IRA encoder (codes built from an Annex-B table), as the
  * reference's GenericEncoder::encode (code/x86/CEncoder/GenericEncoder.cpp:38-78):
  * info [batch][K] 0/1 -> codeword [batch][N] = [info, parity]. */

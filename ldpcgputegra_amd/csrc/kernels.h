@@ -32,6 +32,10 @@ int launch_deinterleave_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, 
 int launch_deinterleave_f32(const float *V, uint8_t *hard, float *soft, int n, int batch, int stride,
                             hipStream_t s);
 
+// rows of `row_bytes` bytes: dst[i] = src[idx[i]] (gather) / dst[idx[i]] = src[i] (scatter)
+int launch_gather_rows(const void *src, void *dst, const int32_t *idx, int rows, int row_bytes, hipStream_t s);
+int launch_scatter_rows(const void *src, void *dst, const int32_t *idx, int rows, int row_bytes, hipStream_t s);
+
 int launch_awgn_i8(int8_t *llr, int n, int batch, uint64_t first_cw, uint64_t seed, const AwgnTable &t,
                    const uint8_t *codeword, hipStream_t s);
 int launch_count_errors(const uint8_t *hard, int n, int batch, int k, const uint8_t *ref,

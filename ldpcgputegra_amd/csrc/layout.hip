@@ -100,6 +100,22 @@ __global__ void __launch_bounds__(256) count_errors_k(const uint8_t *__restrict_
     }
 }
 
+// one block per row; 16-B vector copies when the row allows it
+__global__ void __launch_bounds__(256) copy_rows_k(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                   const int32_t *__restrict__ idx, int row_bytes, int scatter)
+{
+    const int r = blockIdx.x;
+    const size_t so = (size_t)(scatter ? r : idx[r]) * row_bytes;
+    const size_t dof = (size_t)(scatter ? idx[r] : r) * row_bytes;
+    if ((row_bytes & 15) == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+        const uint4 *s4 = (const uint4 *)(src + so);
+        uint4 *d4 = (uint4 *)(dst + dof);
+        for (int i = threadIdx.x; i < row_bytes / 16; i += 256) d4[i] = s4[i];
+    } else {
+        for (int i = threadIdx.x; i < row_bytes; i += 256) dst[dof + i] = src[so + i];
+    }
+}
+
 inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -1; }
 
 }  // namespace
@@ -137,6 +153,20 @@ int launch_awgn_i8(int8_t *llr, int n, int batch, uint64_t first_cw, uint64_t se
     int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(awgn_i8_k, dim3(blocks), dim3(256), 0, s, llr, n, batch, first_cw, seed, t, codeword);
+    return ok();
+}
+int launch_gather_rows(const void *src, void *dst, const int32_t *idx, int rows, int row_bytes, hipStream_t s)
+{
+    if (rows <= 0) return 0;
+    hipLaunchKernelGGL(copy_rows_k, dim3(rows), dim3(256), 0, s, (const uint8_t *)src, (uint8_t *)dst, idx,
+                       row_bytes, 0);
+    return ok();
+}
+int launch_scatter_rows(const void *src, void *dst, const int32_t *idx, int rows, int row_bytes, hipStream_t s)
+{
+    if (rows <= 0) return 0;
+    hipLaunchKernelGGL(copy_rows_k, dim3(rows), dim3(256), 0, s, (const uint8_t *)src, (uint8_t *)dst, idx,
+                       row_bytes, 1);
     return ok();
 }
 int launch_count_errors(const uint8_t *hard, int n, int batch, int k, const uint8_t *ref,

@@ -140,6 +140,35 @@ class Decoder:
         self.close()
 
 
+class MixedDecoder:
+    """Mixed-rate batches (codes of equal N, e.g. the DVB-S2 normal-frame
+    rates): per-code contexts decoding their codewords concurrently."""
+
+    def __init__(self, codes, device=0, max_batch=4096):
+        self.codes = [c if isinstance(c, Code) else Code(c) for c in codes]
+        arr = (C.c_void_p * len(self.codes))(*[c.handle for c in self.codes])
+        h = C.c_void_p()
+        _lib.check(_lib.lib().ldpc_mixed_create(arr, len(self.codes), device, max_batch, C.byref(h)))
+        self._mx = h
+        self.n = self.codes[0].n
+
+    def decode_i8_device(self, llr, hard, code_id, n_iter, params=None, iters_used=None, stream=None):
+        """llr/hard: device tensors [B, N]; code_id: host int array [B]."""
+        ids = np.ascontiguousarray(code_id, dtype=np.int32)
+        p = params or _lib.default_params()
+        _lib.check(_lib.lib().ldpc_decode_i8_mixed_async(
+            self._mx, Decoder._torch_stream(stream), Decoder._ptr(llr), Decoder._ptr(hard),
+            Decoder._ptr(iters_used), ids.ctypes.data, ids.size, n_iter, C.byref(p)))
+
+    def close(self):
+        if getattr(self, "_mx", None) is not None and _lib._lib is not None:
+            _lib._lib.ldpc_mixed_destroy(self._mx)
+            self._mx = None
+
+    def __del__(self):
+        self.close()
+
+
 # ---------------------------------------------------------------------------
 # Reference-shaped mirror (CDecoder hierarchy + CreateDecoder factory)
 

@@ -193,3 +193,37 @@ def test_dvbs2_full_batch_properties():
     sel = llr[::256].cpu().numpy()
     exp = O.decode_i8(t, sel, 50)
     assert np.array_equal(h1[::256].cpu().numpy(), exp)
+
+
+def test_mixed_rate_batch_with_early_termination():
+    """BASELINE config 5 shape: one batch mixing DVB-S2 rates 1/2, 2/3, 8/9,
+    9/10 (3/4 and 5/6 tables are absent from the reference), random
+    codewords, early termination.  Every codeword must equal the oracle's
+    decode under its own code (hard decisions and iterations used)."""
+    torch = _torch()
+    from ldpcgputegra_amd.decoder import MixedDecoder
+    names = ["dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r8_9", "dvbs2_r9_10"]
+    ebn0 = {"dvbs2_r1_2": 1.0, "dvbs2_r2_3": 2.2, "dvbs2_r8_9": 4.0, "dvbs2_r9_10": 4.4}
+    mx = MixedDecoder(names, max_batch=64)
+    B = 24
+    ids = np.array([i % 4 for i in range(B)], np.int32)
+    np.random.default_rng(4).shuffle(ids)
+    llr = np.empty((B, 64800), np.int8)
+    for c, name in enumerate(names):
+        code = Code(name)
+        sel = np.where(ids == c)[0]
+        info = np.random.default_rng(c).integers(0, 2, size=(sel.size, code.k_info), dtype=np.uint8)
+        cw = code.encode(info)
+        table = channel.i8_table(channel.sigma_from_ebn0(ebn0[name], code.k_info / code.n))
+        llr[sel] = channel.awgn_i8_host(code.n, sel.size, seed=31 + c, table=table, codeword=cw)
+    d_hard = torch.empty((B, 64800), dtype=torch.uint8, device="cuda")
+    d_its = torch.empty(B, dtype=torch.int32, device="cuda")
+    mx.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, ids, 20, params=default_params(early_term=1),
+                        iters_used=d_its)
+    torch.cuda.synchronize()
+    hard, its = d_hard.cpu().numpy(), d_its.cpu().numpy()
+    for c, name in enumerate(names):
+        sel = np.where(ids == c)[0]
+        eh, _, eit = O.decode_i8(load_table(name), llr[sel], 20, early_term=True, return_soft=True)
+        assert np.array_equal(hard[sel], eh), name
+        assert np.array_equal(its[sel], eit), name
