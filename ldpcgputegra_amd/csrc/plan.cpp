@@ -52,7 +52,10 @@ int ldpc_plan_windows(const ldpc_code *h, int S, int P, std::vector<ldpc_window>
                 if (lw >= gstart && lw >= u - P) ok = false;      // written by the read-ahead span
             }
             if (!ok) {
-                if (cnt == 0) return ldpc_set_error(LDPC_EINVAL, "plan: check %d cannot start a window", ci);
+                if (cnt == 0) {   // hazards too short for this read-ahead: no windowed schedule
+                    out.clear();
+                    return LDPC_OK;
+                }
                 break;
             }
             for (int j = 0; j < h->check_deg[ci]; j++) in_win[ev[j]] = u;

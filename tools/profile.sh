@@ -1,0 +1,36 @@
+#!/bin/bash
+# rocprofv3 collection for the bench workload (run on the GPU box).
+#   pass "trace": --kernel-trace --stats         -> per-kernel durations (+ the bench JSON line)
+#   pass "fetch": --pmc FETCH_SIZE               -> HBM read bytes (KB; gfx950 counts 1/2 of wide reads)
+#   pass "write": --pmc WRITE_SIZE               -> HBM write bytes (KB)
+#   pass "sq":    wave-state counters            -> issue vs wait breakdown
+#   pass "tcc":   L2 hit / miss
+# Counters get their own passes, filtered to the decode kernel.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+OUT=${PROF_OUT:-gpurun_out/prof}
+mkdir -p $OUT
+ARGS=${PROF_ARGS:---steps 3 --warmup 1 --cpu-seconds 0}
+KRE=${PROF_KERNEL_RE:-decode}
+PASSES=${PROF_PASSES:-trace fetch write sq tcc}
+run() {
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name" >&2
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" >&2
+    tail -3 "$OUT/$name.log" >&2
+    [ $rc -ne 0 ] && exit $rc
+    return 0
+}
+for p in $PASSES; do
+    case $p in
+    trace) run trace 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py $ARGS ;;
+    fetch) run fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/fetch -o run -- python3 bench.py $ARGS ;;
+    write) run write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/write -o run -- python3 bench.py $ARGS ;;
+    sq) run sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-include-regex "$KRE" -f csv -d $OUT/sq -o run -- python3 bench.py $ARGS ;;
+    tcc) run tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KRE" -f csv -d $OUT/tcc -o run -- python3 bench.py $ARGS ;;
+    esac
+done
+exit 0

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Turn the rocprofv3 output merged back into gpurun_out/prof (tools/profile.sh)
+into committed summaries under profiles/:
+
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (pass 1)
+  profiles/<tag>_bench.json         the bench JSON line printed under pass 1
+  profiles/<tag>_pmc.json           per-kernel FETCH_SIZE / WRITE_SIZE per dispatch
+  profiles/traffic.json             {workload key: {hbm_bytes_per_launch, ...}} read by bench.py
+
+HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes): on gfx950
+FETCH_SIZE reports half of the bytes of wide coalesced reads
+(MI355X_MICROARCH.md, HBM section); both counters are summed over the XCDs.
+usage: python tools/summarize_profiles.py <tag> [gpurun_out/prof]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def find(pattern):
+    hits = sorted(glob.glob(pattern, recursive=True))
+    return hits[-1] if hits else None
+
+
+def pmc_per_kernel(path, counter):
+    """mean counter value per dispatch, keyed by kernel name."""
+    acc = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") != counter:
+                continue
+            name = row.get("Kernel_Name", "?")
+            acc.setdefault(name, []).append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    tag = sys.argv[1]
+    src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "prof")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = find(os.path.join(src, "trace", "**", "*kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats, os.path.join(dst, "%s_kernel_stats.csv" % tag))
+    bench = None
+    log = os.path.join(src, "trace.log")
+    if os.path.exists(log):
+        for line in open(log):
+            if line.startswith("{") and '"metric"' in line:
+                bench = json.loads(line)
+        if bench:
+            json.dump(bench, open(os.path.join(dst, "%s_bench.json" % tag), "w"), indent=1)
+    fetch = find(os.path.join(src, "fetch", "**", "*counter_collection.csv"))
+    write = find(os.path.join(src, "write", "**", "*counter_collection.csv"))
+    pmc = {}
+    if fetch and write:
+        fk = pmc_per_kernel(fetch, "FETCH_SIZE")
+        wk = pmc_per_kernel(write, "WRITE_SIZE")
+        for k in fk:
+            pmc[k] = dict(fetch_kb=fk[k], write_kb=wk.get(k), hbm_bytes=(2 * fk[k] + (wk.get(k) or 0)) * 1024)
+        json.dump(pmc, open(os.path.join(dst, "%s_pmc.json" % tag), "w"), indent=1)
+    if bench and pmc:
+        cfg = bench["config"]
+        key = "%s_b%d_it%d_%s" % (cfg["code"], cfg["batch_per_gpu"], cfg["iters"], cfg["kernel"])
+        dec = [v for k, v in pmc.items() if "decode" in k]
+        if dec:
+            tr_path = os.path.join(dst, "traffic.json")
+            tr = json.load(open(tr_path)) if os.path.exists(tr_path) else {}
+            tr[key] = dict(hbm_bytes_per_launch=dec[0]["hbm_bytes"], fetch_kb=dec[0]["fetch_kb"],
+                           write_kb=dec[0]["write_kb"], source="profiles/%s_pmc.json" % tag)
+            json.dump(tr, open(tr_path, "w"), indent=1, sort_keys=True)
+    print(json.dumps(dict(stats=stats, bench=bool(bench), pmc=list(pmc)), indent=1))
+
+
+if __name__ == "__main__":
+    main()
