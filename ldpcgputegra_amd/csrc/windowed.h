@@ -23,10 +23,6 @@ struct Windowed2Code {
     int n_windows;
     int g0_end;
     uint32_t *d_slotvar;
-    uint32_t *d_slotoff;
-    uint8_t *d_flags;
-    int *d_first;
-    int *d_cnt;
 };
 bool windowed2_params_ok(const ldpc_params *p);
 int windowed2_upload(const ldpc_code *h, int S, int P, Windowed2Code *w);

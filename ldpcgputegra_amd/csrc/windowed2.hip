@@ -49,11 +49,7 @@ struct W2Args {
     uint32_t *Mc;
     int stride;
     int iters;
-    const uint32_t *slotvar;   // per window [D][S]
-    const uint32_t *slotoff;   // [n_windows]
-    const uint8_t *flags;      // [n_windows][S]
-    const int *win_first;
-    const int *win_cnt;
+    const uint32_t *slotvar;   // per window [D + 1][S]; group 0 first, then group 1
     int g0_end, n_windows;
     int off, msg_max, early;
     int32_t *iters_used;
@@ -121,9 +117,18 @@ LDPC_DEV int chain_steps(int u, int dprev, int off, int T)
     return u;
 }
 
+// Per window the table holds [D + 1][S] words: rows 0..D-1 the variable of
+// each edge, row D the slot's metadata: check index | flags << 24 |
+// (window count - 1) << 27.  Inactive slots point at variable 0 and repeat a
+// valid check index, so every lane issues the same loads (no data-dependent
+// branch in the read-ahead) and all per-window facts arrive with the table
+// loads one window early.  Tables of one degree group are contiguous, so the
+// table of window w is at a fixed stride from the group's first table and no
+// per-window scalar load (which would force a full vmcnt(0) drain) is needed.
 template <int D>
 struct Tab {
     uint32_t var[D];
+    uint32_t meta;
 };
 
 // compressed message word: 19 header bits + one sign bit per edge
@@ -134,31 +139,32 @@ template <int D>
 struct Buf {
     int v[D];
     uint32_t addr[D];
+    uint32_t mc;     // element index of the check's message word
+    int fl;          // slot flags
+    int cnt;         // active slots of the window
     MsgT<D> m;
 };
 
 template <int D, int S>
-LDPC_DEV void load_tab(Tab<D> &t, const W2Args &a, int w, int slot)
+LDPC_DEV void load_tab(Tab<D> &t, const uint32_t *tab, int i, int slot)
 {
-    const uint32_t *p = a.slotvar + a.slotoff[w] + slot;
+    const uint32_t *p = tab + (size_t)i * (D + 1) * S + slot;
 #pragma unroll
     for (int j = 0; j < D; j++) t.var[j] = p[j * S];
+    t.meta = p[D * S];
 }
 
 template <int D, int S>
-LDPC_DEV void load_buf(Buf<D> &bf, const Tab<D> &t, const W2Args &a, int w, int slot, int b)
+LDPC_DEV void load_buf(Buf<D> &bf, const Tab<D> &t, const W2Args &a, int b)
 {
 #pragma unroll
     for (int j = 0; j < D; j++) bf.addr[j] = t.var[j] * (uint32_t)a.stride + (uint32_t)b;
-    if (a.flags[w * S + slot] & F_ACT) {
+    bf.mc = (t.meta & 0xFFFFFFu) * (uint32_t)a.stride + (uint32_t)b;
+    bf.fl = (int)(t.meta >> 24) & 7;
+    bf.cnt = (int)(t.meta >> 27) + 1;
 #pragma unroll
-        for (int j = 0; j < D; j++) bf.v[j] = a.V[bf.addr[j]];
-        bf.m = reinterpret_cast<const MsgT<D> *>(a.Mc)[(size_t)(a.win_first[w] + slot) * a.stride + b];
-    } else {
-#pragma unroll
-        for (int j = 0; j < D; j++) bf.v[j] = 0;
-        bf.m = 0;
-    }
+    for (int j = 0; j < D; j++) bf.v[j] = a.V[bf.addr[j]];
+    bf.m = reinterpret_cast<const MsgT<D> *>(a.Mc)[bf.mc];
 }
 
 LDPC_DEV int decode_msg(uint32_t word, int j, int c1o, int c2o, int jmo)
@@ -206,10 +212,10 @@ template <int D, int S>
 LDPC_DEV int win_fast(const Buf<D> &bf, const W2Args &a, int w, int slot, int b, int carry, bool live)
 {
     constexpr int X = D - 2, O = D - 1;
-    const int fl = a.flags[w * S + slot];
+    const int fl = bf.fl;
     const bool act = (fl & F_ACT) && live;
     const int off = a.off, mm = a.msg_max;
-    const int cnt = a.win_cnt[w];
+    const int cnt = __builtin_amdgcn_readfirstlane(bf.cnt);   // same window in every lane
     const auto word = bf.m;
     const int c1o = (int)(word & 127), c2o = (int)((word >> 7) & 127), jmo = (int)((word >> 14) & 31);
     int c[D], av[D];
@@ -261,8 +267,7 @@ LDPC_DEV int win_fast(const Buf<D> &bf, const W2Args &a, int w, int slot, int b,
         min1 = min(ax, min1);
     }
     const int cst1 = max(min2 - off, 0), cst2 = max(min1 - off, 0);
-    post_store<D>(a, bf, c, av, min1, sacc, act, fl & F_ODEAD, (size_t)(a.win_first[w] + slot) * a.stride + b,
-                  cst1, cst2);
+    post_store<D>(a, bf, c, av, min1, sacc, act, fl & F_ODEAD, bf.mc, cst1, cst2);
     return new_carry;
 }
 
@@ -272,10 +277,10 @@ template <int D, int S>
 LDPC_DEV int win_exact_later(const Buf<D> &bf, const W2Args &a, int w, int slot, int b, int carry, bool live)
 {
     constexpr int X = D - 2, O = D - 1;
-    const int fl = a.flags[w * S + slot];
+    const int fl = bf.fl;
     const bool act = (fl & F_ACT) && live;
     const int off = a.off, mm = a.msg_max;
-    const int cnt = a.win_cnt[w];
+    const int cnt = __builtin_amdgcn_readfirstlane(bf.cnt);   // same window in every lane
     const auto word = bf.m;
     const int c1o = (int)(word & 127), c2o = (int)((word >> 7) & 127), jmo = (int)((word >> 14) & 31);
     int c[D], av[D];
@@ -324,55 +329,64 @@ LDPC_DEV int win_exact_later(const Buf<D> &bf, const W2Args &a, int w, int slot,
         min2 = med3(ax, min1, min2);
         min1 = min(ax, min1);
     }
-    post_store<D>(a, bf, c, av, min1, sacc, act, fl & F_ODEAD, (size_t)(a.win_first[w] + slot) * a.stride + b,
-                  cst(min2), cst(min1));
+    post_store<D>(a, bf, c, av, min1, sacc, act, fl & F_ODEAD, bf.mc, cst(min2), cst(min1));
     return new_carry;
 }
 
 // windows [wb, we) of one degree group, software-pipelined with read-ahead P
 template <int D, int S, int P, bool FAST>
-LDPC_DEV int run_group(const W2Args &a, int wb, int we, int slot, int b, int carry, bool live)
+LDPC_DEV int run_group(const W2Args &a, const uint32_t *tab, int wb, int we, int slot, int b, int carry, bool live)
 {
     Tab<D> T[2];
     Buf<D> B[P + 1];
+    // The read-ahead loads are unconditional (past the group's end they
+    // re-read its last window, harmlessly): conditional loads make the
+    // compiler's wait-count merge pessimistic (a full vmcnt(0) drain before
+    // every window).
+    const int last = we - 1 - wb;
     // prologue: tables for wb..wb+P, buffers for wb..wb+P-1
 #pragma unroll
-    for (int i = 0; i < P; i++)
-        if (wb + i < we) {
-            load_tab<D, S>(T[i % 2], a, wb + i, slot);
-            load_buf<D, S>(B[i], T[i % 2], a, wb + i, slot, b);
-        }
-    if (wb + P < we) load_tab<D, S>(T[P % 2], a, wb + P, slot);
-    auto step = [&](auto sc, int t) {
+    for (int i = 0; i < P; i++) {
+        load_tab<D, S>(T[i % 2], tab, min(i, last), slot);
+        load_buf<D, S>(B[i], T[i % 2], a, b);
+    }
+    load_tab<D, S>(T[P % 2], tab, min(P, last), slot);
+    auto step = [&](auto sc, int i) {
         constexpr int s = decltype(sc)::value;
-        if (t + P + 1 < we) load_tab<D, S>(T[(s + P + 1) % 2], a, t + P + 1, slot);
-        if (t + P < we) load_buf<D, S>(B[(s + P) % (P + 1)], T[(s + P) % 2], a, t + P, slot, b);
+        load_tab<D, S>(T[(s + P + 1) % 2], tab, min(i + P + 1, last), slot);
+        load_buf<D, S>(B[(s + P) % (P + 1)], T[(s + P) % 2], a, b);
         if constexpr (FAST)
-            carry = win_fast<D, S>(B[s % (P + 1)], a, t, slot, b, carry, live);
+            carry = win_fast<D, S>(B[s % (P + 1)], a, wb + i, slot, b, carry, live);
         else
-            carry = win_exact_later<D, S>(B[s % (P + 1)], a, t, slot, b, carry, live);
+            carry = win_exact_later<D, S>(B[s % (P + 1)], a, wb + i, slot, b, carry, live);
     };
     constexpr int U = (P == 1) ? 2 : 6;   // lcm(2, P + 1)
-    for (int t = wb; t < we; t += U) {
-        step(std::integral_constant<int, 0>{}, t);
-        if (t + 1 < we) step(std::integral_constant<int, 1>{}, t + 1);
+    const int n = we - wb;
+    for (int i = 0; i < n; i += U) {
+        step(std::integral_constant<int, 0>{}, i);
+        if (i + 1 >= n) break;
+        step(std::integral_constant<int, 1>{}, i + 1);
         if constexpr (U == 6) {
-            if (t + 2 < we) step(std::integral_constant<int, 2>{}, t + 2);
-            if (t + 3 < we) step(std::integral_constant<int, 3>{}, t + 3);
-            if (t + 4 < we) step(std::integral_constant<int, 4>{}, t + 4);
-            if (t + 5 < we) step(std::integral_constant<int, 5>{}, t + 5);
+            if (i + 2 >= n) break;
+            step(std::integral_constant<int, 2>{}, i + 2);
+            if (i + 3 >= n) break;
+            step(std::integral_constant<int, 3>{}, i + 3);
+            if (i + 4 >= n) break;
+            step(std::integral_constant<int, 4>{}, i + 4);
+            if (i + 5 >= n) break;
+            step(std::integral_constant<int, 5>{}, i + 5);
         }
     }
     return carry;
 }
 
 template <int D, int S>
-LDPC_DEV int syndrome_part(const W2Args &a, int wb, int we, int slot, int b)
+LDPC_DEV int syndrome_part(const W2Args &a, const uint32_t *tab, int nwin, int slot, int b)
 {
     int bad = 0;
-    for (int w = wb; w < we; w++) {
-        if (!(a.flags[w * S + slot] & F_ACT)) continue;
-        const uint32_t *p = a.slotvar + a.slotoff[w] + slot;
+    for (int w = 0; w < nwin; w++) {
+        const uint32_t *p = tab + (size_t)w * (D + 1) * S + slot;
+        if (!((p[D * S] >> 24) & F_ACT)) continue;
         int par = 0;
 #pragma unroll
         for (int j = 0; j < D; j++) par ^= (a.V[p[j * S] * (uint32_t)a.stride + b] > 0);
@@ -389,17 +403,18 @@ __global__ void __launch_bounds__(64) windowed2_decode(W2Args a)
     const int wave = (id % 8) * (nb / 8) + id / 8;   // XCD-aware: neighbours share an XCD
     const int slot = threadIdx.x & (S - 1), row = threadIdx.x / S;
     const int b = wave * G + row;
-    int carry = a.V[a.slotvar[a.slotoff[0] + (D0 - 2) * S] * (uint32_t)a.stride + b];
+    const uint32_t *tab0 = a.slotvar, *tab1 = a.slotvar + (size_t)a.g0_end * (D0 + 1) * S;
+    int carry = a.V[tab0[(D0 - 2) * S] * (uint32_t)a.stride + b];
     bool live = true;
     int it = 0;
     while (it < a.iters) {
-        carry = run_group<D0, S, P, true>(a, 0, a.g0_end, slot, b, carry, live);
-        carry = run_group<D0 - 1, S, 1, false>(a, a.g0_end, a.n_windows, slot, b, carry, live);
+        carry = run_group<D0, S, P, true>(a, tab0, 0, a.g0_end, slot, b, carry, live);
+        carry = run_group<D0 - 1, S, 1, false>(a, tab1, a.g0_end, a.n_windows, slot, b, carry, live);
         it++;
         if (a.early) {
             if (live) {
-                int bad = syndrome_part<D0, S>(a, 0, a.g0_end, slot, b) |
-                          syndrome_part<D0 - 1, S>(a, a.g0_end, a.n_windows, slot, b);
+                int bad = syndrome_part<D0, S>(a, tab0, a.g0_end, slot, b) |
+                          syndrome_part<D0 - 1, S>(a, tab1, a.n_windows - a.g0_end, slot, b);
                 for (int m = 1; m < S; m <<= 1) bad |= __shfl_xor(bad, m, 64);
                 if (!bad) {
                     live = false;
@@ -432,36 +447,37 @@ int windowed2_upload(const ldpc_code *h, int S, int P, Windowed2Code *w)
     extern int ldpc_plan_windows(const ldpc_code *h, int S, int P, std::vector<ldpc_window> &out);
     if (ldpc_plan_windows(h, S, P, wins) != LDPC_OK || wins.empty()) return LDPC_OK;
     const int nw = (int)wins.size();
-    std::vector<uint32_t> slotvar, slotoff(nw);
-    std::vector<uint8_t> flags((size_t)nw * S, 0);
-    std::vector<int> first(nw), cnt(nw);
+    if (h->m >= (1 << 24)) return LDPC_OK;   // check index must fit the meta word
+    std::vector<uint32_t> slotvar;
     int g0_end = nw;
     for (int i = 0; i < nw; i++) {
         const int c0 = wins[i].first;
         const int d = h->check_deg[c0];
         if (h->check_group[c0] != 0 && g0_end == nw) g0_end = i;
-        first[i] = c0;
-        cnt[i] = wins[i].count;
-        slotoff[i] = (uint32_t)slotvar.size();
-        slotvar.resize(slotvar.size() + (size_t)d * S, 0u);
-        for (int k = 0; k < wins[i].count; k++) {
+        // the kernel addresses tables by group: group 0 windows, then group 1
+        if (h->check_group[c0] != (i < g0_end ? 0 : 1)) return LDPC_OK;
+        const size_t base = slotvar.size();
+        const uint32_t cbits = (uint32_t)(wins[i].count - 1) << 27;
+        slotvar.resize(base + (size_t)(d + 1) * S, 0u);
+        for (int k = 0; k < S; k++) {
+            // inactive slots: variable 0 and the window's first check (valid,
+            // never stored: flags 0)
+            slotvar[base + (size_t)d * S + k] = (uint32_t)c0 | cbits;
+            if (k >= wins[i].count) continue;
             const int c = c0 + k;
             const uint32_t *ev = &h->edge_var[h->check_start[c]];
-            for (int j = 0; j < d; j++) slotvar[slotoff[i] + j * S + k] = ev[j];
-            uint8_t f = F_ACT;
+            for (int j = 0; j < d; j++) slotvar[base + j * S + k] = ev[j];
+            uint32_t f = F_ACT;
             if (h->chain_in[c] >= 0) f |= F_XIN;
             if (h->chain_out[c] >= 0 && c + 1 < h->m) f |= F_ODEAD;
-            flags[(size_t)i * S + k] = f;
+            slotvar[base + (size_t)d * S + k] = (uint32_t)c | (f << 24) | cbits;
         }
     }
     auto up = [&](void **dst, const void *src, size_t bytes) {
         if (hipMalloc(dst, bytes) != hipSuccess) return false;
         return hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
     };
-    if (!up((void **)&w->d_slotvar, slotvar.data(), slotvar.size() * 4) ||
-        !up((void **)&w->d_slotoff, slotoff.data(), slotoff.size() * 4) ||
-        !up((void **)&w->d_flags, flags.data(), flags.size()) || !up((void **)&w->d_first, first.data(), nw * 4) ||
-        !up((void **)&w->d_cnt, cnt.data(), nw * 4)) {
+    if (!up((void **)&w->d_slotvar, slotvar.data(), slotvar.size() * 4)) {
         windowed2_free(w);
         return ldpc_set_error(LDPC_ENOMEM, "windowed2 tables");
     }
@@ -477,10 +493,6 @@ int windowed2_upload(const ldpc_code *h, int S, int P, Windowed2Code *w)
 void windowed2_free(Windowed2Code *w)
 {
     (void)hipFree(w->d_slotvar);
-    (void)hipFree(w->d_slotoff);
-    (void)hipFree(w->d_flags);
-    (void)hipFree(w->d_first);
-    (void)hipFree(w->d_cnt);
     *w = Windowed2Code{};
 }
 
@@ -500,10 +512,6 @@ int launch_windowed2(const DecodeLaunch &L, const Windowed2Code &w, hipStream_t 
     a.stride = L.stride;
     a.iters = L.iters;
     a.slotvar = w.d_slotvar;
-    a.slotoff = w.d_slotoff;
-    a.flags = w.d_flags;
-    a.win_first = w.d_first;
-    a.win_cnt = w.d_cnt;
     a.g0_end = w.g0_end;
     a.n_windows = w.n_windows;
     a.off = L.param;
