@@ -227,7 +227,7 @@ static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float)
     case 3: return (w2 && c->w16.valid) ? 3 : -1;
     case 4: return (w2 && c->w32.valid) ? 4 : -1;
     default:
-        if (w2 && c->w32.valid) return 4;
+        if (w2 && c->w16.valid) return 3;
         if (w1) return 2;
         return 1;
     }

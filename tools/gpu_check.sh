@@ -18,7 +18,7 @@ run() {  # run <name> <seconds> <cmd...>
 }
 STEPS=${STEPS:-smoke,pytest,bench}
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *pytest* ]] && run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 ${PYTEST_ARGS}
+[[ $STEPS == *pytest* ]] && run pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS}
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py ${BENCH_ARGS}
 if [[ $STEPS == *kernels* ]]; then
     for k in ${KERNELS:-2 3 4}; do
@@ -26,5 +26,4 @@ if [[ $STEPS == *kernels* ]]; then
     done
 fi
 [[ $STEPS == *sim* ]] && run sim 300 ldpcgputegra_amd/bin/ldpc_sim -code dvbs2_r1_2 -min 0.8 -max 1.2 -pas 0.1 -iter 50 -fer 50 -frames 65536
-exit 0
 exit 0

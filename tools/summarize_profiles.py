@@ -63,6 +63,15 @@ def main():
         wk = pmc_per_kernel(write, "WRITE_SIZE")
         for k in fk:
             pmc[k] = dict(fetch_kb=fk[k], write_kb=wk.get(k), hbm_bytes=(2 * fk[k] + (wk.get(k) or 0)) * 1024)
+        # other counter passes (sq, tcc, ...): mean per dispatch
+        for extra in ("sq", "tcc", "tcp"):
+            path = find(os.path.join(src, extra, "**", "*counter_collection.csv"))
+            if not path:
+                continue
+            names = sorted({r["Counter_Name"] for r in csv.DictReader(open(path))})
+            for cn in names:
+                for k, v in pmc_per_kernel(path, cn).items():
+                    pmc.setdefault(k, {})[cn] = v
         json.dump(pmc, open(os.path.join(dst, "%s_pmc.json" % tag), "w"), indent=1)
     if bench and pmc:
         cfg = bench["config"]
