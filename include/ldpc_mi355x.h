@@ -120,6 +120,13 @@ int ldpc_code_plan_info(const ldpc_code *h, int *staircase, int *n_windows, int 
  * total count (0 when the code has no staircase schedule). */
 int ldpc_code_window_plan(const ldpc_code *h, int S, int P, int *first, int *count, int max_windows,
                           int *n_windows);
+/* Window schedule of the workgroup-cooperative kernel (S checks per window,
+ * prefetch depth R windows): (first check, count) per window -- count 0 is
+ * an empty window -- the window holding the tail check and the number of
+ * info-edge reads per iteration forwarded through LDS.  n_windows = 0 when
+ * the code has no such schedule. */
+int ldpc_code_coop_plan(const ldpc_code *h, int S, int R, int *first, int *count, int max_windows,
+                        int *n_windows, int *tail, int *n_fwd);
 void ldpc_code_destroy(ldpc_code *h);
 
 /* ---- decoder context --------------------------------------------------- */
@@ -127,11 +134,12 @@ int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ldpc_ctx **ou
 void ldpc_ctx_destroy(ldpc_ctx *ctx);
 int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
 /* Select kernel family: 0 = auto, 1 = generic (per-edge messages),
- * 2 = windowed layered kernel (compressed messages). */
+ * 2 = windowed layered kernel (compressed messages), 3 / 4 = windowed2
+ * (S = 16 / 32), 5 = workgroup-cooperative DVB-S2 kernel. */
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel family the last decode actually ran (1 generic, 2 windowed,
- * 3 windowed2 S=16, 4 windowed2 S=32; 0 before the first decode). */
+ * 3 windowed2 S=16, 4 windowed2 S=32, 5 coop; 0 before the first decode). */
 int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel timing (bench / profiling): when enabled, every decode records HIP
  * events around the decode kernel on the stream it is launched on;

@@ -16,6 +16,7 @@
 #include "kernels.h"
 #include "ldpc_internal.h"
 #include "windowed.h"
+#include "coop.h"
 
 #define HIP_TRY(expr)                                                                          \
     do {                                                                                       \
@@ -29,7 +30,7 @@ struct ldpc_ctx {
     int device = 0;
     int max_batch = 0;
     int max_stride = 0;
-    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32
+    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop
     int last_kernel = 0;
     hipStream_t stream = nullptr;
     // device copy of the code
@@ -37,6 +38,7 @@ struct ldpc_ctx {
     int *d_group_deg = nullptr, *d_group_cnt = nullptr;
     WindowedCode wcode{};           // windowed-kernel tables (windowed.hip)
     Windowed2Code w16{}, w32{};     // windowed2.hip tables, S = 16 and S = 32
+    CoopCode coop{};                // coop.hip tables (workgroup-cooperative DVB-S2 path)
     // scratch (lazily sized)
     void *d_V = nullptr;
     size_t V_bytes = 0;
@@ -44,6 +46,8 @@ struct ldpc_ctx {
     size_t msg_bytes = 0;
     void *d_io = nullptr;           // staging for the host-buffer API
     size_t io_bytes = 0;
+    void *d_early = nullptr;        // coop early termination: live[stride] u8, bad[stride] u32, iters[stride]
+    size_t early_bytes = 0;
     // kernel timing (ldpc_ctx_profile)
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -109,6 +113,7 @@ extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ld
     if ((rc = windowed_code_upload(h, &c->wcode)) != LDPC_OK) return fail(rc);
     if ((rc = windowed2_upload(h, 16, 2, &c->w16)) != LDPC_OK) return fail(rc);
     if ((rc = windowed2_upload(h, 32, 1, &c->w32)) != LDPC_OK) return fail(rc);
+    if ((rc = coop_upload(h, &c->coop)) != LDPC_OK) return fail(rc);
     *out = c;
     return LDPC_OK;
 }
@@ -121,6 +126,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     windowed_code_free(&c->wcode);
     windowed2_free(&c->w16);
     windowed2_free(&c->w32);
+    coop_free(&c->coop);
     for (auto &pr : c->events) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -131,6 +137,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     (void)hipFree(c->d_V);
     (void)hipFree(c->d_msg);
     (void)hipFree(c->d_io);
+    (void)hipFree(c->d_early);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -144,8 +151,9 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 4) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 4");
-    if ((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid))
+    if (!c || k < 0 || k > 5) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 5");
+    if ((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid) ||
+        (k == 5 && !c->coop.valid))
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
     c->kernel = k;
     return LDPC_OK;
@@ -215,18 +223,22 @@ static int check_params(const ldpc_ctx *c, int batch, int n_iter, const ldpc_par
     return LDPC_OK;
 }
 
-// kernel family for this call: 1 generic, 2 windowed, 3 windowed2/S16, 4 windowed2/S32
+// kernel family for this call: 1 generic, 2 windowed, 3 windowed2/S16,
+// 4 windowed2/S32, 5 coop (workgroup-cooperative)
 static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float)
 {
     if (is_float) return 1;
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
     const bool w2 = windowed2_params_ok(p);
+    const bool co = c->coop.valid && coop_params_ok(p);
     switch (c->kernel) {
     case 1: return 1;
     case 2: return w1 ? 2 : -1;
     case 3: return (w2 && c->w16.valid) ? 3 : -1;
     case 4: return (w2 && c->w32.valid) ? 4 : -1;
+    case 5: return co ? 5 : -1;
     default:
+        if (co) return 5;
         if (w2 && c->w16.valid) return 3;
         if (w1) return 2;
         return 1;
@@ -249,8 +261,9 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d selected but not applicable to these params", c->kernel);
     const bool win = kern >= 2;
     c->last_kernel = kern;
-    const size_t msg_need = win ? windowed_msg_bytes(h, stride) : (size_t)h->e * stride * esz;
-    if ((rc = ensure(&c->d_V, &c->V_bytes, (size_t)h->n * stride * esz)) != LDPC_OK) return rc;
+    // + a sink row / sink words for the masked stores of the coop kernel
+    const size_t msg_need = (win ? windowed_msg_bytes(h, stride) : (size_t)h->e * stride * esz) + 4096;
+    if ((rc = ensure(&c->d_V, &c->V_bytes, (size_t)(h->n + 1) * stride * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&c->d_msg, &c->msg_bytes, msg_need)) != LDPC_OK) return rc;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
@@ -283,13 +296,21 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     L.early = p->early_term;
     L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
     L.iters_used = d_iters;
+    if (kern == 5 && p->early_term) {
+        // live u8 | bad u32 | iterations used i32 (when the caller passed none)
+        if ((rc = ensure(&c->d_early, &c->early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
+        L.bad = (uint32_t *)c->d_early;
+        if (!L.iters_used) L.iters_used = (int32_t *)((char *)c->d_early + (size_t)stride * 4);
+        L.live = (uint8_t *)c->d_early + (size_t)stride * 8;
+    }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (c->profile) {
         HIP_TRY(hipEventCreate(&ev0));
         HIP_TRY(hipEventCreate(&ev1));
         HIP_TRY(hipEventRecord(ev0, s));
     }
-    int lr = kern == 4   ? launch_windowed2(L, c->w32, s)
+    int lr = kern == 5   ? launch_coop(L, c->coop, s)
+             : kern == 4 ? launch_windowed2(L, c->w32, s)
              : kern == 3 ? launch_windowed2(L, c->w16, s)
              : kern == 2 ? launch_windowed(L, c->wcode, s)
                          : launch_generic(L, s);

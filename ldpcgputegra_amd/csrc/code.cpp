@@ -327,6 +327,27 @@ extern "C" int ldpc_code_window_plan(const ldpc_code *h, int S, int P, int *firs
     return LDPC_OK;
 }
 
+int coop_plan_windows(const ldpc_code *h, int S, int R, std::vector<int> &first, std::vector<int> &count, int *tail,
+                      int *n_fwd);   // coop.hip
+
+extern "C" int ldpc_code_coop_plan(const ldpc_code *h, int S, int R, int *first, int *count, int max_windows,
+                                   int *n_windows, int *tail, int *n_fwd)
+{
+    if (!h || S < 1 || S > 32 || R < 1 || R > 16 || !n_windows) return ldpc_set_error(LDPC_EINVAL, "coop plan args");
+    std::vector<int> f, c;
+    int t = -1, nf = 0;
+    *n_windows = 0;
+    if (coop_plan_windows(h, S, R, f, c, &t, &nf) != 0) return LDPC_OK;   // no cooperative schedule
+    *n_windows = (int)f.size();
+    for (int i = 0; i < (int)f.size() && i < max_windows; i++) {
+        if (first) first[i] = f[i];
+        if (count) count[i] = c[i];
+    }
+    if (tail) *tail = t;
+    if (n_fwd) *n_fwd = nf;
+    return LDPC_OK;
+}
+
 extern "C" void ldpc_code_destroy(ldpc_code *h) { delete h; }
 
 // ---------------------------------------------------------------- channel

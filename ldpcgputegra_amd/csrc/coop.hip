@@ -1,0 +1,779 @@
+// coop.hip -- workgroup-cooperative layered int8 offset-min-sum decoder for
+// the DVB-S2 staircase codes (the BASELINE.json headline path).
+//
+// Arithmetic: bit-exact with the reference's CDecoder_OMS_fixed_SSE::decode_8bits
+// (code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:172-546): every check in
+// schedule order sees the V values left by all earlier checks.
+//
+// Layout / decomposition (CDNA4-first, not a translation of the reference's
+// per-thread-codeword CUDA kernels):
+//
+// * A workgroup owns CW = 16 consecutive codewords.  V stays in HBM as
+//   V[var][stride] (codeword fastest): one check slot touches 16 contiguous
+//   bytes, and the 8 workgroups sharing a 128-B line are placed on one XCD
+//   (block -> codeword-group remap) so the line is served by that XCD's L2.
+//   Messages are compressed per check (cst1 | cst2 << 7 | jmin << 14 |
+//   sign_j << (19 + j)) and laid out Mc[group][check][16]: a wave's 4 slots
+//   read 256 contiguous bytes.
+// * The schedule is cut into windows of <= S consecutive checks (plan at the
+//   bottom).  WS = S / 4 "slab" waves own 4 check slots x 16 codewords each
+//   and do all per-edge work in parallel: gather V, decode the old message,
+//   min1 / min2 / sign (pre), new messages and V (post).
+// * Inside a window the only dependency between checks is the staircase
+//   parity variable: check k writes it as its last edge o, check k+1 reads it
+//   as its edge x.  Pre reduces each check to six constants and one extra
+//   "chain" wave runs the serial recurrence for the 16 codewords (one lane
+//   each), 4 VALU per check:
+//       Y_k = med3(med3(eps Y + A, co, eps Y + B), co - T, co + T)
+//   (= co + eps dz(Y_{k-1} - mx), dz the offset dead zone clipped at T; see
+//   pre_fast).  The x-edge inputs Y_{k-1} return to the slab waves through LDS.
+// * Period p: the chain wave runs window p; the slab waves post window p-1
+//   (phase A), then issue the loads of window p+1+R and pre window p+1
+//   (phase B); two workgroup barriers per period.  A value written by window
+//   w that window u loaded too early (2 <= u - w <= R + 1; u - w = 1 never
+//   shares a variable, by plan) is forwarded through an LDS ring.  Global
+//   stores and later loads of one workgroup are ordered by issue order (the
+//   gfx950 workgroup-scope memory model needs no vmcnt wait for that).
+#include <algorithm>
+#include <vector>
+
+#include "coop.h"
+
+namespace {
+
+constexpr int CW = 16;                          // codewords per workgroup
+constexpr uint32_t M_ACT = 1u << 20;            // slot holds a check
+constexpr uint32_t M_FWD = 1u << 21;            // an info edge of the slot reads the LDS ring
+constexpr int SRC_SHIFT = 22;                   // bit 22 + j: info edge j feeds the LDS ring
+constexpr uint32_t CHK_MASK = (1u << 20) - 1;   // check index
+constexpr uint32_t FWD_NONE = 0xFFFFu;          // forwarding code: dW << 8 | slot << 3 | edge
+
+template <int D0>
+struct Geo {
+    static constexpr int X = D0 - 2;                          // info edges of a group-0 check
+    static constexpr int NFW = (X + 1) / 2;                   // dwords of u16 forwarding codes
+    static constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;   // record: vars, meta, fwd (16-B multiple)
+};
+
+struct CoopArgs {
+    int8_t *V;             // V[n + 1][stride]; row n receives masked stores
+    uint32_t *Mc;          // Mc[stride / 16][m][16], then a 1024-word sink
+    const uint32_t *tab;   // [nw][S][RECW] slot records
+    const uint8_t *live;   // [stride] early termination: 0 = codeword frozen (NULL: all live)
+    int stride, G, nw, tail, m, n, off, mm, remap;
+};
+
+LDPC_DEV int med3(int x, int y, int z)
+{
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+    return r;
+}
+
+LDPC_DEV int mad24(int a, int b, int c)
+{
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+LDPC_DEV int clamp127(int x) { return min(max(x, -127), 127); }
+
+// old message of edge j from the compressed word
+LDPC_DEV int dec_msg(uint32_t w, int j, int c1, int c2, int jm)
+{
+    const int mag = (jm == j) ? c1 : c2;
+    const int sm = ((int)(w << (12 - j))) >> 31;   // bit 19 + j
+    return (mag ^ sm) - sm;
+}
+
+template <int D0, int WS, int R>
+struct alignas(16) Smem {
+    static constexpr int S = 4 * WS, X = Geo<D0>::X, RECW = Geo<D0>::RECW, TQ = R + 4;
+    uint32_t tab[TQ][S][RECW];   // slot records of windows p-1 .. p+R+2
+    int cst[2][S][CW][8];        // chain constants eps, A, B, co, L, H (pre -> chain)
+    int xin[2][CW][S];           // chain outputs: x-edge input of each slot (chain -> post)
+    uint8_t ring[R][S][X][CW];   // forwarded V values of the last R windows
+};
+
+template <int D0>
+struct Pf {                       // prefetched inputs of one window (raw bytes: the
+    uint32_t v[D0 - 1];           // sign extension happens at the use, so no wait
+    uint32_t m;                   // is forced right after the load); info, o; message
+};
+
+template <int D0>
+struct St {                       // one window's state between pre and post
+    int c[D0 - 1];                // contributions c_j (info, o); tail: new V values
+    int a[D0 - 1];                // |c_j| clipped
+    int mx, min1, min2, sacc;     // tail: sacc = new message word
+};
+
+template <int D0, int WS, int R>
+struct Slab {
+    using SM = Smem<D0, WS, R>;
+    static constexpr int S = SM::S, X = SM::X, RECW = SM::RECW, TQ = SM::TQ, NFW = Geo<D0>::NFW;
+    SM &sm;
+    const CoopArgs &a;
+    int k, c;
+    uint32_t b, mcbase, vsink, mcsink;
+    int bsh;   // bit offset of this codeword's byte in a V dword
+    bool live; // early termination: stores of a converged codeword are masked
+
+    // issue the loads of window g (local index u) into pf
+    LDPC_DEV void prefetch(int g, int u, Pf<D0> &pf) const
+    {
+        const uint32_t *r = sm.tab[g % TQ][k];
+        uint32_t var[D0];
+#pragma unroll
+        for (int j = 0; j < D0; j++) var[j] = r[j];
+        const uint32_t meta = r[D0];
+        const uint32_t st = (uint32_t)a.stride;
+        // whole dwords (4 codewords; this lane's byte is extracted in pre):
+        // byte loads make the compiler copy the value right after the load
+        const uint32_t *V4 = (const uint32_t *)a.V;
+#pragma unroll
+        for (int j = 0; j < X; j++) pf.v[j] = V4[(var[j] * st + b) >> 2];
+        const uint32_t vo = (u == a.tail) ? var[X] : var[D0 - 1];
+        pf.v[X] = V4[(vo * st + b) >> 2];
+        pf.m = a.Mc[mcbase + (meta & CHK_MASK) * CW];
+    }
+
+    // pre of window g: forwarding, contributions, chain constants
+    LDPC_DEV void pre(int g, int u, const Pf<D0> &pf, St<D0> &s) const
+    {
+        const uint32_t *r = sm.tab[g % TQ][k];
+        const uint32_t meta = r[D0];
+        int v[D0 - 1];
+#pragma unroll
+        for (int j = 0; j < D0 - 1; j++) v[j] = __builtin_amdgcn_sbfe(pf.v[j], bsh, 8);
+        if (__any((meta & M_FWD) != 0)) {
+            uint32_t fw[NFW];
+#pragma unroll
+            for (int i = 0; i < NFW; i++) fw[i] = r[D0 + 1 + i];
+#pragma unroll
+            for (int j = 0; j < X; j++) {
+                const uint32_t code = (fw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+                const int dw = (int)(code >> 8);
+                if (code != FWD_NONE && g >= dw) {
+                    const int q = (g - dw) % R;
+                    v[j] = (int8_t)sm.ring[q][(code >> 3) & 31][code & 7][c];
+                }
+            }
+        }
+        const uint32_t w = pf.m;
+        const int c1 = (int)(w & 127), c2 = (int)((w >> 7) & 127), jm = (int)((w >> 14) & 31);
+        const int off = a.off, mm = a.mm;
+        int eps, A, B, co, L, H;
+        int min1 = 127, min2 = 127, sacc = 0;
+        if (u != a.tail) {
+            // first degree group: a = min(|c|, msg_max) (OMS_fixed_SSE.cpp:211)
+#pragma unroll
+            for (int j = 0; j < X; j++) {
+                const int cj = clamp127(v[j] - dec_msg(w, j, c1, c2, jm));
+                const int aj = med3(cj, -cj, mm);
+                s.c[j] = cj;
+                s.a[j] = aj;
+                sacc ^= cj;
+                min2 = med3(aj, min1, min2);
+                min1 = min(aj, min1);
+            }
+            // chain constants of this check: T = cst(min over the info edges),
+            // eps = -1 iff the info edges' sign parity (with the odd-degree
+            // flip) is odd.  With w = Y_{k-1} - mx:
+            //   new V[o] = co + eps * sign(w) * min(max(|w| - off, 0), T)
+            //            = med3(med3(eps Y + A, co, eps Y + B), co - T, co + T)
+            // A = co - eps (mx + off), B = co - eps (mx - off).  Y may stay
+            // unclamped along the chain: a value beyond +-127 gives the same
+            // dead-zone output as its clamp because 127 - msg_max >= T + off.
+            const int T = max(min1 - off, 0);
+            const int kbit = (int)(((uint32_t)sacc >> 31) ^ (uint32_t)(D0 & 1));
+            co = clamp127(v[X] - dec_msg(w, D0 - 1, c1, c2, jm));
+            const int ao = med3(co, -co, mm);
+            s.c[X] = co;
+            s.a[X] = ao;
+            sacc ^= co;
+            min2 = med3(ao, min1, min2);
+            min1 = min(ao, min1);
+            const int mx = dec_msg(w, X, c1, c2, jm);
+            s.mx = mx;
+            s.min1 = min1;
+            s.min2 = min2;
+            s.sacc = sacc;
+            eps = 1 - 2 * kbit;
+            A = co - eps * (mx + off);
+            B = co - eps * (mx - off);
+            L = co - T;
+            H = co + T;
+        } else {
+            // the tail check (later degree group: a = |min(c, msg_max)|,
+            // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
+#pragma unroll
+            for (int j = 0; j <= X; j++) {
+                const int cj = clamp127(v[j] - dec_msg(w, j, c1, c2, jm));
+                const int t = min(cj, mm);
+                const int aj = max(t, -t);
+                s.c[j] = cj;
+                s.a[j] = aj;
+                sacc ^= cj;
+                min2 = med3(aj, min1, min2);
+                min1 = min(aj, min1);
+            }
+            const int cst1 = min(max(min2 - off, 0), mm), cst2 = min(max(min1 - off, 0), mm);
+            const int P = sacc ^ (((D0 - 1) & 1) ? (int)0x80000000 : 0);
+            uint32_t nw = (uint32_t)cst1 | ((uint32_t)cst2 << 7);
+            int jmin = 0;
+#pragma unroll
+            for (int j = 0; j <= X; j++) {
+                const bool eq = s.a[j] == min1;
+                const int rr = eq ? cst1 : cst2;
+                jmin = eq ? j : jmin;
+                const int t = s.c[j] ^ P;
+                const int sm = t >> 31;
+                const int lsb = (int)((uint32_t)t >> 31);
+                nw |= (uint32_t)lsb << (19 + j);
+                s.c[j] = clamp127(s.c[j] + (rr ^ sm) + lsb);
+            }
+            s.sacc = (int)(nw | ((uint32_t)jmin << 14));
+            const int y = s.c[X];
+            eps = 0;
+            A = B = co = L = H = y;
+        }
+        if (!(meta & M_ACT)) {   // pass-through: Y_k = Y_{k-1}
+            eps = 1;
+            A = B = co = 0;
+            L = -1024;
+            H = 1024;
+        }
+        int *dst = sm.cst[g & 1][k][c];
+        *(int4 *)dst = make_int4(eps, A, B, co);
+        *(int2 *)(dst + 4) = make_int2(L, H);
+    }
+
+    // post of window g: new messages and V, stores, LDS ring
+    LDPC_DEV void post(int g, int u, const St<D0> &s) const
+    {
+        const uint32_t *r = sm.tab[g % TQ][k];
+        uint32_t var[D0];
+#pragma unroll
+        for (int j = 0; j < D0; j++) var[j] = r[j];
+        const uint32_t meta = r[D0];
+        const bool act = (meta & M_ACT) && live;
+        const bool tl = (u == a.tail);
+        const int xin = sm.xin[g & 1][c][k];
+        int vn[D0];
+        uint32_t nw;
+        if (!tl) {
+            const int off = a.off, mm = a.mm;
+            const int cx = clamp127(clamp127(xin) - s.mx);
+            const int ax = med3(cx, -cx, mm);
+            const int sacc = s.sacc ^ cx;
+            const int min2 = med3(ax, s.min1, s.min2);
+            const int min1 = min(ax, s.min1);
+            const int cst1 = max(min2 - off, 0), cst2 = max(min1 - off, 0);   // <= msg_max already
+            const int P = sacc ^ ((D0 & 1) ? (int)0x80000000 : 0);
+            nw = (uint32_t)cst1 | ((uint32_t)cst2 << 7);
+            int jmin = 0;
+#pragma unroll
+            for (int j = 0; j < D0; j++) {
+                const int cj = (j < X) ? s.c[j] : (j == X ? cx : s.c[X]);
+                const int aj = (j < X) ? s.a[j] : (j == X ? ax : s.a[X]);
+                const bool eq = aj == min1;
+                const int rr = eq ? cst1 : cst2;
+                jmin = eq ? j : jmin;
+                const int t = cj ^ P;
+                const int sm = t >> 31;
+                const int lsb = (int)((uint32_t)t >> 31);
+                nw |= (uint32_t)lsb << (19 + j);
+                vn[j] = clamp127(cj + (rr ^ sm) + lsb);
+            }
+            nw |= (uint32_t)jmin << 14;
+        } else {
+#pragma unroll
+            for (int j = 0; j <= X; j++) vn[j] = s.c[j];
+            vn[D0 - 1] = clamp127(xin);   // V of the last group-0 check's o edge (only the chain had it)
+            nw = (uint32_t)s.sacc;
+        }
+        // Stores: edges 0..D0-2 (info + x; the tail: info + o).  A group-0 o
+        // store is dead (the next check rewrites the variable through its x
+        // edge); the last one is written by the tail from the chain.  Masked
+        // slots store to the sink row, so every store is issued unconditionally.
+        const uint32_t st = (uint32_t)a.stride;
+#pragma unroll
+        for (int j = 0; j < D0 - 1; j++) a.V[act ? var[j] * st + b : vsink] = (int8_t)vn[j];
+        if (tl) a.V[act ? var[D0 - 1] * st + b : vsink] = (int8_t)vn[D0 - 1];
+        a.Mc[act ? mcbase + (meta & CHK_MASK) * CW : mcsink] = nw;
+#pragma unroll
+        for (int j = 0; j < X; j++)
+            if ((meta >> (SRC_SHIFT + j)) & 1) sm.ring[g % R][k][j][c] = (uint8_t)vn[j];
+    }
+};
+
+// chain steps [K0, K1) of window g for the 16 codewords (lane & 15); every
+// lane group computes the same values, so the LDS accesses need no masking
+template <int D0, int WS, int R, int K0, int K1>
+LDPC_DEV void chain_steps(Smem<D0, WS, R> &sm, int g, int c, int &Y)
+{
+    const int buf = g & 1;
+    int xv[4];
+#pragma unroll
+    for (int k = K0; k < K1; k++) {
+        const int4 q0 = *(const int4 *)sm.cst[buf][k][c];
+        const int2 q1 = *(const int2 *)(sm.cst[buf][k][c] + 4);
+        xv[k & 3] = Y;
+        const int p = mad24(Y, q0.x, q0.y), q = mad24(Y, q0.x, q0.z);
+        Y = med3(med3(p, q0.w, q), q1.x, q1.y);
+        if ((k & 3) == 3) *(int4 *)&sm.xin[buf][c][k - 3] = make_int4(xv[0], xv[1], xv[2], xv[3]);
+    }
+}
+
+template <int D0, int WS, int R>
+__global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
+{
+    using SM = Smem<D0, WS, R>;
+    constexpr int S = SM::S, X = SM::X, RECW = SM::RECW, TQ = SM::TQ;
+    constexpr int U = (R + 1) % 2 ? 2 * (R + 1) : (R + 1);   // lcm(2, R + 1)
+    constexpr int SPLIT = (S / 2) & ~3;
+    __shared__ SM sm;
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int nb = gridDim.x, id = blockIdx.x;
+    const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
+    const int G = a.G;
+    if (G == 0) return;
+    const bool live = a.live ? a.live[wg * CW + (lane & 15)] != 0 : true;
+    if (a.live && !__syncthreads_or(live)) return;   // all 16 codewords converged
+
+    if (wave == WS) {
+        // ------------------------------------------------------------ chain wave
+        constexpr int NCH = S * RECW / 4;   // 16-B chunks per window table
+        static_assert(NCH <= 128, "window table too large for two chunks per lane");
+        const int c = lane & 15;
+        const int i0 = min(lane, NCH - 1), i1 = min(lane + 64, NCH - 1);
+        auto load = [&](int u, uint4 &t0, uint4 &t1) {
+            const uint4 *src = (const uint4 *)(a.tab + (size_t)u * S * RECW);
+            t0 = src[i0];
+            t1 = src[i1];
+        };
+        auto store = [&](int slot, const uint4 &t0, const uint4 &t1) {
+            uint4 *dst = (uint4 *)&sm.tab[slot][0][0];
+            if (lane < NCH) dst[lane] = t0;
+            if (lane + 64 < NCH) dst[lane + 64] = t1;
+        };
+        uint4 t0, t1;
+        for (int q = 0; q <= R + 1; q++) {
+            load(q % a.nw, t0, t1);
+            store(q, t0, t1);
+        }
+        int Y = a.V[a.tab[X] * (uint32_t)a.stride + (uint32_t)(wg * CW + c)];   // x input of the first check
+        load((R + 2) % a.nw, t0, t1);
+        int un = (R + 3) % a.nw;
+        __syncthreads();   // prologue: tables in LDS
+        __syncthreads();   // pre(0) done: constants of window 0 in LDS
+        for (int p = 0; p <= G; p++) {
+            if (p < G) chain_steps<D0, WS, R, 0, SPLIT>(sm, p, c, Y);
+            store((p + R + 2) % TQ, t0, t1);
+            load(un, t0, t1);
+            un = (un + 1 == a.nw) ? 0 : un + 1;
+            __syncthreads();   // A
+            if (p < G) chain_steps<D0, WS, R, SPLIT, S>(sm, p, c, Y);
+            __syncthreads();   // B
+        }
+        return;
+    }
+
+    // -------------------------------------------------------------- slab waves
+    const int k = 4 * wave + (lane >> 4), c = lane & 15;
+    Slab<D0, WS, R> sl{sm, a, k, c, (uint32_t)(wg * CW + c), (uint32_t)(wg * a.m * CW + c),
+                       (uint32_t)a.n * (uint32_t)a.stride + (uint32_t)lane,
+                       (uint32_t)nb * (uint32_t)a.m * CW + threadIdx.x, (c & 3) * 8, live};
+    Pf<D0> pf[R + 1];
+    St<D0> st[2];
+    __syncthreads();   // prologue: tables of windows 0 .. R+1 are in LDS
+#pragma unroll
+    for (int i = 0; i <= R; i++) sl.prefetch(i, i, pf[i]);   // nw > R + 3
+    sl.pre(0, 0, pf[0], st[0]);
+    // period 0: chain(0) | nothing to post | loads of R+1, pre(1)
+    __syncthreads();   // B of the prologue
+    __syncthreads();   // A(0)
+    sl.prefetch(R + 1, (R + 1) % a.nw, pf[0]);
+    sl.pre(1, 1, pf[1], st[1]);
+    __syncthreads();   // B(0)
+    int uA = 0, uB = 2 % a.nw, uP = (R + 2) % a.nw;   // windows p-1, p+1, p+1+R (local index)
+    auto next = [&](int &u) { u = (u + 1 == a.nw) ? 0 : u + 1; };
+    // steady state p = 1 .. G: every memory operation unconditional (loads past
+    // the end read valid table rows; their pre only writes unused constants)
+    auto step = [&](auto sc, int p) {
+        constexpr int s = decltype(sc)::value;
+        sl.post(p - 1, uA, st[s % 2]);
+        __syncthreads();   // A(p)
+        sl.prefetch(p + 1 + R, uP, pf[(s + 1) % (R + 1)]);
+        sl.pre(p + 1, uB, pf[(s + 2) % (R + 1)], st[s % 2]);
+        __syncthreads();   // B(p)
+        next(uA);
+        next(uB);
+        next(uP);
+    };
+    // single-exit loop over whole unroll groups (multi-exit loops get
+    // restructured and lose the precise wait counts), then the remainder
+    const int nfull = G / U;
+    int p = 1;
+    for (int i = 0; i < nfull; i++, p += U) {
+        step(std::integral_constant<int, 0>{}, p);
+        step(std::integral_constant<int, 1>{}, p + 1);
+        if constexpr (U > 2) {
+            step(std::integral_constant<int, 2>{}, p + 2);
+            step(std::integral_constant<int, 3>{}, p + 3);
+        }
+        if constexpr (U > 4) {
+            step(std::integral_constant<int, 4>{}, p + 4);
+            step(std::integral_constant<int, 5>{}, p + 5);
+        }
+        if constexpr (U > 6) {
+            step(std::integral_constant<int, 6>{}, p + 6);
+            step(std::integral_constant<int, 7>{}, p + 7);
+        }
+        if constexpr (U > 8) {
+            step(std::integral_constant<int, 8>{}, p + 8);
+            step(std::integral_constant<int, 9>{}, p + 9);
+        }
+        static_assert(U <= 10, "unroll");
+    }
+    const int rem = G - nfull * U;
+    if (rem > 0) step(std::integral_constant<int, 0>{}, p);
+    if (rem > 1) step(std::integral_constant<int, 1>{}, p + 1);
+    if constexpr (U > 2) {
+        if (rem > 2) step(std::integral_constant<int, 2>{}, p + 2);
+        if (rem > 3) step(std::integral_constant<int, 3>{}, p + 3);
+    }
+    if constexpr (U > 4) {
+        if (rem > 4) step(std::integral_constant<int, 4>{}, p + 4);
+        if (rem > 5) step(std::integral_constant<int, 5>{}, p + 5);
+    }
+    if constexpr (U > 6) {
+        if (rem > 6) step(std::integral_constant<int, 6>{}, p + 6);
+        if (rem > 7) step(std::integral_constant<int, 7>{}, p + 7);
+    }
+    if constexpr (U > 8) {
+        if (rem > 8) step(std::integral_constant<int, 8>{}, p + 8);
+    }
+}
+
+// ------------------------------------------------------- early termination
+// After each iteration (one coop launch): a codeword stops once all its
+// parity checks hold on the hard decisions V > 0 (the reference's commented
+// `arret` test, CDecoder_OMS_fixed_SSE.cpp:551-553; the oracle's early_term).
+// Block = 64 consecutive codewords (coalesced V rows) x a chunk of checks;
+// the H indices are wave-uniform (scalar loads).
+__global__ void __launch_bounds__(64) syndrome_k(const int8_t *V, int stride, int batch, const uint32_t *ev,
+                                                 const int *gdeg, const int *gcnt, int ngroups, int m, int chunk,
+                                                 const uint8_t *live, uint32_t *bad)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= batch || !live[b]) return;
+    const int c0 = blockIdx.y * chunk, c1 = min(m, c0 + chunk);
+    int g = 0, gfirst = 0, e = 0;
+    while (g < ngroups && c0 >= gfirst + gcnt[g]) {
+        e += gdeg[g] * gcnt[g];
+        gfirst += gcnt[g];
+        g++;
+    }
+    int d = gdeg[g];
+    e += (c0 - gfirst) * d;
+    int gend = gfirst + gcnt[g];
+    int badv = 0;
+    for (int c = c0; c < c1; c++) {
+        if (c == gend) {
+            g++;
+            d = gdeg[g];
+            gend += gcnt[g];
+        }
+        int par = 0;
+        for (int j = 0; j < d; j++) par ^= V[(size_t)ev[e + j] * stride + b] > 0;
+        badv |= par;
+        e += d;
+    }
+    if (badv) atomicOr(&bad[b], 1u);
+}
+
+__global__ void syndrome_finish_k(int batch, uint8_t *live, uint32_t *bad, int32_t *iters_used, int it)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    if (live[b] && !bad[b]) {
+        live[b] = 0;
+        iters_used[b] = it;
+    }
+    bad[b] = 0;
+}
+
+__global__ void fill_iters_k(int batch, int32_t *iters_used, int iters)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < batch) iters_used[b] = iters;
+}
+
+__global__ void early_init_k(int batch, uint8_t *live, uint32_t *bad, int32_t *iters_used, int iters)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    live[b] = 1;
+    bad[b] = 0;
+    iters_used[b] = iters;
+}
+
+// ------------------------------------------------------------------ host plan
+
+struct Plan {
+    std::vector<int> first, count;
+    int tail = -1, n_fwd = 0;
+    std::vector<uint32_t> tab;
+};
+
+// Windows: runs of <= S consecutive group-0 checks in schedule order such that
+// no two checks of a window, and no checks of two consecutive windows
+// (cyclically, across the iteration boundary too), share an information
+// variable; an empty window is inserted where a check would conflict with the
+// previous window.  The tail check (the one check of the second degree group)
+// is a window of its own.  Forwarding: every info-edge read whose latest
+// writer is 2..R+1 windows earlier (cyclic) reads that writer's LDS ring entry.
+static int build_plan(const ldpc_code *h, int S, int R, int recw, Plan &o, bool want_tab)
+{
+    if (!h->staircase || h->n_groups != 2 || h->group_cnt[1] != 1) return -1;
+    const int D0 = h->group_deg[0], X = D0 - 2, M = h->m, T = M - 1;
+    if (h->group_deg[1] != D0 - 1 || X < 1 || X > 8 || M < 4 || M >= (1 << 20)) return -1;
+    auto ev = [&](int c, int j) { return h->edge_var[h->check_start[c] + j]; };
+    // staircase: x edge (D0-2) of check c is the o edge (D0-1) of check c-1;
+    // the x edge of check 0 is the tail's last edge
+    for (int c = 1; c < T; c++)
+        if (ev(c, X) != ev(c - 1, D0 - 1)) return -1;
+    if (ev(0, X) != ev(T, X)) return -1;
+    std::vector<char> par(h->n, 0);
+    for (int c = 0; c < T; c++) par[ev(c, X)] = par[ev(c, D0 - 1)] = 1;
+    for (int c = 0; c < M; c++)
+        for (int j = 0; j < X; j++)
+            if (par[ev(c, j)]) return -1;
+    std::vector<int> mark(h->n, -(1 << 29));
+    auto conflict = [&](int c, int u) {
+        for (int j = 0; j < X; j++)
+            if (mark[ev(c, j)] >= u - 1) return true;
+        return false;
+    };
+    auto take = [&](int c, int u) {
+        for (int j = 0; j < X; j++) mark[ev(c, j)] = u;
+    };
+    o.first.clear();
+    o.count.clear();
+    int c = 0;
+    while (c < T) {
+        const int u = (int)o.first.size();
+        if (conflict(c, u)) {   // touched by the previous window: leave a gap
+            o.first.push_back(c);
+            o.count.push_back(0);
+            continue;
+        }
+        int cnt = 0;
+        while (c + cnt < T && cnt < S && !conflict(c + cnt, u)) {
+            take(c + cnt, u);
+            cnt++;
+        }
+        o.first.push_back(c);
+        o.count.push_back(cnt);
+        c += cnt;
+    }
+    {
+        int u = (int)o.first.size();
+        if (conflict(T, u)) {
+            o.first.push_back(T);
+            o.count.push_back(0);
+            u++;
+        }
+        take(T, u);
+        o.first.push_back(T);
+        o.count.push_back(1);
+        o.tail = u;
+    }
+    {   // the next iteration's window 0 follows the last window
+        const int last = (int)o.first.size() - 1;
+        bool bad = false;
+        for (int k = 0; k < o.count[0]; k++)
+            for (int j = 0; j < X; j++) bad |= (mark[ev(o.first[0] + k, j)] == last);
+        if (bad) {
+            o.first.push_back(M);
+            o.count.push_back(0);
+        }
+    }
+    const int nw = (int)o.first.size();
+    if (nw < R + 4) return -1;   // ring / table-ring sizes and parity reuse distance
+    // forwarding (two passes over the cyclic schedule)
+    std::vector<int> lw(h->n, -1), lk(h->n, 0), lj(h->n, 0);
+    std::vector<uint16_t> fwd((size_t)nw * S * X, (uint16_t)FWD_NONE);
+    std::vector<uint32_t> src((size_t)nw * S, 0);
+    o.n_fwd = 0;
+    for (int pass = 0; pass < 2; pass++)
+        for (int u = 0; u < nw; u++)
+            for (int k = 0; k < o.count[u]; k++) {
+                const int cc = o.first[u] + k;
+                for (int j = 0; j < X; j++) {
+                    const uint32_t v = ev(cc, j);
+                    if (pass == 1) {
+                        const int gw = lw[v];
+                        const int dW = (nw + u) - gw;
+                        if (dW == 1) return -1;   // violates the window rule
+                        if (dW >= 2 && dW <= R + 1) {
+                            const int w = gw % nw;
+                            fwd[((size_t)u * S + k) * X + j] = (uint16_t)(dW << 8 | lk[v] << 3 | lj[v]);
+                            src[(size_t)w * S + lk[v]] |= 1u << lj[v];
+                            o.n_fwd++;
+                        }
+                    }
+                    lw[v] = pass * nw + u;
+                    lk[v] = k;
+                    lj[v] = j;
+                }
+            }
+    if (!want_tab) return 0;
+    o.tab.assign((size_t)nw * S * recw, 0u);
+    for (int u = 0; u < nw; u++)
+        for (int k = 0; k < S; k++) {
+            uint32_t *rec = &o.tab[((size_t)u * S + k) * recw];
+            for (int i = 0; i < (X + 1) / 2; i++) rec[D0 + 1 + i] = 0xFFFFFFFFu;
+            if (k >= o.count[u]) {
+                rec[D0] = (uint32_t)std::min(o.first[u], M - 1);   // a valid check, never stored
+                continue;
+            }
+            const int cc = o.first[u] + k;
+            for (int j = 0; j < h->check_deg[cc]; j++) rec[j] = ev(cc, j);
+            if (u == o.tail) rec[D0 - 1] = ev(T - 1, D0 - 1);   // the last group-0 check's o variable
+            bool any = false;
+            for (int j = 0; j < X; j++) {
+                const uint16_t f = fwd[((size_t)u * S + k) * X + j];
+                if (f == FWD_NONE) continue;
+                any = true;
+                uint32_t &d = rec[D0 + 1 + j / 2];
+                d = (j & 1) ? ((d & 0xFFFFu) | ((uint32_t)f << 16)) : ((d & 0xFFFF0000u) | f);
+            }
+            rec[D0] = (uint32_t)cc | M_ACT | (any ? M_FWD : 0u) | (src[(size_t)u * S + k] << SRC_SHIFT);
+        }
+    return 0;
+}
+
+constexpr int kWS = 7;   // slab waves: S = 28 checks per window
+constexpr int kR = 3;    // prefetch depth (windows)
+
+template <int D0>
+int launch_d0(const CoopArgs &a, int grid, hipStream_t s)
+{
+    hipLaunchKernelGGL((coop_decode<D0, kWS, kR>), dim3(grid), dim3(64 * (kWS + 1)), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace
+
+bool coop_params_ok(const ldpc_params *p)
+{
+    // the unclamped chain needs 127 - msg_max >= T + offset (T <= msg_max - offset)
+    return (p->algo == LDPC_ALGO_OMS || p->algo == LDPC_ALGO_MS) && p->var_min == -127 && p->var_max == 127 &&
+           p->msg_max >= 0 && p->msg_max <= 63 && (p->algo == LDPC_ALGO_MS || (p->offset >= 0 && p->offset <= 63));
+}
+
+int coop_plan_windows(const ldpc_code *h, int S, int R, std::vector<int> &first, std::vector<int> &count, int *tail,
+                      int *n_fwd)
+{
+    Plan pl;
+    if (build_plan(h, S, R, 0, pl, false) != 0) {
+        first.clear();
+        count.clear();
+        return -1;
+    }
+    first = pl.first;
+    count = pl.count;
+    if (tail) *tail = pl.tail;
+    if (n_fwd) *n_fwd = pl.n_fwd;
+    return 0;
+}
+
+int coop_upload(const ldpc_code *h, CoopCode *cc)
+{
+    *cc = CoopCode{};
+    if (!h->staircase || h->n_groups != 2) return LDPC_OK;
+    const int d0 = h->group_deg[0];
+    int recw;
+    if (d0 == 7)
+        recw = Geo<7>::RECW;
+    else if (d0 == 10)
+        recw = Geo<10>::RECW;
+    else
+        return LDPC_OK;
+    Plan pl;
+    if (build_plan(h, 4 * kWS, kR, recw, pl, true) != 0) return LDPC_OK;
+    if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop tables");
+    if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        coop_free(cc);
+        return ldpc_set_error(LDPC_EDEVICE, "coop table upload");
+    }
+    cc->valid = 1;
+    cc->d0 = d0;
+    cc->S = 4 * kWS;
+    cc->R = kR;
+    cc->nw = (int)pl.first.size();
+    cc->tail = pl.tail;
+    cc->n_fwd = pl.n_fwd;
+    return LDPC_OK;
+}
+
+void coop_free(CoopCode *cc)
+{
+    (void)hipFree(cc->d_tab);
+    *cc = CoopCode{};
+}
+
+static int launch_coop_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
+                             hipStream_t s)
+{
+    CoopArgs a;
+    a.V = (int8_t *)L.V;
+    a.Mc = (uint32_t *)L.msg;
+    a.tab = cc.d_tab;
+    a.stride = L.stride;
+    a.G = cc.nw * iters;
+    a.live = live;
+    a.nw = cc.nw;
+    a.tail = cc.tail;
+    a.m = L.m;
+    a.n = L.n;
+    a.off = L.param;
+    a.mm = L.msg_max;
+    const int grid = L.stride / CW;
+    a.remap = (grid % 8) == 0;
+    if (cc.d0 == 7) return launch_d0<7>(a, grid, s);
+    if (cc.d0 == 10) return launch_d0<10>(a, grid, s);
+    return -1;
+}
+
+int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
+{
+    if (!cc.valid || L.stride % 64) return -1;
+    if (!L.early) {
+        if (L.iters_used)
+            hipLaunchKernelGGL(fill_iters_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used,
+                               L.iters);
+        return launch_coop_iters(L, cc, L.iters, nullptr, s);
+    }
+    // early termination: one launch per iteration (V, messages and the chain
+    // input V[p_0] carry the state), then the syndrome of the live codewords
+    if (!L.live || !L.bad || !L.iters_used) return -1;
+    const int nb = (L.batch + 255) / 256;
+    hipLaunchKernelGGL(early_init_k, dim3(nb), dim3(256), 0, s, L.batch, L.live, L.bad, L.iters_used, L.iters);
+    constexpr int kChunk = 512;
+    const dim3 sgrid((L.batch + 63) / 64, (L.m + kChunk - 1) / kChunk);
+    for (int it = 0; it < L.iters; it++) {
+        if (launch_coop_iters(L, cc, 1, L.live, s)) return -1;
+        hipLaunchKernelGGL(syndrome_k, sgrid, dim3(64), 0, s, (const int8_t *)L.V, L.stride, L.batch, L.d_edge_var,
+                           L.d_group_deg, L.d_group_cnt, L.n_groups, L.m, kChunk, (const uint8_t *)L.live, L.bad);
+        hipLaunchKernelGGL(syndrome_finish_k, dim3(nb), dim3(256), 0, s, L.batch, L.live, L.bad, L.iters_used,
+                           it + 1);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

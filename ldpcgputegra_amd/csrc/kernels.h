@@ -20,6 +20,9 @@ struct DecodeLaunch {
     int algo, param, var_min, msg_max, early;
     float beta;
     int32_t *iters_used;
+    // early-termination scratch of the coop kernel ([stride] each)
+    uint8_t *live;
+    uint32_t *bad;
 };
 
 int launch_generic(const DecodeLaunch &L, hipStream_t s);

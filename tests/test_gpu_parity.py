@@ -29,13 +29,15 @@ def decoder(code, kernel=0, max_batch=4096):
 
 def kernels_for(code):
     """Kernel families that can run this code: 1 generic, 2 windowed,
-    3 windowed2 (S=16), 4 windowed2 (S=32)."""
+    3 windowed2 (S=16), 4 windowed2 (S=32), 5 coop (workgroup-cooperative)."""
     ks = [1]
     c = Code(code)
     if c.plan_info()["windowed"]:
         ks.append(2)
     if c.window_plan(16, 2):
         ks += [3, 4]
+    if c.coop_plan() is not None and c.max_deg in (7, 10):
+        ks.append(5)
     return ks
 
 
