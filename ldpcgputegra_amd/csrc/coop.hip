@@ -91,7 +91,8 @@ template <int D0, int WS, int R>
 struct alignas(16) Smem {
     static constexpr int S = 4 * WS, X = Geo<D0>::X, RECW = Geo<D0>::RECW, TQ = R + 4;
     uint32_t tab[TQ][S][RECW];   // slot records of windows p-1 .. p+R+2
-    int cst[2][S][CW][8];        // chain constants eps, A, B, co, L, H (pre -> chain)
+    int4 cst0[2][S][CW];         // chain constants (eps, A, B, co)   (pre -> chain)
+    int2 cst1[2][S][CW];         //                 (L, H); lane-contiguous: no bank conflicts
     int xin[2][CW][S];           // chain outputs: x-edge input of each slot (chain -> post)
     uint8_t ring[R][S][X][CW];   // forwarded V values of the last R windows
 };
@@ -245,9 +246,8 @@ struct Slab {
             L = -1024;
             H = 1024;
         }
-        int *dst = sm.cst[g & 1][k][c];
-        *(int4 *)dst = make_int4(eps, A, B, co);
-        *(int2 *)(dst + 4) = make_int2(L, H);
+        sm.cst0[g & 1][k][c] = make_int4(eps, A, B, co);
+        sm.cst1[g & 1][k][c] = make_int2(L, H);
     }
 
     // post of window g: new messages and V, stores, LDS ring
@@ -309,20 +309,28 @@ struct Slab {
     }
 };
 
-// chain steps [K0, K1) of window g for the 16 codewords (lane & 15); every
-// lane group computes the same values, so the LDS accesses need no masking
+// chain steps [K0, K1) of window g for the 16 codewords (lanes 0..15).  All
+// constants of the range are read first (the LDS latency would otherwise sit
+// on the serial chain once per step), then the recurrence runs back to back.
 template <int D0, int WS, int R, int K0, int K1>
 LDPC_DEV void chain_steps(Smem<D0, WS, R> &sm, int g, int c, int &Y)
 {
+    constexpr int NK = K1 - K0;
     const int buf = g & 1;
+    int4 q0[NK];
+    int2 q1[NK];
+#pragma unroll
+    for (int i = 0; i < NK; i++) {
+        q0[i] = sm.cst0[buf][K0 + i][c];
+        q1[i] = sm.cst1[buf][K0 + i][c];
+    }
     int xv[4];
 #pragma unroll
-    for (int k = K0; k < K1; k++) {
-        const int4 q0 = *(const int4 *)sm.cst[buf][k][c];
-        const int2 q1 = *(const int2 *)(sm.cst[buf][k][c] + 4);
+    for (int i = 0; i < NK; i++) {
+        const int k = K0 + i;
         xv[k & 3] = Y;
-        const int p = mad24(Y, q0.x, q0.y), q = mad24(Y, q0.x, q0.z);
-        Y = med3(med3(p, q0.w, q), q1.x, q1.y);
+        const int p = mad24(Y, q0[i].x, q0[i].y), q = mad24(Y, q0[i].x, q0[i].z);
+        Y = med3(med3(p, q0[i].w, q), q1[i].x, q1[i].y);
         if ((k & 3) == 3) *(int4 *)&sm.xin[buf][c][k - 3] = make_int4(xv[0], xv[1], xv[2], xv[3]);
     }
 }
@@ -371,13 +379,14 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
         int un = (R + 3) % a.nw;
         __syncthreads();   // prologue: tables in LDS
         __syncthreads();   // pre(0) done: constants of window 0 in LDS
+        const bool cl = lane < CW;   // the chain runs on 16 lanes
         for (int p = 0; p <= G; p++) {
-            if (p < G) chain_steps<D0, WS, R, 0, SPLIT>(sm, p, c, Y);
+            if (p < G && cl) chain_steps<D0, WS, R, 0, SPLIT>(sm, p, c, Y);
             store((p + R + 2) % TQ, t0, t1);
             load(un, t0, t1);
             un = (un + 1 == a.nw) ? 0 : un + 1;
             __syncthreads();   // A
-            if (p < G) chain_steps<D0, WS, R, SPLIT, S>(sm, p, c, Y);
+            if (p < G && cl) chain_steps<D0, WS, R, SPLIT, S>(sm, p, c, Y);
             __syncthreads();   // B
         }
         return;

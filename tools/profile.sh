@@ -30,6 +30,8 @@ for p in $PASSES; do
     fetch) run fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/fetch -o run -- python3 bench.py $ARGS ;;
     write) run write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/write -o run -- python3 bench.py $ARGS ;;
     sq) run sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-include-regex "$KRE" -f csv -d $OUT/sq -o run -- python3 bench.py $ARGS ;;
+    sq2) run sq2 600 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES --kernel-include-regex "$KRE" -f csv -d $OUT/sq2 -o run -- python3 bench.py $ARGS ;;
+    list) timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true ;;
     tcc) run tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KRE" -f csv -d $OUT/tcc -o run -- python3 bench.py $ARGS ;;
     esac
 done

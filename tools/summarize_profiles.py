@@ -64,7 +64,7 @@ def main():
         for k in fk:
             pmc[k] = dict(fetch_kb=fk[k], write_kb=wk.get(k), hbm_bytes=(2 * fk[k] + (wk.get(k) or 0)) * 1024)
         # other counter passes (sq, tcc, ...): mean per dispatch
-        for extra in ("sq", "tcc", "tcp"):
+        for extra in ("sq", "sq2", "tcc", "tcp"):
             path = find(os.path.join(src, extra, "**", "*counter_collection.csv"))
             if not path:
                 continue
