@@ -333,7 +333,7 @@ int coop_plan_windows(const ldpc_code *h, int S, int R, std::vector<int> &first,
 extern "C" int ldpc_code_coop_plan(const ldpc_code *h, int S, int R, int *first, int *count, int max_windows,
                                    int *n_windows, int *tail, int *n_fwd)
 {
-    if (!h || S < 1 || S > 32 || R < 1 || R > 16 || !n_windows) return ldpc_set_error(LDPC_EINVAL, "coop plan args");
+    if (!h || S < 1 || S > 64 || R < 1 || R > 6 || !n_windows) return ldpc_set_error(LDPC_EINVAL, "coop plan args");
     std::vector<int> f, c;
     int t = -1, nf = 0;
     *n_windows = 0;

@@ -20,3 +20,27 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
 // host-side plan (tests: ldpc_code_coop_plan)
 int coop_plan_windows(const ldpc_code *h, int S, int R, std::vector<int> &first, std::vector<int> &count, int *tail,
                       int *n_fwd);
+
+// ---- window plan shared by coop.hip and coop2.hip ----
+// Slot record [recw] u32: edge variables [D0], meta, forwarding codes (u16 per
+// information edge: dW << 9 | slot << 3 | edge; 0xFFFF = none).
+constexpr uint32_t COOP_M_ACT = 1u << 20;            // slot holds a check
+constexpr uint32_t COOP_M_FWD = 1u << 21;            // an info edge of the slot reads the LDS ring
+constexpr int COOP_SRC_SHIFT = 22;                   // bit 22 + j: info edge j feeds the LDS ring
+constexpr uint32_t COOP_CHK_MASK = (1u << 20) - 1;   // check index
+constexpr uint32_t COOP_FWD_NONE = 0xFFFFu;
+
+struct CoopPlan {
+    std::vector<int> first, count;   // per window: first check, checks (0: empty window)
+    int tail = -1, n_fwd = 0;        // window of the tail check; forwarded reads per iteration
+    std::vector<uint32_t> tab;       // [nw][S][recw] slot records (want_tab)
+};
+// S <= 64 checks per window, R <= 6 prefetch windows; -1: no cooperative schedule
+int coop_build_plan(const ldpc_code *h, int S, int R, int recw, CoopPlan &o, bool want_tab);
+
+// ---- coop2.hip: packed-pair variant (two codewords per lane, 16-bit halves) ----
+bool coop2_params_ok(const ldpc_params *p);
+bool coop2_stride_ok(int stride);                    // V row pitch fits the buffer descriptor
+size_t coop2_msg_bytes(const ldpc_code *h, int stride);
+int coop2_upload(const ldpc_code *h, CoopCode *cc);
+int launch_coop2(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);

@@ -42,11 +42,11 @@
 namespace {
 
 constexpr int CW = 16;                          // codewords per workgroup
-constexpr uint32_t M_ACT = 1u << 20;            // slot holds a check
-constexpr uint32_t M_FWD = 1u << 21;            // an info edge of the slot reads the LDS ring
-constexpr int SRC_SHIFT = 22;                   // bit 22 + j: info edge j feeds the LDS ring
-constexpr uint32_t CHK_MASK = (1u << 20) - 1;   // check index
-constexpr uint32_t FWD_NONE = 0xFFFFu;          // forwarding code: dW << 8 | slot << 3 | edge
+constexpr uint32_t M_ACT = COOP_M_ACT;
+constexpr uint32_t M_FWD = COOP_M_FWD;
+constexpr int SRC_SHIFT = COOP_SRC_SHIFT;
+constexpr uint32_t CHK_MASK = COOP_CHK_MASK;
+constexpr uint32_t FWD_NONE = COOP_FWD_NONE;    // forwarding code: dW << 9 | slot << 3 | edge
 
 template <int D0>
 struct Geo {
@@ -155,10 +155,10 @@ struct Slab {
 #pragma unroll
             for (int j = 0; j < X; j++) {
                 const uint32_t code = (fw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
-                const int dw = (int)(code >> 8);
+                const int dw = (int)(code >> 9);
                 if (code != FWD_NONE && g >= dw) {
                     const int q = (g - dw) % R;
-                    v[j] = (int8_t)sm.ring[q][(code >> 3) & 31][code & 7][c];
+                    v[j] = (int8_t)sm.ring[q][(code >> 3) & 63][code & 7][c];
                 }
             }
         }
@@ -532,13 +532,9 @@ __global__ void early_init_k(int batch, uint8_t *live, uint32_t *bad, int32_t *i
     iters_used[b] = iters;
 }
 
-// ------------------------------------------------------------------ host plan
+}  // namespace
 
-struct Plan {
-    std::vector<int> first, count;
-    int tail = -1, n_fwd = 0;
-    std::vector<uint32_t> tab;
-};
+// ------------------------------------------------------------------ host plan
 
 // Windows: runs of <= S consecutive group-0 checks in schedule order such that
 // no two checks of a window, and no checks of two consecutive windows
@@ -547,8 +543,9 @@ struct Plan {
 // previous window.  The tail check (the one check of the second degree group)
 // is a window of its own.  Forwarding: every info-edge read whose latest
 // writer is 2..R+1 windows earlier (cyclic) reads that writer's LDS ring entry.
-static int build_plan(const ldpc_code *h, int S, int R, int recw, Plan &o, bool want_tab)
+int coop_build_plan(const ldpc_code *h, int S, int R, int recw, CoopPlan &o, bool want_tab)
 {
+    if (S < 1 || S > 64 || R < 1 || R > 6) return -1;   // forwarding code: 6-bit slot, 3-bit dW
     if (!h->staircase || h->n_groups != 2 || h->group_cnt[1] != 1) return -1;
     const int D0 = h->group_deg[0], X = D0 - 2, M = h->m, T = M - 1;
     if (h->group_deg[1] != D0 - 1 || X < 1 || X > 8 || M < 4 || M >= (1 << 20)) return -1;
@@ -632,7 +629,7 @@ static int build_plan(const ldpc_code *h, int S, int R, int recw, Plan &o, bool 
                         if (dW == 1) return -1;   // violates the window rule
                         if (dW >= 2 && dW <= R + 1) {
                             const int w = gw % nw;
-                            fwd[((size_t)u * S + k) * X + j] = (uint16_t)(dW << 8 | lk[v] << 3 | lj[v]);
+                            fwd[((size_t)u * S + k) * X + j] = (uint16_t)(dW << 9 | lk[v] << 3 | lj[v]);
                             src[(size_t)w * S + lk[v]] |= 1u << lj[v];
                             o.n_fwd++;
                         }
@@ -668,6 +665,8 @@ static int build_plan(const ldpc_code *h, int S, int R, int recw, Plan &o, bool 
     return 0;
 }
 
+namespace {
+
 constexpr int kWS = 7;   // slab waves: S = 28 checks per window
 constexpr int kR = 3;    // prefetch depth (windows)
 
@@ -690,8 +689,8 @@ bool coop_params_ok(const ldpc_params *p)
 int coop_plan_windows(const ldpc_code *h, int S, int R, std::vector<int> &first, std::vector<int> &count, int *tail,
                       int *n_fwd)
 {
-    Plan pl;
-    if (build_plan(h, S, R, 0, pl, false) != 0) {
+    CoopPlan pl;
+    if (coop_build_plan(h, S, R, 0, pl, false) != 0) {
         first.clear();
         count.clear();
         return -1;
@@ -715,8 +714,8 @@ int coop_upload(const ldpc_code *h, CoopCode *cc)
         recw = Geo<10>::RECW;
     else
         return LDPC_OK;
-    Plan pl;
-    if (build_plan(h, 4 * kWS, kR, recw, pl, true) != 0) return LDPC_OK;
+    CoopPlan pl;
+    if (coop_build_plan(h, 4 * kWS, kR, recw, pl, true) != 0) return LDPC_OK;
     if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop tables");
     if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         coop_free(cc);
