@@ -135,11 +135,12 @@ void ldpc_ctx_destroy(ldpc_ctx *ctx);
 int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
 /* Select kernel family: 0 = auto, 1 = generic (per-edge messages),
  * 2 = windowed layered kernel (compressed messages), 3 / 4 = windowed2
- * (S = 16 / 32), 5 = workgroup-cooperative DVB-S2 kernel. */
+ * (S = 16 / 32), 5 = workgroup-cooperative DVB-S2 kernel, 6 = its packed-pair
+ * variant (two codewords per lane; first-group degree 7, no early termination). */
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel family the last decode actually ran (1 generic, 2 windowed,
- * 3 windowed2 S=16, 4 windowed2 S=32, 5 coop; 0 before the first decode). */
+ * 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2; 0 before the first decode). */
 int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel timing (bench / profiling): when enabled, every decode records HIP
  * events around the decode kernel on the stream it is launched on;

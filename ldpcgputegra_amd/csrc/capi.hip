@@ -30,7 +30,7 @@ struct ldpc_ctx {
     int device = 0;
     int max_batch = 0;
     int max_stride = 0;
-    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop
+    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop, 6 coop2
     int last_kernel = 0;
     hipStream_t stream = nullptr;
     // device copy of the code
@@ -39,6 +39,7 @@ struct ldpc_ctx {
     WindowedCode wcode{};           // windowed-kernel tables (windowed.hip)
     Windowed2Code w16{}, w32{};     // windowed2.hip tables, S = 16 and S = 32
     CoopCode coop{};                // coop.hip tables (workgroup-cooperative DVB-S2 path)
+    CoopCode coop2{};               // coop2.hip tables (packed-pair variant, D0 = 7)
     // scratch (lazily sized)
     void *d_V = nullptr;
     size_t V_bytes = 0;
@@ -114,6 +115,7 @@ extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ld
     if ((rc = windowed2_upload(h, 16, 2, &c->w16)) != LDPC_OK) return fail(rc);
     if ((rc = windowed2_upload(h, 32, 1, &c->w32)) != LDPC_OK) return fail(rc);
     if ((rc = coop_upload(h, &c->coop)) != LDPC_OK) return fail(rc);
+    if ((rc = coop2_upload(h, &c->coop2)) != LDPC_OK) return fail(rc);
     *out = c;
     return LDPC_OK;
 }
@@ -127,6 +129,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     windowed2_free(&c->w16);
     windowed2_free(&c->w32);
     coop_free(&c->coop);
+    coop_free(&c->coop2);
     for (auto &pr : c->events) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -151,9 +154,9 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 5) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 5");
+    if (!c || k < 0 || k > 6) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 6");
     if ((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid) ||
-        (k == 5 && !c->coop.valid))
+        (k == 5 && !c->coop.valid) || (k == 6 && !c->coop2.valid))
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
     c->kernel = k;
     return LDPC_OK;
@@ -224,20 +227,23 @@ static int check_params(const ldpc_ctx *c, int batch, int n_iter, const ldpc_par
 }
 
 // kernel family for this call: 1 generic, 2 windowed, 3 windowed2/S16,
-// 4 windowed2/S32, 5 coop (workgroup-cooperative)
-static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float)
+// 4 windowed2/S32, 5 coop (workgroup-cooperative), 6 coop2 (packed pairs)
+static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, int stride)
 {
     if (is_float) return 1;
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
     const bool w2 = windowed2_params_ok(p);
     const bool co = c->coop.valid && coop_params_ok(p);
+    const bool co2 = c->coop2.valid && coop2_params_ok(p) && coop2_stride_ok(stride);
     switch (c->kernel) {
     case 1: return 1;
     case 2: return w1 ? 2 : -1;
     case 3: return (w2 && c->w16.valid) ? 3 : -1;
     case 4: return (w2 && c->w32.valid) ? 4 : -1;
     case 5: return co ? 5 : -1;
+    case 6: return co2 ? 6 : -1;
     default:
+        if (co2) return 6;
         if (co) return 5;
         if (w2 && c->w16.valid) return 3;
         if (w1) return 2;
@@ -256,13 +262,16 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     const ldpc_code *h = c->code;
     const int stride = (batch + 63) / 64 * 64;
     const size_t esz = is_float ? 4 : 1;
-    const int kern = pick_kernel(c, p, is_float);
+    const int kern = pick_kernel(c, p, is_float, stride);
     if (kern < 0)
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d selected but not applicable to these params", c->kernel);
     const bool win = kern >= 2;
     c->last_kernel = kern;
     // + a sink row / sink words for the masked stores of the coop kernel
-    const size_t msg_need = (win ? windowed_msg_bytes(h, stride) : (size_t)h->e * stride * esz) + 4096;
+    const size_t msg_need = (kern == 6 ? coop2_msg_bytes(h, stride)
+                             : win    ? windowed_msg_bytes(h, stride)
+                                      : (size_t)h->e * stride * esz) +
+                            4096;
     if ((rc = ensure(&c->d_V, &c->V_bytes, (size_t)(h->n + 1) * stride * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&c->d_msg, &c->msg_bytes, msg_need)) != LDPC_OK) return rc;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
@@ -309,7 +318,8 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
         HIP_TRY(hipEventCreate(&ev1));
         HIP_TRY(hipEventRecord(ev0, s));
     }
-    int lr = kern == 5   ? launch_coop(L, c->coop, s)
+    int lr = kern == 6   ? launch_coop2(L, c->coop2, s)
+             : kern == 5 ? launch_coop(L, c->coop, s)
              : kern == 4 ? launch_windowed2(L, c->w32, s)
              : kern == 3 ? launch_windowed2(L, c->w16, s)
              : kern == 2 ? launch_windowed(L, c->wcode, s)

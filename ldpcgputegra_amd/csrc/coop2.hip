@@ -1,0 +1,710 @@
+// coop2.hip -- packed-pair variant of the workgroup-cooperative layered int8
+// offset-min-sum decoder for the DVB-S2 staircase codes: the BASELINE.json
+// headline path (DVB-S2 r1/2, 50 iterations).  Bit-exact with the reference's
+// CDecoder_OMS_fixed_SSE::decode_8bits (code/x86/CDecoder/OMS/
+// CDecoder_OMS_fixed_SSE.cpp:172-546) like coop.hip, whose window plan
+// (coop_build_plan), staircase chain recurrence and period pipeline it
+// shares.  What changes is the slab waves' data path.  On MI355X coop.hip is
+// bound by instruction issue (about 370 instructions per slab wave and
+// period, two slab waves per SIMD, ~3.5k cycles per period at 2.1 TB/s of
+// HBM traffic), so this kernel spends fewer instructions per codeword:
+//
+// * a lane holds TWO codewords, one per 16-bit half of a VGPR, and evaluates
+//   the check with gfx950 packed math (v_pk_sub_i16 / v_pk_add_i16 with
+//   clamp, v_pk_min_i16, v_pk_max_i16, v_pk_ashrrev_i16) plus v_perm_b32 and
+//   v_bfi_b32;
+// * an int8 value x sits in a half as R(x) = 256 x + 255 (value in the high
+//   byte, low byte all ones) and a message m as C(m) = 256 m.  Then
+//   R(x) - C(m) = R(x - m), R(x) + C(m) = R(x + m), and the i16 saturation
+//   0x7FFF is R(127): the reference's _mm_subs_epi8 / _mm_adds_epi8 upper
+//   clamp for free.  |x| = max(R, 510 - R) stays in R form, and min / max /
+//   compares are monotone in R;
+// * V moves two bytes at a time (one u16 per pair) through structured buffer
+//   loads and stores, address = group base + var * pitch + 2 * pair: no
+//   address arithmetic on the VALU;
+// * a check's messages for a pair are two dwords
+//     MA: bits 2j, 2j+1 (codeword 0) and 16+2j, 17+2j (codeword 1) hold the
+//         2-bit code of edge j: bit 0 = message negative, bit 1 = the edge got
+//         cst2 (a_j != min1; ties give cst1 == cst2, so this is exact),
+//     MB: bytes cst1_0, cst2_0, cst1_1, cst2_1,
+//   (4 B per codeword and check, as coop.hip), and an old message is one
+//   v_perm_b32 into each codeword's byte table [+cst1, -cst1, +cst2, -cst2];
+// * inactive window slots point at a sink V row and a sink message row, so
+//   every memory operation is unconditional; the forwarding ring is written
+//   for every information edge.
+// The workgroup owns 16 codewords: 8 pairs = 8 lanes per slot, 8 slots per
+// slab wave, S = 8 WS checks per window.  With WS = 3 every wave has a SIMD of
+// its own.  Early termination stays on coop.hip (a converged codeword may
+// share a lane with a live one).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+#include <vector>
+
+#include "coop.h"
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+// structured buffer access, address = base + index * stride + offset
+__device__ uint32_t sbuf_load_u32(i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.load.i32");
+__device__ void sbuf_store_u16(unsigned short v, i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.store.i16");
+__device__ i32x2 sbuf_load_v2(i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.load.v2i32");
+__device__ void sbuf_store_v2(i32x2 v, i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.store.v2i32");
+
+namespace {
+
+constexpr int CW = 16;     // codewords per workgroup
+constexpr int NP = 8;      // codeword pairs per workgroup = lanes per slot
+constexpr int R2 = 3;      // prefetch depth (windows)
+constexpr int KAHEAD = R2 + 4;   // window tables are DMA'd into LDS this many windows ahead of the chain
+constexpr int DPER = 3;          // ... and waited for DPER periods later (window p+R+1 is read at period p)
+constexpr int TQ = 16;           // window-table slots in LDS (>= KAHEAD + 2)
+constexpr int RING = 4;    // forwarding ring windows (>= R2)
+constexpr int MREC = 64;   // message bytes per check and workgroup (8 pairs x 8 B)
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// descriptor from wave-uniform values (kernel arguments, block index)
+LDPC_DEV i32x4 buffer_rsrc(const void *base, uint32_t stride, uint32_t records)
+{
+    const uint64_t a = (uint64_t)base;
+    i32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) | (stride << 16)));
+    r.z = __builtin_amdgcn_readfirstlane((int)records);
+    r.w = 0x00020000;
+    return r;
+}
+
+LDPC_DEV s16x2 sv(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+LDPC_DEV uint32_t us(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+LDPC_DEV uint32_t pk_sub_sat(uint32_t a, uint32_t b) { return us(__builtin_elementwise_sub_sat(sv(a), sv(b))); }
+LDPC_DEV uint32_t pk_add_sat(uint32_t a, uint32_t b) { return us(__builtin_elementwise_add_sat(sv(a), sv(b))); }
+LDPC_DEV uint32_t pk_max(uint32_t a, uint32_t b) { return us(__builtin_elementwise_max(sv(a), sv(b))); }
+LDPC_DEV uint32_t pk_min(uint32_t a, uint32_t b) { return us(__builtin_elementwise_min(sv(a), sv(b))); }
+LDPC_DEV uint32_t pk_sub(uint32_t a, uint32_t b) { return us(sv(a) - sv(b)); }
+LDPC_DEV uint32_t pk_sra15(uint32_t a) { return us(sv(a) >> (short)15); }
+LDPC_DEV uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+LDPC_DEV uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) { return __builtin_amdgcn_perm(s0, s1, sel); }
+// hide a value from the optimiser: keeps sign-splat masks as bit masks (v_bfi_b32)
+// instead of per-half compare/select, and constants in VGPRs (no op_sel / literal splits)
+LDPC_DEV uint32_t opaque(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+LDPC_DEV int hi8(uint32_t x, int h) { return __builtin_amdgcn_sbfe((int)x, 8 + 16 * h, 8); }   // half h's value
+
+constexpr uint32_t RNEG127 = 0x81FF81FFu;   // R(-127) per half
+constexpr uint32_t R127 = 0x7FFF7FFFu;      // R(127)
+constexpr uint32_t R0 = 0x00FF00FFu;        // R(0)
+constexpr uint32_t C510 = 0x01FE01FEu;      // |R(x)| = max(R, 510 - R)
+constexpr uint32_t HIBYTES = 0xFF00FF00u;   // R -> C
+constexpr uint32_t SIGNS = 0x80008000u;
+
+LDPC_DEV uint32_t unpack_v(uint32_t raw, uint32_t sel) { return perm(raw, raw, sel); }   // V dword -> R pair
+LDPC_DEV uint32_t pack_v(uint32_t r) { return perm(r, r, 0x0c0c0301u); }           // R pair -> u16 [b0 b1]
+LDPC_DEV uint32_t abs_r(uint32_t r) { return pk_max(r, pk_sub(C510, r)); }
+
+// byte tables [+cst1, -cst1, +cst2, -cst2] of the two codewords of a pair
+struct MsgTab {
+    uint32_t t0, t1;
+};
+LDPC_DEV MsgTab msg_tab(uint32_t MB)
+{
+    const uint32_t p0 = perm(MB, MB, 0x0c010c00u), p1 = perm(MB, MB, 0x0c030c02u);   // (cst1, cst2) as u16
+    return {perm(pk_sub(0u, p0), p0, 0x06020400u), perm(pk_sub(0u, p1), p1, 0x06020400u)};
+}
+
+// old message of edge J (C pair): byte 1 = t0[code0], byte 3 = t1[code1]
+template <int J>
+LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t)
+{
+    uint32_t sh;
+    if constexpr (J <= 4)
+        sh = MA << (8 - 2 * J);
+    else
+        sh = MA >> (2 * J - 8);
+    return perm(t.t1, t.t0, (sh & 0x03000300u) | 0x040c000cu);
+}
+
+// new message of edge J: its code into MA, the new V (R pair) returned
+template <int J>
+LDPC_DEV uint32_t new_msg(uint32_t c, uint32_t a, uint32_t min1, uint32_t k1, uint32_t k2, uint32_t P, uint32_t &MA)
+{
+    const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));   // -1: a > min1, the edge gets cst2
+    const uint32_t rr = bfi(neq, k2, k1);
+    const uint32_t sgn = pk_sra15(c ^ P);             // -1: the message is negative
+    MA |= (sgn & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
+    return pk_max(pk_add_sat(c, pk_sub(rr ^ sgn, sgn)), RNEG127);
+}
+
+template <int I, int N, typename F>
+LDPC_DEV void static_for(F &&f)
+{
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+struct Coop2Args {
+    int8_t *V;                     // V[n + 1][pitch]; row n is the sink of inactive slots
+    uint8_t *Mc;                   // [pitch / 16][mrows][8 pairs][2] u32; row m is the sink
+    const uint32_t *tab;           // [nw][S][RECW] slot records
+    unsigned long long *stamps;    // diagnostic build: [grid][waves][4]
+    int pitch, G, nw, tail, mrows, n, remap, prio, off;
+    uint32_t rmm, coff;            // R(msg_max), C(offset) per half
+};
+
+template <int D0>
+struct Geo {
+    static constexpr int X = D0 - 2;
+    static constexpr int NFW = (X + 1) / 2;
+    static constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;
+};
+
+template <int D0, int WS>
+struct alignas(16) Smem2 {
+    static constexpr int S = 8 * WS, X = Geo<D0>::X, RECW = Geo<D0>::RECW;
+    uint32_t tab[TQ][S][RECW];     // slot records, window g in slot g % TQ
+    int4 cst0[2][S][CW];           // chain constants (eps, A, B, co)   (pre -> chain)
+    int2 cst1[2][S][CW];           //                 (L, H)
+    int xin[2][CW][S];             // clamped x input of each slot      (chain -> post)
+    uint32_t ring[RING][S][X][NP]; // V pairs (R form) of the last windows, for forwarding
+};
+
+template <int D0>
+struct Pf2 {                       // prefetched raw inputs of one window
+    uint32_t v[D0 - 1];            // V dwords (this pair + its neighbour): info edges, then edge D0-1 of the record
+    uint32_t ma, mb;
+};
+
+template <int D0>
+struct St2 {                       // one window between pre and post (R / C pairs)
+    uint32_t c[D0 - 1];            // contributions (info, o); tail: new V
+    uint32_t a[D0 - 1];            // |c| clipped
+    uint32_t mx, min1, min2, sacc; // tail: min1 = MA, min2 = MB
+};
+
+template <int D0, int WS>
+struct Slab2 {
+    using SM = Smem2<D0, WS>;
+    static constexpr int S = SM::S, X = SM::X, NFW = Geo<D0>::NFW;
+    SM &sm;
+    const Coop2Args &a;
+    i32x4 vr, mr;                  // V rows of this group (stride pitch), message rows (stride 64)
+    int k, q, tail;
+    uint32_t usel;                 // v_perm selector: this pair's two bytes of a V dword -> R pair
+
+    // whole aligned dwords (two pairs): a u16 load result carried across the
+    // loop back-edge gets a zero-extension there, which waits for the load
+    LDPC_DEV uint32_t ldv(uint32_t var) const { return sbuf_load_u32(vr, (int)var, 4 * (q >> 1), 0, 0); }
+    LDPC_DEV void stv(uint32_t var, uint32_t r) const
+    {
+        sbuf_store_u16((unsigned short)pack_v(r), vr, (int)var, 2 * q, 0, 0);
+    }
+
+    // issue the loads of the window in table slot ts
+    LDPC_DEV void prefetch(int ts, Pf2<D0> &pf) const
+    {
+        const uint32_t *r = sm.tab[ts][k];
+        uint32_t var[D0];
+#pragma unroll
+        for (int j = 0; j < D0; j++) var[j] = r[j];
+        const uint32_t meta = r[D0];
+#pragma unroll
+        for (int j = 0; j < X; j++) pf.v[j] = ldv(var[j]);
+        pf.v[X] = ldv(var[D0 - 1]);   // o edge (tail: its last edge, swapped by the upload)
+        const i32x2 m = sbuf_load_v2(mr, (int)(meta & COOP_CHK_MASK), 8 * q, 0, 0);
+        pf.ma = (uint32_t)m.x;
+        pf.mb = (uint32_t)m.y;
+    }
+
+    // V pairs written 2..R+1 windows ago replace the loaded ones (rare)
+    LDPC_DEV void forward(int ts, int g, uint32_t *v) const
+    {
+        const uint32_t *r = sm.tab[ts][k];
+        uint32_t fw[NFW];
+#pragma unroll
+        for (int i = 0; i < NFW; i++) fw[i] = r[D0 + 1 + i];
+#pragma unroll
+        for (int j = 0; j < X; j++) {
+            const uint32_t code = (fw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+            const int dw = (int)(code >> 9);
+            if (code != COOP_FWD_NONE && g >= dw) v[j] = sm.ring[(g - dw) & (RING - 1)][(code >> 3) & 63][code & 7][q];
+        }
+    }
+
+    // pre of window g (table slot ts, constant buffer cb, local index u)
+    LDPC_DEV void pre(int ts, int cb, int g, int u, const Pf2<D0> &pf, St2<D0> &s) const
+    {
+        const uint32_t meta = sm.tab[ts][k][D0];
+        uint32_t v[D0 - 1];
+#pragma unroll
+        for (int j = 0; j < D0 - 1; j++) v[j] = unpack_v(pf.v[j], usel);
+        if (__any((meta & COOP_M_FWD) != 0)) forward(ts, g, v);
+        const MsgTab t = msg_tab(pf.mb);
+        const uint32_t MA = pf.ma, rmm = a.rmm, coff = a.coff;
+        uint32_t min1 = R127, min2 = R127, sacc = 0;
+        int eps[2], A[2], B[2], co[2], L[2], H[2];
+        if (u != tail) {
+            // first degree group: a = min(|c|, msg_max) (OMS_fixed_SSE.cpp:211)
+            static_for<0, X>([&](auto jc) {
+                constexpr int J = decltype(jc)::value;
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), RNEG127);
+                const uint32_t aj = pk_min(abs_r(c), rmm);
+                s.c[J] = c;
+                s.a[J] = aj;
+                sacc ^= c;
+                min2 = pk_max(min1, pk_min(aj, min2));
+                min1 = pk_min(min1, aj);
+            });
+            // chain constants, as coop.hip: T = cst(min over the info edges),
+            // eps = -1 iff the info edges' sign parity (odd-degree flip
+            // included) is odd, co = the o-edge contribution, mx = the x-edge
+            // old message
+            const uint32_t T = pk_max(pk_sub(min1, coff), R0);
+            const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
+            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), RNEG127);
+            const uint32_t ao = pk_min(abs_r(cor), rmm);
+            s.c[X] = cor;
+            s.a[X] = ao;
+            s.sacc = sacc ^ cor;
+            s.min2 = pk_max(min1, pk_min(ao, min2));
+            s.min1 = pk_min(min1, ao);
+            const uint32_t mx = old_msg<X>(MA, t);
+            s.mx = mx;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int th = hi8(T, h), ch = hi8(cor, h), mh = hi8(mx, h);
+                eps[h] = 1 - 2 * (int)((kb >> (15 + 16 * h)) & 1u);
+                co[h] = ch;
+                A[h] = ch - eps[h] * (mh + a.off);
+                B[h] = ch - eps[h] * (mh - a.off);
+                L[h] = ch - th;
+                H[h] = ch + th;
+            }
+        } else {
+            // the tail check (later degree group: a = |min(c, msg_max)|,
+            // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
+            static_for<0, X + 1>([&](auto jc) {
+                constexpr int J = decltype(jc)::value;
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), RNEG127);
+                const uint32_t aj = abs_r(pk_min(c, rmm));
+                s.c[J] = c;
+                s.a[J] = aj;
+                sacc ^= c;
+                min2 = pk_max(min1, pk_min(aj, min2));
+                min1 = pk_min(min1, aj);
+            });
+            const uint32_t k1 = pk_min(pk_max(pk_sub(min2, coff), R0), rmm) & HIBYTES;
+            const uint32_t k2 = pk_min(pk_max(pk_sub(min1, coff), R0), rmm) & HIBYTES;
+            const uint32_t P = (sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u)) & SIGNS;
+            uint32_t MAn = 0;
+            static_for<0, X + 1>([&](auto jc) {
+                constexpr int J = decltype(jc)::value;
+                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn);
+            });
+            s.min1 = MAn;
+            s.min2 = perm(k2, k1, 0x07030501u);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int y = hi8(s.c[X], h);
+                eps[h] = 0;
+                A[h] = B[h] = co[h] = L[h] = H[h] = y;
+            }
+        }
+        if (__any(!(meta & COOP_M_ACT))) {   // pass-through slots: Y_k = Y_{k-1}
+            if (!(meta & COOP_M_ACT)) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    eps[h] = 1;
+                    A[h] = B[h] = co[h] = 0;
+                    L[h] = -1024;
+                    H[h] = 1024;
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            sm.cst0[cb][k][2 * q + h] = make_int4(eps[h], A[h], B[h], co[h]);
+            sm.cst1[cb][k][2 * q + h] = make_int2(L[h], H[h]);
+        }
+    }
+
+    // post of the window in table slot ts (x inputs in buffer xb, ring slot rs)
+    LDPC_DEV void post(int ts, int xb, int rs, int u, const St2<D0> &s) const
+    {
+        const uint32_t *r = sm.tab[ts][k];
+        uint32_t var[D0];
+#pragma unroll
+        for (int j = 0; j < D0; j++) var[j] = r[j];
+        const uint32_t meta = r[D0];
+        const uint32_t x0 = (uint32_t)sm.xin[xb][2 * q][k], x1 = (uint32_t)sm.xin[xb][2 * q + 1][k];
+        const uint32_t xr = perm(x1, x0, 0x040d000du);   // clamped by the chain -> R pair
+        uint32_t MA, MB;
+        if (u != tail) {
+            const uint32_t cx = pk_max(pk_sub_sat(xr, s.mx), RNEG127);
+            const uint32_t ax = pk_min(abs_r(cx), a.rmm);
+            const uint32_t sacc = s.sacc ^ cx;
+            const uint32_t min2 = pk_max(s.min1, pk_min(ax, s.min2)), min1 = pk_min(ax, s.min1);
+            const uint32_t k1 = pk_max(pk_sub(min2, a.coff), R0) & HIBYTES;   // <= msg_max already
+            const uint32_t k2 = pk_max(pk_sub(min1, a.coff), R0) & HIBYTES;
+            const uint32_t P = (sacc ^ ((D0 & 1) ? SIGNS : 0u)) & SIGNS;
+            MA = 0;
+            static_for<0, X>([&](auto jc) {
+                constexpr int J = decltype(jc)::value;
+                const uint32_t vn = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA);
+                stv(var[J], vn);
+                sm.ring[rs][k][J][q] = vn;
+            });
+            stv(var[X], new_msg<X>(cx, ax, min1, k1, k2, P, MA));
+            // the o edge: message bits only (the next check rewrites V[o] as its x edge)
+            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA);
+            MB = perm(k2, k1, 0x07030501u);
+        } else {
+            static_for<0, X>([&](auto jc) {
+                constexpr int J = decltype(jc)::value;
+                stv(var[J], s.c[J]);
+                sm.ring[rs][k][J][q] = s.c[J];
+            });
+            stv(var[D0 - 1], s.c[X]);   // the tail's last edge (record entries X, D0-1 swapped)
+            stv(var[X], xr);            // V of the last group-0 check's o edge: only the chain had it
+            MA = s.min1;
+            MB = s.min2;
+        }
+        i32x2 m;
+        m.x = (int)MA;
+        m.y = (int)MB;
+        sbuf_store_v2(m, mr, (int)(meta & COOP_CHK_MASK), 8 * q, 0, 0);
+    }
+};
+
+// chain steps [K0, K1) of the window in constant buffer buf for the 16
+// codewords (lanes 0..15): the recurrence of coop.hip, one asm block per step
+// (clamped x input for post, two mad24, two med3) so that hipcc pads no
+// wait states between its four dependent instructions
+template <int D0, int WS, int K0, int K1>
+LDPC_DEV void chain_steps2(Smem2<D0, WS> &sm, int buf, int c, int &Y)
+{
+    constexpr int NK = K1 - K0;
+    int4 q0[NK];
+    int2 q1[NK];
+#pragma unroll
+    for (int i = 0; i < NK; i++) {
+        q0[i] = sm.cst0[buf][K0 + i][c];
+        q1[i] = sm.cst1[buf][K0 + i][c];
+    }
+    const int lo = -127, hi = 127;
+    int xv[4];
+#pragma unroll
+    for (int i = 0; i < NK; i++) {
+        const int k = K0 + i;
+        int p, qq;
+        asm("v_med3_i32 %1, %0, %8, %9\n\t"
+            "v_mad_i32_i24 %2, %0, %4, %5\n\t"
+            "v_mad_i32_i24 %3, %0, %4, %6\n\t"
+            "v_med3_i32 %2, %2, %7, %3\n\t"
+            "v_med3_i32 %0, %2, %10, %11"
+            : "+v"(Y), "=&v"(xv[k & 3]), "=&v"(p), "=&v"(qq)
+            : "v"(q0[i].x), "v"(q0[i].y), "v"(q0[i].z), "v"(q0[i].w), "v"(lo), "v"(hi), "v"(q1[i].x),
+              "v"(q1[i].y));
+        if ((k & 3) == 3) *(int4 *)&sm.xin[buf][c][k - 3] = make_int4(xv[0], xv[1], xv[2], xv[3]);
+    }
+}
+
+// LDS-DMA: every active lane copies 16 B from gsrc to lds_dst + 16 * lane,
+// without passing through VGPRs (the compiler neither counts nor waits for
+// it: the chain wave waits with an explicit vmcnt)
+LDPC_DEV void dma16(const void *gsrc, uint32_t lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+LDPC_DEV unsigned long long stamp()
+{
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+template <int D0, int WS, bool STAMP>
+__global__ void __launch_bounds__(64 * (WS + 1)) coop2_decode(Coop2Args a)
+{
+    using SM = Smem2<D0, WS>;
+    constexpr int S = SM::S, X = SM::X, RECW = SM::RECW, R = R2;
+    constexpr int U = 4;                      // lcm(2, R + 1): prefetch and state buffers repeat
+    constexpr int SPLIT = (S / 2) & ~3;       // chain steps before barrier A
+    static_assert(TQ >= R + 4 && RING >= R && (R + 1) % 4 == 0, "ring sizes");
+    __shared__ SM sm;
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int nb = gridDim.x, id = blockIdx.x;
+    const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
+    const int G = a.G;
+    if (G == 0) return;
+    unsigned long long sA = 0, sB = 0, t0 = 0, tx = 0;
+
+    if (wave == WS) {
+        // ------------------------------------------------------------ chain wave
+        if (a.prio) __builtin_amdgcn_s_setprio(2);
+        constexpr int NCH = S * RECW / 4;   // 16-B chunks per window table
+        constexpr int CPL = (NCH + 63) / 64;
+        static_assert(TQ >= KAHEAD + 2 && KAHEAD >= R + 1 + DPER && CPL * DPER <= 63, "table staging");
+        const int c = lane & 15;
+        // window u's slot records -> LDS slot u % TQ by LDS-DMA, CPL instructions
+        auto stage = [&](int u, int slot) {
+            const uint4 *src = (const uint4 *)(a.tab + (size_t)u * S * RECW);
+            const uint32_t dst = (uint32_t)(uintptr_t)&sm.tab[slot][0][0];
+#pragma unroll
+            for (int i = 0; i < CPL; i++)
+                if (lane + 64 * i < NCH) dma16(src + 64 * i + lane, dst + 1024 * i);
+        };
+        for (int w = 0; w < KAHEAD; w++) stage(w % a.nw, w);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int Y = a.V[(size_t)a.tab[X] * (uint32_t)a.pitch + (uint32_t)(wg * CW + c)];   // x input of check 0
+        int un = KAHEAD % a.nw;
+        __syncthreads();   // prologue: tables in LDS
+        __syncthreads();   // pre(0) done: constants of window 0 in LDS
+        const bool cl = lane < CW;
+        if (STAMP) t0 = stamp();
+        auto period = [&](auto, int p) {
+            if (STAMP) tx = stamp();
+            if (p < G && cl) chain_steps2<D0, WS, 0, SPLIT>(sm, p & 1, c, Y);
+            stage(un, (p + KAHEAD) & (TQ - 1));   // window p+KAHEAD
+            un = (un + 1 == a.nw) ? 0 : un + 1;
+            // the tables DMA'd DPER periods ago (window p+R+1 at the latest,
+            // prefetched by the slab waves after barrier A) have landed
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPL * DPER) : "memory");
+            if (STAMP) sA += stamp() - tx;
+            __syncthreads();   // A
+            if (STAMP) tx = stamp();
+            if (p < G && cl) chain_steps2<D0, WS, SPLIT, S>(sm, p & 1, c, Y);
+            if (STAMP) sB += stamp() - tx;
+            __syncthreads();   // B
+        };
+        for (int p = 0; p <= G; p += 2) {
+            period(std::integral_constant<int, 0>{}, p);
+            if (p + 1 <= G) period(std::integral_constant<int, 1>{}, p + 1);
+        }
+        if (STAMP && lane == 0) {
+            unsigned long long *o = a.stamps + ((size_t)id * (WS + 1) + wave) * 4;
+            o[0] = sA;
+            o[1] = sB;
+            o[2] = stamp() - t0;
+            o[3] = (unsigned long long)G;
+        }
+        return;
+    }
+
+    // -------------------------------------------------------------- slab waves
+    Slab2<D0, WS> sl{sm,
+                     a,
+                     buffer_rsrc(a.V + (size_t)wg * CW, (uint32_t)a.pitch, (uint32_t)(a.n + 1)),
+                     buffer_rsrc(a.Mc + (size_t)wg * a.mrows * MREC, (uint32_t)MREC, (uint32_t)a.mrows),
+                     8 * wave + (lane >> 3),
+                     lane & 7,
+                     a.tail,
+                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u};
+    Pf2<D0> pf[R + 1];
+    St2<D0> st[2];
+    __syncthreads();   // prologue: tables of windows 0 .. R+1 are in LDS
+#pragma unroll
+    for (int i = 0; i <= R; i++) sl.prefetch(i, pf[i]);   // nw > R + 3
+    sl.pre(0, 0, 0, 0, pf[0], st[0]);
+    // period 0: chain(0) | nothing to post | loads of R+1, pre(1)
+    __syncthreads();   // B of the prologue
+    __syncthreads();   // A(0)
+    sl.prefetch(R + 1, pf[0]);
+    sl.pre(1, 1, 1, 1 % a.nw, pf[1], st[1]);
+    __syncthreads();   // B(0)
+    int uA = 0, uB = 2 % a.nw;   // local index of windows p-1, p+1
+    auto next = [&](int &u) { u = (u + 1 == a.nw) ? 0 : u + 1; };
+    if (STAMP) t0 = stamp();
+    // steady state p = 1 .. G: every memory operation unconditional (loads past
+    // the end read valid table rows; their pre only writes unused constants)
+    auto step = [&](auto sc, int p) {
+        constexpr int s = decltype(sc)::value;
+        if (STAMP) tx = stamp();
+        sl.post((p - 1) & (TQ - 1), (p - 1) & 1, (p - 1) & (RING - 1), uA, st[s % 2]);
+        if (STAMP) sA += stamp() - tx;
+        __syncthreads();   // A(p)
+        if (STAMP) tx = stamp();
+        sl.prefetch((p + 1 + R) & (TQ - 1), pf[(s + 1) % (R + 1)]);
+        sl.pre((p + 1) & (TQ - 1), (p + 1) & 1, p + 1, uB, pf[(s + 2) % (R + 1)], st[s % 2]);
+        if (STAMP) sB += stamp() - tx;
+        __syncthreads();   // B(p)
+        next(uA);
+        next(uB);
+    };
+    // single-exit loop over whole unroll groups, then the remainder
+    const int nfull = G / U;
+    int p = 1;
+    for (int i = 0; i < nfull; i++, p += U) {
+        step(std::integral_constant<int, 0>{}, p);
+        step(std::integral_constant<int, 1>{}, p + 1);
+        step(std::integral_constant<int, 2>{}, p + 2);
+        step(std::integral_constant<int, 3>{}, p + 3);
+    }
+    const int rem = G - nfull * U;
+    if (rem > 0) step(std::integral_constant<int, 0>{}, p);
+    if (rem > 1) step(std::integral_constant<int, 1>{}, p + 1);
+    if (rem > 2) step(std::integral_constant<int, 2>{}, p + 2);
+    if (STAMP && lane == 0) {
+        unsigned long long *o = a.stamps + ((size_t)id * (WS + 1) + wave) * 4;
+        o[0] = sA;
+        o[1] = sB;
+        o[2] = stamp() - t0;
+        o[3] = (unsigned long long)G;
+    }
+}
+
+__global__ void fill_iters2_k(int batch, int32_t *iters_used, int iters)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < batch) iters_used[b] = iters;
+}
+
+int env_int(const char *name, int def)
+{
+    const char *e = getenv(name);
+    return (e && *e) ? atoi(e) : def;
+}
+
+// diagnostic build (LDPC_COOP2_STAMP=1): per-period cycles of each wave role
+void report_stamps(const unsigned long long *d, int grid, int nwaves, hipStream_t s)
+{
+    std::vector<unsigned long long> h((size_t)grid * nwaves * 4);
+    if (hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    double ch[3] = {0, 0, 0}, sl[3] = {0, 0, 0}, slmax[2] = {0, 0};
+    for (int b = 0; b < grid; b++)
+        for (int w = 0; w < nwaves; w++) {
+            const unsigned long long *o = &h[((size_t)b * nwaves + w) * 4];
+            const double G = o[3] ? (double)o[3] : 1.0;
+            double *acc = (w == nwaves - 1) ? ch : sl;
+            for (int i = 0; i < 3; i++) acc[i] += o[i] / G;
+            if (w < nwaves - 1) {
+                slmax[0] = std::max(slmax[0], o[0] / G);
+                slmax[1] = std::max(slmax[1], o[1] / G);
+            }
+        }
+    const double ns = (double)grid * (nwaves - 1);
+    fprintf(stderr,
+            "coop2 stamps [cycles per period]: chain A %.0f B %.0f total %.0f | slab post %.0f pre %.0f "
+            "(max wave %.0f %.0f) total %.0f\n",
+            ch[0] / grid, ch[1] / grid, ch[2] / grid, sl[0] / ns, sl[1] / ns, slmax[0], slmax[1], sl[2] / ns);
+}
+
+template <int WS>
+int launch_ws(const Coop2Args &a, int grid, bool stamped, hipStream_t s)
+{
+    if (stamped)
+        hipLaunchKernelGGL((coop2_decode<7, WS, true>), dim3(grid), dim3(64 * (WS + 1)), 0, s, a);
+    else
+        hipLaunchKernelGGL((coop2_decode<7, WS, false>), dim3(grid), dim3(64 * (WS + 1)), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// slab waves per workgroup (S = 8 WS checks per window); LDPC_COOP2_WS overrides
+int coop2_ws()
+{
+    const int ws = env_int("LDPC_COOP2_WS", 3);
+    return (ws == 3 || ws == 4) ? ws : 3;
+}
+
+}  // namespace
+
+bool coop2_params_ok(const ldpc_params *p) { return coop_params_ok(p) && !p->early_term; }
+
+// the V descriptor's record stride is a 14-bit byte count
+bool coop2_stride_ok(int stride) { return stride > 0 && stride % 64 == 0 && stride < (1 << 14); }
+
+size_t coop2_msg_bytes(const ldpc_code *h, int stride) { return (size_t)(h->m + 1) * (size_t)stride * 4; }
+
+int coop2_upload(const ldpc_code *h, CoopCode *cc)
+{
+    *cc = CoopCode{};
+    constexpr int D0 = 7, X = D0 - 2, RECW = Geo<D0>::RECW;
+    if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return LDPC_OK;
+    const int S = 8 * coop2_ws();
+    CoopPlan pl;
+    if (coop_build_plan(h, S, R2, RECW, pl, true) != 0) return LDPC_OK;
+    const int nw = (int)pl.first.size();
+    for (int u = 0; u < nw; u++)
+        for (int k = 0; k < S; k++) {
+            uint32_t *rec = &pl.tab[((size_t)u * S + k) * RECW];
+            if (k >= pl.count[u]) {   // inactive slot: sink V row n, sink message row m, no flags
+                for (int j = 0; j < D0; j++) rec[j] = (uint32_t)h->n;
+                rec[D0] = (uint32_t)h->m;
+            } else if (u == pl.tail) {
+                std::swap(rec[X], rec[D0 - 1]);   // prefetch always loads record entry D0-1
+            }
+        }
+    if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop2 tables");
+    if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        coop_free(cc);
+        return ldpc_set_error(LDPC_EDEVICE, "coop2 table upload");
+    }
+    cc->valid = 1;
+    cc->d0 = D0;
+    cc->S = S;
+    cc->R = R2;
+    cc->nw = nw;
+    cc->tail = pl.tail;
+    cc->n_fwd = pl.n_fwd;
+    return LDPC_OK;
+}
+
+int launch_coop2(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
+{
+    if (!cc.valid || L.early || !coop2_stride_ok(L.stride)) return -1;
+    if (L.iters_used)
+        hipLaunchKernelGGL(fill_iters2_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used,
+                           L.iters);
+    Coop2Args a{};
+    a.V = (int8_t *)L.V;
+    a.Mc = (uint8_t *)L.msg;
+    a.tab = cc.d_tab;
+    a.pitch = L.stride;
+    a.G = cc.nw * L.iters;
+    a.nw = cc.nw;
+    a.tail = cc.tail;
+    a.mrows = L.m + 1;
+    a.n = L.n;
+    a.off = L.param;
+    a.rmm = (uint32_t)(L.msg_max * 256 + 255) * 0x00010001u;
+    a.coff = (uint32_t)(L.param * 256) * 0x00010001u;
+    a.prio = env_int("LDPC_COOP2_PRIO", 1);
+    const int grid = L.stride / CW;
+    a.remap = (grid % 8) == 0;
+    const int nwaves = cc.S / 8 + 1;
+    const bool stamped = env_int("LDPC_COOP2_STAMP", 0) != 0;
+    if (stamped) {
+        const size_t bytes = (size_t)grid * nwaves * 4 * sizeof(unsigned long long);
+        if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
+        (void)hipMemsetAsync(a.stamps, 0, bytes, s);
+    }
+    const int rc = (cc.S == 24) ? launch_ws<3>(a, grid, stamped, s) : launch_ws<4>(a, grid, stamped, s);
+    if (stamped) {
+        if (rc == 0) report_stamps(a.stamps, grid, nwaves, s);
+        (void)hipFree(a.stamps);
+    }
+    return rc;
+}

@@ -24,7 +24,7 @@ def checks(t):
 
 
 @pytest.mark.parametrize("code", ["dvbs2_r1_2", "dvbs2_r2_3"])
-@pytest.mark.parametrize("S,R", [(28, 3), (28, 4), (32, 3)])
+@pytest.mark.parametrize("S,R", [(24, 3), (28, 3), (28, 4), (32, 3)])
 def test_coop_plan_rules(code, S, R):
     t = load_table(code)
     plan = Code(code).coop_plan(S, R)

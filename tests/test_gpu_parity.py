@@ -29,7 +29,8 @@ def decoder(code, kernel=0, max_batch=4096):
 
 def kernels_for(code):
     """Kernel families that can run this code: 1 generic, 2 windowed,
-    3 windowed2 (S=16), 4 windowed2 (S=32), 5 coop (workgroup-cooperative)."""
+    3 windowed2 (S=16), 4 windowed2 (S=32), 5 coop (workgroup-cooperative),
+    6 coop2 (its packed-pair variant, first-group degree 7)."""
     ks = [1]
     c = Code(code)
     if c.plan_info()["windowed"]:
@@ -38,6 +39,8 @@ def kernels_for(code):
         ks += [3, 4]
     if c.coop_plan() is not None and c.max_deg in (7, 10):
         ks.append(5)
+    if c.coop_plan(24, 3) is not None and c.max_deg == 7:
+        ks.append(6)
     return ks
 
 
@@ -110,6 +113,8 @@ def test_early_termination_vs_oracle(code):
     ref_hard, ref_soft, ref_its = O.decode_i8(t, llr, 30, O.OMS, 1, early_term=True, return_soft=True)
     assert ref_its.min() < 30                                # some codewords stop early
     for k in kernels_for(code):
+        if k == 6:          # coop2 has no early termination (auto selection falls back to coop)
+            continue
         dec = decoder(code, k, max_batch=64)
         d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
         d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
