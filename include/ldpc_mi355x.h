@@ -127,6 +127,11 @@ int ldpc_code_window_plan(const ldpc_code *h, int S, int P, int *first, int *cou
  * the code has no such schedule. */
 int ldpc_code_coop_plan(const ldpc_code *h, int S, int R, int *first, int *count, int max_windows,
                         int *n_windows, int *tail, int *n_fwd);
+/* Same with the window distance rule of the kernel: dist = 1 (coop: consecutive
+ * windows share no information variable) or 2 (coop2: nor do windows two
+ * apart; reads written dist+1 .. R+dist windows earlier are forwarded). */
+int ldpc_code_coop_plan_dist(const ldpc_code *h, int S, int R, int dist, int *first, int *count, int max_windows,
+                             int *n_windows, int *tail, int *n_fwd);
 void ldpc_code_destroy(ldpc_code *h);
 
 /* ---- decoder context --------------------------------------------------- */

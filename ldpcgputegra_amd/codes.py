@@ -200,19 +200,21 @@ class Code:
                                            C.byref(n)))
         return list(zip(first[:n.value].tolist(), count[:n.value].tolist()))
 
-    def coop_plan(self, S=28, R=3):
-        """Schedule of the workgroup-cooperative kernel: dict(windows=[(first,
-        count)], tail=window index of the tail check, n_fwd=forwarded reads per
-        iteration); None when the code has no such schedule."""
+    def coop_plan(self, S=28, R=3, dist=1):
+        """Schedule of the workgroup-cooperative kernels (dist 1: coop, 2:
+        coop2): dict(windows=[(first, count)], tail=window index of the tail
+        check, n_fwd=forwarded reads per iteration); None when the code has no
+        such schedule."""
         L = _lib.lib()
         n, t, f = C.c_int(), C.c_int(), C.c_int()
-        _lib.check(L.ldpc_code_coop_plan(self._h, S, R, None, None, 0, C.byref(n), C.byref(t), C.byref(f)))
+        _lib.check(L.ldpc_code_coop_plan_dist(self._h, S, R, dist, None, None, 0, C.byref(n), C.byref(t),
+                                              C.byref(f)))
         if n.value == 0:
             return None
         first = np.empty(n.value, dtype=np.int32)
         count = np.empty(n.value, dtype=np.int32)
-        _lib.check(L.ldpc_code_coop_plan(self._h, S, R, first.ctypes.data, count.ctypes.data, n.value, C.byref(n),
-                                         C.byref(t), C.byref(f)))
+        _lib.check(L.ldpc_code_coop_plan_dist(self._h, S, R, dist, first.ctypes.data, count.ctypes.data, n.value,
+                                              C.byref(n), C.byref(t), C.byref(f)))
         return dict(windows=list(zip(first.tolist(), count.tolist())), tail=t.value, n_fwd=f.value)
 
     def __del__(self):

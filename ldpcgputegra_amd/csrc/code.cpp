@@ -327,17 +327,24 @@ extern "C" int ldpc_code_window_plan(const ldpc_code *h, int S, int P, int *firs
     return LDPC_OK;
 }
 
-int coop_plan_windows(const ldpc_code *h, int S, int R, std::vector<int> &first, std::vector<int> &count, int *tail,
-                      int *n_fwd);   // coop.hip
+int coop_plan_windows(const ldpc_code *h, int S, int R, int dist, std::vector<int> &first, std::vector<int> &count,
+                      int *tail, int *n_fwd);   // coop.hip
 
 extern "C" int ldpc_code_coop_plan(const ldpc_code *h, int S, int R, int *first, int *count, int max_windows,
                                    int *n_windows, int *tail, int *n_fwd)
 {
-    if (!h || S < 1 || S > 64 || R < 1 || R > 6 || !n_windows) return ldpc_set_error(LDPC_EINVAL, "coop plan args");
+    return ldpc_code_coop_plan_dist(h, S, R, 1, first, count, max_windows, n_windows, tail, n_fwd);
+}
+
+extern "C" int ldpc_code_coop_plan_dist(const ldpc_code *h, int S, int R, int dist, int *first, int *count,
+                                        int max_windows, int *n_windows, int *tail, int *n_fwd)
+{
+    if (!h || S < 1 || S > 64 || R < 1 || R > 6 || dist < 1 || dist > 2 || !n_windows)
+        return ldpc_set_error(LDPC_EINVAL, "coop plan args");
     std::vector<int> f, c;
     int t = -1, nf = 0;
     *n_windows = 0;
-    if (coop_plan_windows(h, S, R, f, c, &t, &nf) != 0) return LDPC_OK;   // no cooperative schedule
+    if (coop_plan_windows(h, S, R, dist, f, c, &t, &nf) != 0) return LDPC_OK;   // no cooperative schedule
     *n_windows = (int)f.size();
     for (int i = 0; i < (int)f.size() && i < max_windows; i++) {
         if (first) first[i] = f[i];

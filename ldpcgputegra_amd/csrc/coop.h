@@ -18,8 +18,8 @@ int coop_upload(const ldpc_code *h, CoopCode *cc);
 void coop_free(CoopCode *cc);
 int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
 // host-side plan (tests: ldpc_code_coop_plan)
-int coop_plan_windows(const ldpc_code *h, int S, int R, std::vector<int> &first, std::vector<int> &count, int *tail,
-                      int *n_fwd);
+int coop_plan_windows(const ldpc_code *h, int S, int R, int dist, std::vector<int> &first, std::vector<int> &count,
+                      int *tail, int *n_fwd);
 
 // ---- window plan shared by coop.hip and coop2.hip ----
 // Slot record [recw] u32: edge variables [D0], meta, forwarding codes (u16 per
@@ -35,8 +35,11 @@ struct CoopPlan {
     int tail = -1, n_fwd = 0;        // window of the tail check; forwarded reads per iteration
     std::vector<uint32_t> tab;       // [nw][S][recw] slot records (want_tab)
 };
-// S <= 64 checks per window, R <= 6 prefetch windows; -1: no cooperative schedule
-int coop_build_plan(const ldpc_code *h, int S, int R, int recw, CoopPlan &o, bool want_tab);
+// S <= 64 checks per window, R <= 6 prefetch windows; windows closer than
+// dist + 1 (1: neighbours, 2: also next-but-one) share no information
+// variable, reads of values written dist+1 .. R+dist windows earlier are
+// forwarded through the LDS ring; -1: no cooperative schedule
+int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPlan &o, bool want_tab);
 
 // ---- coop2.hip: packed-pair variant (two codewords per lane, 16-bit halves) ----
 bool coop2_params_ok(const ldpc_params *p);

@@ -543,9 +543,9 @@ __global__ void early_init_k(int batch, uint8_t *live, uint32_t *bad, int32_t *i
 // previous window.  The tail check (the one check of the second degree group)
 // is a window of its own.  Forwarding: every info-edge read whose latest
 // writer is 2..R+1 windows earlier (cyclic) reads that writer's LDS ring entry.
-int coop_build_plan(const ldpc_code *h, int S, int R, int recw, CoopPlan &o, bool want_tab)
+int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPlan &o, bool want_tab)
 {
-    if (S < 1 || S > 64 || R < 1 || R > 6) return -1;   // forwarding code: 6-bit slot, 3-bit dW
+    if (S < 1 || S > 64 || R < 1 || R > 6 || dist < 1 || dist > 2) return -1;   // forwarding code: 6-bit slot
     if (!h->staircase || h->n_groups != 2 || h->group_cnt[1] != 1) return -1;
     const int D0 = h->group_deg[0], X = D0 - 2, M = h->m, T = M - 1;
     if (h->group_deg[1] != D0 - 1 || X < 1 || X > 8 || M < 4 || M >= (1 << 20)) return -1;
@@ -563,7 +563,7 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int recw, CoopPlan &o, boo
     std::vector<int> mark(h->n, -(1 << 29));
     auto conflict = [&](int c, int u) {
         for (int j = 0; j < X; j++)
-            if (mark[ev(c, j)] >= u - 1) return true;
+            if (mark[ev(c, j)] >= u - dist) return true;
         return false;
     };
     auto take = [&](int c, int u) {
@@ -600,15 +600,17 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int recw, CoopPlan &o, boo
         o.count.push_back(1);
         o.tail = u;
     }
-    {   // the next iteration's window 0 follows the last window
-        const int last = (int)o.first.size() - 1;
+    // the next iteration's first windows follow the last ones: pad with empty
+    // windows until no window within `dist` (cyclically) shares a variable
+    for (;;) {
+        const int nwin = (int)o.first.size();
         bool bad = false;
-        for (int k = 0; k < o.count[0]; k++)
-            for (int j = 0; j < X; j++) bad |= (mark[ev(o.first[0] + k, j)] == last);
-        if (bad) {
-            o.first.push_back(M);
-            o.count.push_back(0);
-        }
+        for (int w0 = 0; w0 < dist && w0 < nwin; w0++)
+            for (int k = 0; k < o.count[w0]; k++)
+                for (int j = 0; j < X; j++) bad |= (mark[ev(o.first[w0] + k, j)] >= nwin + w0 - dist);
+        if (!bad) break;
+        o.first.push_back(M);
+        o.count.push_back(0);
     }
     const int nw = (int)o.first.size();
     if (nw < R + 4) return -1;   // ring / table-ring sizes and parity reuse distance
@@ -626,8 +628,8 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int recw, CoopPlan &o, boo
                     if (pass == 1) {
                         const int gw = lw[v];
                         const int dW = (nw + u) - gw;
-                        if (dW == 1) return -1;   // violates the window rule
-                        if (dW >= 2 && dW <= R + 1) {
+                        if (dW <= dist) return -1;   // violates the window rule
+                        if (dW > dist && dW <= R + dist) {
                             const int w = gw % nw;
                             fwd[((size_t)u * S + k) * X + j] = (uint16_t)(dW << 9 | lk[v] << 3 | lj[v]);
                             src[(size_t)w * S + lk[v]] |= 1u << lj[v];
@@ -686,11 +688,11 @@ bool coop_params_ok(const ldpc_params *p)
            p->msg_max >= 0 && p->msg_max <= 63 && (p->algo == LDPC_ALGO_MS || (p->offset >= 0 && p->offset <= 63));
 }
 
-int coop_plan_windows(const ldpc_code *h, int S, int R, std::vector<int> &first, std::vector<int> &count, int *tail,
-                      int *n_fwd)
+int coop_plan_windows(const ldpc_code *h, int S, int R, int dist, std::vector<int> &first, std::vector<int> &count,
+                      int *tail, int *n_fwd)
 {
     CoopPlan pl;
-    if (coop_build_plan(h, S, R, 0, pl, false) != 0) {
+    if (coop_build_plan(h, S, R, dist, 0, pl, false) != 0) {
         first.clear();
         count.clear();
         return -1;
@@ -715,7 +717,7 @@ int coop_upload(const ldpc_code *h, CoopCode *cc)
     else
         return LDPC_OK;
     CoopPlan pl;
-    if (coop_build_plan(h, 4 * kWS, kR, recw, pl, true) != 0) return LDPC_OK;
+    if (coop_build_plan(h, 4 * kWS, kR, 1, recw, pl, true) != 0) return LDPC_OK;
     if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop tables");
     if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         coop_free(cc);

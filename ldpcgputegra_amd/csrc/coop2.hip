@@ -61,11 +61,14 @@ namespace {
 
 constexpr int CW = 16;     // codewords per workgroup
 constexpr int NP = 8;      // codeword pairs per workgroup = lanes per slot
+constexpr int WS2 = 3;     // slab waves per role: S = 24 checks per window
 constexpr int R2 = 3;      // prefetch depth (windows)
-constexpr int KAHEAD = R2 + 4;   // window tables are DMA'd into LDS this many windows ahead of the chain
-constexpr int DPER = 3;          // ... and waited for DPER periods later (window p+R+1 is read at period p)
-constexpr int TQ = 16;           // window-table slots in LDS (>= KAHEAD + 2)
-constexpr int RING = 4;    // forwarding ring windows (>= R2)
+constexpr int DIST = 2;    // windows closer than DIST + 1 share no information variable (plan rule)
+constexpr int DPER = 3;    // a window table's LDS-DMA is waited for DPER periods after its issue
+constexpr int KAHEAD = R2 + 2 + DPER;   // ... which is KAHEAD windows ahead of the chain
+constexpr int TQ = 16;     // window-table slots in LDS (>= KAHEAD + 2)
+constexpr int RING = 8;    // forwarding ring windows (>= R2 + DIST)
+constexpr int NSB = 4;     // pre -> post state buffers (a window's state lives 3 periods)
 constexpr int MREC = 64;   // message bytes per check and workgroup (8 pairs x 8 B)
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -111,7 +114,14 @@ constexpr uint32_t SIGNS = 0x80008000u;
 
 LDPC_DEV uint32_t unpack_v(uint32_t raw, uint32_t sel) { return perm(raw, raw, sel); }   // V dword -> R pair
 LDPC_DEV uint32_t pack_v(uint32_t r) { return perm(r, r, 0x0c0c0301u); }           // R pair -> u16 [b0 b1]
-LDPC_DEV uint32_t abs_r(uint32_t r) { return pk_max(r, pk_sub(C510, r)); }
+LDPC_DEV uint32_t abs_r(uint32_t r, uint32_t c510) { return pk_max(r, pk_sub(c510, r)); }
+
+// the packed-math constants, held in VGPRs: as SGPR operands hipcc splats
+// them with op_sel_hi, and gfx950 then needs a wait state before the result
+// is read
+struct PkK {
+    uint32_t neg127, r0, c510, rmm, coff;   // R(-127), R(0), 510, R(msg_max), C(offset) per half
+};
 
 // byte tables [+cst1, -cst1, +cst2, -cst2] of the two codewords of a pair
 struct MsgTab {
@@ -137,13 +147,14 @@ LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t)
 
 // new message of edge J: its code into MA, the new V (R pair) returned
 template <int J>
-LDPC_DEV uint32_t new_msg(uint32_t c, uint32_t a, uint32_t min1, uint32_t k1, uint32_t k2, uint32_t P, uint32_t &MA)
+LDPC_DEV uint32_t new_msg(uint32_t c, uint32_t a, uint32_t min1, uint32_t k1, uint32_t k2, uint32_t P, uint32_t &MA,
+                          uint32_t neg127)
 {
     const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));   // -1: a > min1, the edge gets cst2
     const uint32_t rr = bfi(neq, k2, k1);
     const uint32_t sgn = pk_sra15(c ^ P);             // -1: the message is negative
     MA |= (sgn & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
-    return pk_max(pk_add_sat(c, pk_sub(rr ^ sgn, sgn)), RNEG127);
+    return pk_max(pk_add_sat(c, pk_sub(rr ^ sgn, sgn)), neg127);
 }
 
 template <int I, int N, typename F>
@@ -179,6 +190,7 @@ struct alignas(16) Smem2 {
     int2 cst1[2][S][CW];           //                 (L, H)
     int xin[2][CW][S];             // clamped x input of each slot      (chain -> post)
     uint32_t ring[RING][S][X][NP]; // V pairs (R form) of the last windows, for forwarding
+    uint4 st[NSB][WS][4][64];      // one window's St2 per lane          (pre -> post)
 };
 
 template <int D0>
@@ -188,12 +200,15 @@ struct Pf2 {                       // prefetched raw inputs of one window
 };
 
 template <int D0>
-struct St2 {                       // one window between pre and post (R / C pairs)
+struct St2 {                       // one window between pre and post (R / C pairs): 16 dwords
     uint32_t c[D0 - 1];            // contributions (info, o); tail: new V
     uint32_t a[D0 - 1];            // |c| clipped
     uint32_t mx, min1, min2, sacc; // tail: min1 = MA, min2 = MB
 };
+static_assert(sizeof(St2<7>) == 64, "pre -> post state is four uint4 per lane");
 
+// one slab wave: lane = (slot k, codeword pair q); the same slots in the pre
+// role (prefetch + pre) and in the post role
 template <int D0, int WS>
 struct Slab2 {
     using SM = Smem2<D0, WS>;
@@ -201,8 +216,9 @@ struct Slab2 {
     SM &sm;
     const Coop2Args &a;
     i32x4 vr, mr;                  // V rows of this group (stride pitch), message rows (stride 64)
-    int k, q, tail;
+    int k, q, w, lane, tail;
     uint32_t usel;                 // v_perm selector: this pair's two bytes of a V dword -> R pair
+    PkK K;
 
     // whole aligned dwords (two pairs): a u16 load result carried across the
     // loop back-edge gets a zero-extension there, which waits for the load
@@ -228,7 +244,7 @@ struct Slab2 {
         pf.mb = (uint32_t)m.y;
     }
 
-    // V pairs written 2..R+1 windows ago replace the loaded ones (rare)
+    // V pairs written DIST+1 .. R+DIST windows ago replace the loaded ones (rare)
     LDPC_DEV void forward(int ts, int g, uint32_t *v) const
     {
         const uint32_t *r = sm.tab[ts][k];
@@ -243,24 +259,26 @@ struct Slab2 {
         }
     }
 
-    // pre of window g (table slot ts, constant buffer cb, local index u)
-    LDPC_DEV void pre(int ts, int cb, int g, int u, const Pf2<D0> &pf, St2<D0> &s) const
+    // pre of window g (local index u): chain constants -> cst[g & 1], state -> st[g % NSB]
+    LDPC_DEV void pre(int g, int u, const Pf2<D0> &pf) const
     {
+        const int ts = g & (TQ - 1), cb = g & 1;
         const uint32_t meta = sm.tab[ts][k][D0];
         uint32_t v[D0 - 1];
 #pragma unroll
         for (int j = 0; j < D0 - 1; j++) v[j] = unpack_v(pf.v[j], usel);
         if (__any((meta & COOP_M_FWD) != 0)) forward(ts, g, v);
         const MsgTab t = msg_tab(pf.mb);
-        const uint32_t MA = pf.ma, rmm = a.rmm, coff = a.coff;
+        const uint32_t MA = pf.ma, rmm = K.rmm, coff = K.coff, neg127 = K.neg127;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
+        St2<D0> s;
         int eps[2], A[2], B[2], co[2], L[2], H[2];
         if (u != tail) {
             // first degree group: a = min(|c|, msg_max) (OMS_fixed_SSE.cpp:211)
             static_for<0, X>([&](auto jc) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), RNEG127);
-                const uint32_t aj = pk_min(abs_r(c), rmm);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
+                const uint32_t aj = pk_min(abs_r(c, K.c510), rmm);
                 s.c[J] = c;
                 s.a[J] = aj;
                 sacc ^= c;
@@ -271,10 +289,10 @@ struct Slab2 {
             // eps = -1 iff the info edges' sign parity (odd-degree flip
             // included) is odd, co = the o-edge contribution, mx = the x-edge
             // old message
-            const uint32_t T = pk_max(pk_sub(min1, coff), R0);
+            const uint32_t T = pk_max(pk_sub(min1, coff), K.r0);
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
-            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), RNEG127);
-            const uint32_t ao = pk_min(abs_r(cor), rmm);
+            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), neg127);
+            const uint32_t ao = pk_min(abs_r(cor, K.c510), rmm);
             s.c[X] = cor;
             s.a[X] = ao;
             s.sacc = sacc ^ cor;
@@ -297,22 +315,24 @@ struct Slab2 {
             // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
             static_for<0, X + 1>([&](auto jc) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), RNEG127);
-                const uint32_t aj = abs_r(pk_min(c, rmm));
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
+                const uint32_t aj = abs_r(pk_min(c, rmm), K.c510);
                 s.c[J] = c;
                 s.a[J] = aj;
                 sacc ^= c;
                 min2 = pk_max(min1, pk_min(aj, min2));
                 min1 = pk_min(min1, aj);
             });
-            const uint32_t k1 = pk_min(pk_max(pk_sub(min2, coff), R0), rmm) & HIBYTES;
-            const uint32_t k2 = pk_min(pk_max(pk_sub(min1, coff), R0), rmm) & HIBYTES;
+            const uint32_t k1 = pk_min(pk_max(pk_sub(min2, coff), K.r0), rmm) & HIBYTES;
+            const uint32_t k2 = pk_min(pk_max(pk_sub(min1, coff), K.r0), rmm) & HIBYTES;
             const uint32_t P = (sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u)) & SIGNS;
             uint32_t MAn = 0;
             static_for<0, X + 1>([&](auto jc) {
                 constexpr int J = decltype(jc)::value;
-                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn);
+                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn, neg127);
             });
+            s.mx = 0;
+            s.sacc = 0;
             s.min1 = MAn;
             s.min2 = perm(k2, k1, 0x07030501u);
 #pragma unroll
@@ -338,11 +358,19 @@ struct Slab2 {
             sm.cst0[cb][k][2 * q + h] = make_int4(eps[h], A[h], B[h], co[h]);
             sm.cst1[cb][k][2 * q + h] = make_int2(L[h], H[h]);
         }
+        const uint4 *sp = (const uint4 *)&s;
+#pragma unroll
+        for (int i = 0; i < 4; i++) sm.st[g & (NSB - 1)][w][i][lane] = sp[i];
     }
 
-    // post of the window in table slot ts (x inputs in buffer xb, ring slot rs)
-    LDPC_DEV void post(int ts, int xb, int rs, int u, const St2<D0> &s) const
+    // post of window g (local index u): state from st[g % NSB], x inputs from xin[g & 1]
+    LDPC_DEV void post(int g, int u) const
     {
+        const int ts = g & (TQ - 1), xb = g & 1, rs = g & (RING - 1);
+        St2<D0> s;
+        uint4 *sp = (uint4 *)&s;
+#pragma unroll
+        for (int i = 0; i < 4; i++) sp[i] = sm.st[g & (NSB - 1)][w][i][lane];
         const uint32_t *r = sm.tab[ts][k];
         uint32_t var[D0];
 #pragma unroll
@@ -352,23 +380,23 @@ struct Slab2 {
         const uint32_t xr = perm(x1, x0, 0x040d000du);   // clamped by the chain -> R pair
         uint32_t MA, MB;
         if (u != tail) {
-            const uint32_t cx = pk_max(pk_sub_sat(xr, s.mx), RNEG127);
-            const uint32_t ax = pk_min(abs_r(cx), a.rmm);
+            const uint32_t cx = pk_max(pk_sub_sat(xr, s.mx), K.neg127);
+            const uint32_t ax = pk_min(abs_r(cx, K.c510), K.rmm);
             const uint32_t sacc = s.sacc ^ cx;
             const uint32_t min2 = pk_max(s.min1, pk_min(ax, s.min2)), min1 = pk_min(ax, s.min1);
-            const uint32_t k1 = pk_max(pk_sub(min2, a.coff), R0) & HIBYTES;   // <= msg_max already
-            const uint32_t k2 = pk_max(pk_sub(min1, a.coff), R0) & HIBYTES;
+            const uint32_t k1 = pk_max(pk_sub(min2, K.coff), K.r0) & HIBYTES;   // <= msg_max already
+            const uint32_t k2 = pk_max(pk_sub(min1, K.coff), K.r0) & HIBYTES;
             const uint32_t P = (sacc ^ ((D0 & 1) ? SIGNS : 0u)) & SIGNS;
             MA = 0;
             static_for<0, X>([&](auto jc) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t vn = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA);
+                const uint32_t vn = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
                 stv(var[J], vn);
                 sm.ring[rs][k][J][q] = vn;
             });
-            stv(var[X], new_msg<X>(cx, ax, min1, k1, k2, P, MA));
+            stv(var[X], new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127));
             // the o edge: message bits only (the next check rewrites V[o] as its x edge)
-            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA);
+            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
             MB = perm(k2, k1, 0x07030501u);
         } else {
             static_for<0, X>([&](auto jc) {
@@ -442,14 +470,23 @@ LDPC_DEV unsigned long long stamp()
     return t;
 }
 
+// Waves: 0 .. WS-1 "pre" (loads + pre), WS the chain, WS+1 .. 2 WS "post".
+// Workgroup waves go to the SIMDs cyclically, so pre wave i and post wave i
+// share a SIMD and the chain has one of its own.  One barrier per period p:
+//   chain: steps of window p; LDS-DMA of the table of window p + KAHEAD
+//   pre:   loads of window p+1+R, pre of window p+1
+//   post:  post of window p-1
+// The plan keeps windows within DIST = 2 free of shared information
+// variables, so post(p-1) and pre(p+1) need no ordering; values written 3 ..
+// R+2 windows before a pre are forwarded through the LDS ring, and every
+// other earlier write is ordered before the loads by a barrier.
 template <int D0, int WS, bool STAMP>
-__global__ void __launch_bounds__(64 * (WS + 1)) coop2_decode(Coop2Args a)
+__global__ void __launch_bounds__(64 * (2 * WS + 1)) coop2_decode(Coop2Args a)
 {
     using SM = Smem2<D0, WS>;
     constexpr int S = SM::S, X = SM::X, RECW = SM::RECW, R = R2;
-    constexpr int U = 4;                      // lcm(2, R + 1): prefetch and state buffers repeat
-    constexpr int SPLIT = (S / 2) & ~3;       // chain steps before barrier A
-    static_assert(TQ >= R + 4 && RING >= R && (R + 1) % 4 == 0, "ring sizes");
+    constexpr int U = R + 1;                  // prefetch buffers repeat
+    static_assert(TQ >= KAHEAD + 2 && RING >= R + DIST && (NSB & (NSB - 1)) == 0 && NSB >= 3, "ring sizes");
     __shared__ SM sm;
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -458,16 +495,25 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop2_decode(Coop2Args a)
     const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
     const int G = a.G;
     if (G == 0) return;
-    unsigned long long sA = 0, sB = 0, t0 = 0, tx = 0;
+    unsigned long long sA = 0, t0 = 0, tx = 0;
+    auto write_stamps = [&]() {
+        if (STAMP && lane == 0) {
+            unsigned long long *o = a.stamps + ((size_t)id * (2 * WS + 1) + wave) * 4;
+            o[0] = sA;
+            o[1] = 0;
+            o[2] = stamp() - t0;
+            o[3] = (unsigned long long)G;
+        }
+    };
 
     if (wave == WS) {
         // ------------------------------------------------------------ chain wave
         if (a.prio) __builtin_amdgcn_s_setprio(2);
         constexpr int NCH = S * RECW / 4;   // 16-B chunks per window table
         constexpr int CPL = (NCH + 63) / 64;
-        static_assert(TQ >= KAHEAD + 2 && KAHEAD >= R + 1 + DPER && CPL * DPER <= 63, "table staging");
+        static_assert(CPL * DPER <= 63, "table staging");
         const int c = lane & 15;
-        // window u's slot records -> LDS slot u % TQ by LDS-DMA, CPL instructions
+        // window u's slot records -> LDS slot by LDS-DMA, CPL instructions
         auto stage = [&](int u, int slot) {
             const uint4 *src = (const uint4 *)(a.tab + (size_t)u * S * RECW);
             const uint32_t dst = (uint32_t)(uintptr_t)&sm.tab[slot][0][0];
@@ -479,99 +525,89 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop2_decode(Coop2Args a)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int Y = a.V[(size_t)a.tab[X] * (uint32_t)a.pitch + (uint32_t)(wg * CW + c)];   // x input of check 0
         int un = KAHEAD % a.nw;
-        __syncthreads();   // prologue: tables in LDS
-        __syncthreads();   // pre(0) done: constants of window 0 in LDS
+        __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 in LDS
+        __syncthreads();   // prologue 2: constants of window 0 in LDS
         const bool cl = lane < CW;
         if (STAMP) t0 = stamp();
-        auto period = [&](auto, int p) {
+        for (int p = 0; p <= G; p++) {
             if (STAMP) tx = stamp();
-            if (p < G && cl) chain_steps2<D0, WS, 0, SPLIT>(sm, p & 1, c, Y);
-            stage(un, (p + KAHEAD) & (TQ - 1));   // window p+KAHEAD
+            if (p < G && cl) chain_steps2<D0, WS, 0, S>(sm, p & 1, c, Y);
+            stage(un, (p + KAHEAD) & (TQ - 1));
             un = (un + 1 == a.nw) ? 0 : un + 1;
-            // the tables DMA'd DPER periods ago (window p+R+1 at the latest,
-            // prefetched by the slab waves after barrier A) have landed
+            // the tables DMA'd DPER periods ago have landed (the next period's
+            // loads read window p+R+2, issued at period p+R+2-KAHEAD = p-DPER)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPL * DPER) : "memory");
             if (STAMP) sA += stamp() - tx;
-            __syncthreads();   // A
-            if (STAMP) tx = stamp();
-            if (p < G && cl) chain_steps2<D0, WS, SPLIT, S>(sm, p & 1, c, Y);
-            if (STAMP) sB += stamp() - tx;
-            __syncthreads();   // B
-        };
-        for (int p = 0; p <= G; p += 2) {
-            period(std::integral_constant<int, 0>{}, p);
-            if (p + 1 <= G) period(std::integral_constant<int, 1>{}, p + 1);
+            __syncthreads();
         }
-        if (STAMP && lane == 0) {
-            unsigned long long *o = a.stamps + ((size_t)id * (WS + 1) + wave) * 4;
-            o[0] = sA;
-            o[1] = sB;
-            o[2] = stamp() - t0;
-            o[3] = (unsigned long long)G;
-        }
+        write_stamps();
         return;
     }
 
-    // -------------------------------------------------------------- slab waves
+    const bool is_pre = wave < WS;
+    const int w = is_pre ? wave : wave - WS - 1;
     Slab2<D0, WS> sl{sm,
                      a,
                      buffer_rsrc(a.V + (size_t)wg * CW, (uint32_t)a.pitch, (uint32_t)(a.n + 1)),
                      buffer_rsrc(a.Mc + (size_t)wg * a.mrows * MREC, (uint32_t)MREC, (uint32_t)a.mrows),
-                     8 * wave + (lane >> 3),
+                     8 * w + (lane >> 3),
                      lane & 7,
+                     w,
+                     lane,
                      a.tail,
-                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u};
-    Pf2<D0> pf[R + 1];
-    St2<D0> st[2];
-    __syncthreads();   // prologue: tables of windows 0 .. R+1 are in LDS
-#pragma unroll
-    for (int i = 0; i <= R; i++) sl.prefetch(i, pf[i]);   // nw > R + 3
-    sl.pre(0, 0, 0, 0, pf[0], st[0]);
-    // period 0: chain(0) | nothing to post | loads of R+1, pre(1)
-    __syncthreads();   // B of the prologue
-    __syncthreads();   // A(0)
-    sl.prefetch(R + 1, pf[0]);
-    sl.pre(1, 1, 1, 1 % a.nw, pf[1], st[1]);
-    __syncthreads();   // B(0)
-    int uA = 0, uB = 2 % a.nw;   // local index of windows p-1, p+1
+                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
+                     PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)}};
     auto next = [&](int &u) { u = (u + 1 == a.nw) ? 0 : u + 1; };
-    if (STAMP) t0 = stamp();
-    // steady state p = 1 .. G: every memory operation unconditional (loads past
-    // the end read valid table rows; their pre only writes unused constants)
-    auto step = [&](auto sc, int p) {
-        constexpr int s = decltype(sc)::value;
-        if (STAMP) tx = stamp();
-        sl.post((p - 1) & (TQ - 1), (p - 1) & 1, (p - 1) & (RING - 1), uA, st[s % 2]);
-        if (STAMP) sA += stamp() - tx;
-        __syncthreads();   // A(p)
-        if (STAMP) tx = stamp();
-        sl.prefetch((p + 1 + R) & (TQ - 1), pf[(s + 1) % (R + 1)]);
-        sl.pre((p + 1) & (TQ - 1), (p + 1) & 1, p + 1, uB, pf[(s + 2) % (R + 1)], st[s % 2]);
-        if (STAMP) sB += stamp() - tx;
-        __syncthreads();   // B(p)
-        next(uA);
-        next(uB);
-    };
-    // single-exit loop over whole unroll groups, then the remainder
-    const int nfull = G / U;
-    int p = 1;
-    for (int i = 0; i < nfull; i++, p += U) {
-        step(std::integral_constant<int, 0>{}, p);
-        step(std::integral_constant<int, 1>{}, p + 1);
-        step(std::integral_constant<int, 2>{}, p + 2);
-        step(std::integral_constant<int, 3>{}, p + 3);
+    __syncthreads();   // prologue 1: tables in LDS
+
+    if (is_pre) {
+        // ------------------------------------------------------ pre waves
+        Pf2<D0> pf[R + 1];
+#pragma unroll
+        for (int i = 0; i <= R; i++) sl.prefetch(i, pf[i]);   // nw > R + 3
+        sl.pre(0, 0, pf[0]);
+        __syncthreads();   // prologue 2
+        if (STAMP) t0 = stamp();
+        int uB = 1 % a.nw;   // local index of window p+1
+        // period p: loads of window p+1+R into pf[(p+R+1) % U], pre of window
+        // p+1 from pf[(p+1) % U]
+        auto step = [&](auto sc, int p) {
+            constexpr int s = decltype(sc)::value;   // p % U
+            if (STAMP) tx = stamp();
+            sl.prefetch((p + 1 + R) & (TQ - 1), pf[(s + R + 1) % U]);
+            sl.pre(p + 1, uB, pf[(s + 1) % U]);
+            if (STAMP) sA += stamp() - tx;
+            __syncthreads();
+            next(uB);
+        };
+        const int np = G + 1, nfull = np / U;
+        int p = 0;
+        for (int i = 0; i < nfull; i++, p += U) {
+            step(std::integral_constant<int, 0>{}, p);
+            step(std::integral_constant<int, 1>{}, p + 1);
+            step(std::integral_constant<int, 2>{}, p + 2);
+            step(std::integral_constant<int, 3>{}, p + 3);
+        }
+        static_assert(U == 4, "unroll");
+        const int rem = np - nfull * U;
+        if (rem > 0) step(std::integral_constant<int, 0>{}, p);
+        if (rem > 1) step(std::integral_constant<int, 1>{}, p + 1);
+        if (rem > 2) step(std::integral_constant<int, 2>{}, p + 2);
+    } else {
+        // ----------------------------------------------------- post waves
+        __syncthreads();   // prologue 2
+        if (STAMP) t0 = stamp();
+        __syncthreads();   // period 0: nothing to post yet
+        int uA = 0;        // local index of window p-1
+        for (int p = 1; p <= G; p++) {
+            if (STAMP) tx = stamp();
+            sl.post(p - 1, uA);
+            if (STAMP) sA += stamp() - tx;
+            __syncthreads();
+            next(uA);
+        }
     }
-    const int rem = G - nfull * U;
-    if (rem > 0) step(std::integral_constant<int, 0>{}, p);
-    if (rem > 1) step(std::integral_constant<int, 1>{}, p + 1);
-    if (rem > 2) step(std::integral_constant<int, 2>{}, p + 2);
-    if (STAMP && lane == 0) {
-        unsigned long long *o = a.stamps + ((size_t)id * (WS + 1) + wave) * 4;
-        o[0] = sA;
-        o[1] = sB;
-        o[2] = stamp() - t0;
-        o[3] = (unsigned long long)G;
-    }
+    write_stamps();
 }
 
 __global__ void fill_iters2_k(int batch, int32_t *iters_used, int iters)
@@ -587,46 +623,40 @@ int env_int(const char *name, int def)
 }
 
 // diagnostic build (LDPC_COOP2_STAMP=1): per-period cycles of each wave role
-void report_stamps(const unsigned long long *d, int grid, int nwaves, hipStream_t s)
+void report_stamps(const unsigned long long *d, int grid, hipStream_t s)
 {
+    constexpr int nwaves = 2 * WS2 + 1;
     std::vector<unsigned long long> h((size_t)grid * nwaves * 4);
     if (hipStreamSynchronize(s) != hipSuccess ||
         hipMemcpy(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
         return;
-    double ch[3] = {0, 0, 0}, sl[3] = {0, 0, 0}, slmax[2] = {0, 0};
+    // role: 0 pre, 1 chain, 2 post; work = cycles between the period's barriers
+    double work[3] = {0, 0, 0}, wmax[3] = {0, 0, 0}, total = 0;
+    int cnt[3] = {0, 0, 0};
     for (int b = 0; b < grid; b++)
         for (int w = 0; w < nwaves; w++) {
             const unsigned long long *o = &h[((size_t)b * nwaves + w) * 4];
             const double G = o[3] ? (double)o[3] : 1.0;
-            double *acc = (w == nwaves - 1) ? ch : sl;
-            for (int i = 0; i < 3; i++) acc[i] += o[i] / G;
-            if (w < nwaves - 1) {
-                slmax[0] = std::max(slmax[0], o[0] / G);
-                slmax[1] = std::max(slmax[1], o[1] / G);
-            }
+            const int role = w < WS2 ? 0 : (w == WS2 ? 1 : 2);
+            work[role] += o[0] / G;
+            wmax[role] = std::max(wmax[role], o[0] / G);
+            cnt[role]++;
+            total += o[2] / G;
         }
-    const double ns = (double)grid * (nwaves - 1);
     fprintf(stderr,
-            "coop2 stamps [cycles per period]: chain A %.0f B %.0f total %.0f | slab post %.0f pre %.0f "
-            "(max wave %.0f %.0f) total %.0f\n",
-            ch[0] / grid, ch[1] / grid, ch[2] / grid, sl[0] / ns, sl[1] / ns, slmax[0], slmax[1], sl[2] / ns);
+            "coop2 stamps [cycles per period]: total %.0f | pre %.0f (max %.0f) | chain %.0f (max %.0f) | "
+            "post %.0f (max %.0f)\n",
+            total / (grid * nwaves), work[0] / cnt[0], wmax[0], work[1] / cnt[1], wmax[1], work[2] / cnt[2], wmax[2]);
 }
 
-template <int WS>
 int launch_ws(const Coop2Args &a, int grid, bool stamped, hipStream_t s)
 {
+    constexpr int threads = 64 * (2 * WS2 + 1);
     if (stamped)
-        hipLaunchKernelGGL((coop2_decode<7, WS, true>), dim3(grid), dim3(64 * (WS + 1)), 0, s, a);
+        hipLaunchKernelGGL((coop2_decode<7, WS2, true>), dim3(grid), dim3(threads), 0, s, a);
     else
-        hipLaunchKernelGGL((coop2_decode<7, WS, false>), dim3(grid), dim3(64 * (WS + 1)), 0, s, a);
+        hipLaunchKernelGGL((coop2_decode<7, WS2, false>), dim3(grid), dim3(threads), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// slab waves per workgroup (S = 8 WS checks per window); LDPC_COOP2_WS overrides
-int coop2_ws()
-{
-    const int ws = env_int("LDPC_COOP2_WS", 3);
-    return (ws == 3 || ws == 4) ? ws : 3;
 }
 
 }  // namespace
@@ -643,9 +673,9 @@ int coop2_upload(const ldpc_code *h, CoopCode *cc)
     *cc = CoopCode{};
     constexpr int D0 = 7, X = D0 - 2, RECW = Geo<D0>::RECW;
     if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return LDPC_OK;
-    const int S = 8 * coop2_ws();
+    const int S = 8 * WS2;
     CoopPlan pl;
-    if (coop_build_plan(h, S, R2, RECW, pl, true) != 0) return LDPC_OK;
+    if (coop_build_plan(h, S, R2, DIST, RECW, pl, true) != 0) return LDPC_OK;
     const int nw = (int)pl.first.size();
     for (int u = 0; u < nw; u++)
         for (int k = 0; k < S; k++) {
@@ -694,16 +724,16 @@ int launch_coop2(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.prio = env_int("LDPC_COOP2_PRIO", 1);
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0;
-    const int nwaves = cc.S / 8 + 1;
+    const int nwaves = 2 * WS2 + 1;
     const bool stamped = env_int("LDPC_COOP2_STAMP", 0) != 0;
     if (stamped) {
         const size_t bytes = (size_t)grid * nwaves * 4 * sizeof(unsigned long long);
         if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
-    const int rc = (cc.S == 24) ? launch_ws<3>(a, grid, stamped, s) : launch_ws<4>(a, grid, stamped, s);
+    const int rc = launch_ws(a, grid, stamped, s);
     if (stamped) {
-        if (rc == 0) report_stamps(a.stamps, grid, nwaves, s);
+        if (rc == 0) report_stamps(a.stamps, grid, s);
         (void)hipFree(a.stamps);
     }
     return rc;

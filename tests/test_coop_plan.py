@@ -24,10 +24,10 @@ def checks(t):
 
 
 @pytest.mark.parametrize("code", ["dvbs2_r1_2", "dvbs2_r2_3"])
-@pytest.mark.parametrize("S,R", [(24, 3), (28, 3), (28, 4), (32, 3)])
-def test_coop_plan_rules(code, S, R):
+@pytest.mark.parametrize("S,R,dist", [(24, 3, 1), (28, 3, 1), (28, 4, 1), (32, 3, 1), (24, 3, 2)])
+def test_coop_plan_rules(code, S, R, dist):
     t = load_table(code)
-    plan = Code(code).coop_plan(S, R)
+    plan = Code(code).coop_plan(S, R, dist)
     assert plan is not None
     ch = checks(t)
     M, D0 = t.m, t.groups[0][0]
@@ -54,8 +54,9 @@ def test_coop_plan_rules(code, S, R):
             s |= info[c]
         wvars.append(s)
     for u in range(nw):
-        assert not (wvars[u] & wvars[u - 1]), "consecutive windows share a variable (u=%d)" % u
-    # forwarded reads: latest earlier touch 2..R+1 windows back (cyclic)
+        for d in range(1, dist + 1):
+            assert not (wvars[u] & wvars[u - d]), "windows %d apart share a variable (u=%d)" % (d, u)
+    # forwarded reads: latest earlier touch dist+1 .. R+dist windows back (cyclic)
     last = {}
     for u, (first, cnt) in enumerate(wins):
         for c in range(first, first + cnt):
@@ -66,12 +67,12 @@ def test_coop_plan_rules(code, S, R):
         for c in range(first, first + cnt):
             for v in ch[c][:X]:
                 d = (u - last[v]) % nw or nw
-                if 2 <= d <= R + 1:
+                if dist + 1 <= d <= R + dist:
                     nf += 1
                 last[v] = u
     assert nf == plan["n_fwd"]
     # windows are mostly full and forwarding is rare
-    assert (M - 1) / (nw * S) > 0.85
+    assert (M - 1) / (nw * S) > (0.85 if dist == 1 else 0.8)
     assert plan["n_fwd"] < 0.05 * (M * X)
 
 
