@@ -61,14 +61,14 @@ namespace {
 
 constexpr int CW = 16;     // codewords per workgroup
 constexpr int NP = 8;      // codeword pairs per workgroup = lanes per slot
-constexpr int WS2 = 3;     // slab waves per role: S = 24 checks per window
+constexpr int WS_DEFAULT = 3;   // slab waves per role (S = 8 WS checks per window); LDPC_COOP2_WS = 3 | 4
 constexpr int R2 = 3;      // prefetch depth (windows)
 constexpr int DIST = 2;    // windows closer than DIST + 1 share no information variable (plan rule)
 constexpr int DPER = 3;    // a window table's LDS-DMA is waited for DPER periods after its issue
 constexpr int KAHEAD = R2 + 2 + DPER;   // ... which is KAHEAD windows ahead of the chain
 constexpr int TQ = 16;     // window-table slots in LDS (>= KAHEAD + 2)
 constexpr int RING = 8;    // forwarding ring windows (>= R2 + DIST)
-constexpr int NSB = 4;     // pre -> post state buffers (a window's state lives 3 periods)
+constexpr int NSB = 3;     // pre -> post state buffers (a window's state lives 3 periods)
 constexpr int MREC = 64;   // message bytes per check and workgroup (8 pairs x 8 B)
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -172,6 +172,7 @@ struct Coop2Args {
     const uint32_t *tab;           // [nw][S][RECW] slot records
     unsigned long long *stamps;    // diagnostic build: [grid][waves][4]
     int pitch, G, nw, tail, mrows, n, remap, prio, off;
+    int pre_prio, post_prio;       // s_setprio of the pre / post waves (the chain wave: prio ? 2 : 0)
     uint32_t rmm, coff;            // R(msg_max), C(offset) per half
 };
 
@@ -360,7 +361,7 @@ struct Slab2 {
         }
         const uint4 *sp = (const uint4 *)&s;
 #pragma unroll
-        for (int i = 0; i < 4; i++) sm.st[g & (NSB - 1)][w][i][lane] = sp[i];
+        for (int i = 0; i < 4; i++) sm.st[(unsigned)g % NSB][w][i][lane] = sp[i];
     }
 
     // post of window g (local index u): state from st[g % NSB], x inputs from xin[g & 1]
@@ -370,7 +371,7 @@ struct Slab2 {
         St2<D0> s;
         uint4 *sp = (uint4 *)&s;
 #pragma unroll
-        for (int i = 0; i < 4; i++) sp[i] = sm.st[g & (NSB - 1)][w][i][lane];
+        for (int i = 0; i < 4; i++) sp[i] = sm.st[(unsigned)g % NSB][w][i][lane];
         const uint32_t *r = sm.tab[ts][k];
         uint32_t var[D0];
 #pragma unroll
@@ -420,8 +421,10 @@ struct Slab2 {
 // codewords (lanes 0..15): the recurrence of coop.hip, one asm block per step
 // (clamped x input for post, two mad24, two med3) so that hipcc pads no
 // wait states between its four dependent instructions
-template <int D0, int WS, int K0, int K1>
-LDPC_DEV void chain_steps2(Smem2<D0, WS> &sm, int buf, int c, int &Y)
+LDPC_DEV unsigned long long stamp();
+
+template <int D0, int WS, int K0, int K1, bool STAMP = false>
+LDPC_DEV void chain_steps2(Smem2<D0, WS> &sm, int buf, int c, int &Y, unsigned long long *sL = nullptr)
 {
     constexpr int NK = K1 - K0;
     int4 q0[NK];
@@ -430,6 +433,11 @@ LDPC_DEV void chain_steps2(Smem2<D0, WS> &sm, int buf, int c, int &Y)
     for (int i = 0; i < NK; i++) {
         q0[i] = sm.cst0[buf][K0 + i][c];
         q1[i] = sm.cst1[buf][K0 + i][c];
+    }
+    if constexpr (STAMP) {   // diagnostic: the constants' LDS latency apart from the steps
+        const unsigned long long t = stamp();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        *sL += stamp() - t;
     }
     const int lo = -127, hi = 127;
     int xv[4];
@@ -486,7 +494,7 @@ __global__ void __launch_bounds__(64 * (2 * WS + 1)) coop2_decode(Coop2Args a)
     using SM = Smem2<D0, WS>;
     constexpr int S = SM::S, X = SM::X, RECW = SM::RECW, R = R2;
     constexpr int U = R + 1;                  // prefetch buffers repeat
-    static_assert(TQ >= KAHEAD + 2 && RING >= R + DIST && (NSB & (NSB - 1)) == 0 && NSB >= 3, "ring sizes");
+    static_assert(TQ >= KAHEAD + 2 && RING >= R + DIST && NSB >= 3, "ring sizes");
     __shared__ SM sm;
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -495,14 +503,14 @@ __global__ void __launch_bounds__(64 * (2 * WS + 1)) coop2_decode(Coop2Args a)
     const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
     const int G = a.G;
     if (G == 0) return;
-    unsigned long long sA = 0, t0 = 0, tx = 0;
+    unsigned long long sA = 0, sB = 0, sL = 0, t0 = 0, tx = 0;
     auto write_stamps = [&]() {
         if (STAMP && lane == 0) {
             unsigned long long *o = a.stamps + ((size_t)id * (2 * WS + 1) + wave) * 4;
             o[0] = sA;
-            o[1] = 0;
+            o[1] = sB | sL << 32;
             o[2] = stamp() - t0;
-            o[3] = (unsigned long long)G;
+            o[3] = (unsigned long long)G | (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) << 32;
         }
     };
 
@@ -531,7 +539,15 @@ __global__ void __launch_bounds__(64 * (2 * WS + 1)) coop2_decode(Coop2Args a)
         if (STAMP) t0 = stamp();
         for (int p = 0; p <= G; p++) {
             if (STAMP) tx = stamp();
-            if (p < G && cl) chain_steps2<D0, WS, 0, S>(sm, p & 1, c, Y);
+            if (p < G && cl) {
+                if constexpr (S <= 24) {
+                    chain_steps2<D0, WS, 0, S, STAMP>(sm, p & 1, c, Y, &sL);
+                } else {   // constants of 16 steps at a time (VGPRs)
+                    chain_steps2<D0, WS, 0, S / 2, STAMP>(sm, p & 1, c, Y, &sL);
+                    chain_steps2<D0, WS, S / 2, S, STAMP>(sm, p & 1, c, Y, &sL);
+                }
+            }
+            if (STAMP) sB += stamp() - tx;
             stage(un, (p + KAHEAD) & (TQ - 1));
             un = (un + 1 == a.nw) ? 0 : un + 1;
             // the tables DMA'd DPER periods ago have landed (the next period's
@@ -562,6 +578,7 @@ __global__ void __launch_bounds__(64 * (2 * WS + 1)) coop2_decode(Coop2Args a)
 
     if (is_pre) {
         // ------------------------------------------------------ pre waves
+        if (a.pre_prio) __builtin_amdgcn_s_setprio(1);
         Pf2<D0> pf[R + 1];
 #pragma unroll
         for (int i = 0; i <= R; i++) sl.prefetch(i, pf[i]);   // nw > R + 3
@@ -595,6 +612,7 @@ __global__ void __launch_bounds__(64 * (2 * WS + 1)) coop2_decode(Coop2Args a)
         if (rem > 2) step(std::integral_constant<int, 2>{}, p + 2);
     } else {
         // ----------------------------------------------------- post waves
+        if (a.post_prio) __builtin_amdgcn_s_setprio(1);
         __syncthreads();   // prologue 2
         if (STAMP) t0 = stamp();
         __syncthreads();   // period 0: nothing to post yet
@@ -623,39 +641,54 @@ int env_int(const char *name, int def)
 }
 
 // diagnostic build (LDPC_COOP2_STAMP=1): per-period cycles of each wave role
+template <int WS>
 void report_stamps(const unsigned long long *d, int grid, hipStream_t s)
 {
-    constexpr int nwaves = 2 * WS2 + 1;
+    constexpr int nwaves = 2 * WS + 1;
     std::vector<unsigned long long> h((size_t)grid * nwaves * 4);
     if (hipStreamSynchronize(s) != hipSuccess ||
         hipMemcpy(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
         return;
     // role: 0 pre, 1 chain, 2 post; work = cycles between the period's barriers
-    double work[3] = {0, 0, 0}, wmax[3] = {0, 0, 0}, total = 0;
+    double work[3] = {0, 0, 0}, wmax[3] = {0, 0, 0}, total = 0, chain_steps = 0, chain_lds = 0;
     int cnt[3] = {0, 0, 0};
+    std::vector<double> per_wave(nwaves, 0.0), per_wave_max(nwaves, 0.0);
+    std::vector<int> simd(nwaves, -1);
     for (int b = 0; b < grid; b++)
         for (int w = 0; w < nwaves; w++) {
             const unsigned long long *o = &h[((size_t)b * nwaves + w) * 4];
-            const double G = o[3] ? (double)o[3] : 1.0;
-            const int role = w < WS2 ? 0 : (w == WS2 ? 1 : 2);
+            const double G = (o[3] & 0xffffffffu) ? (double)(o[3] & 0xffffffffu) : 1.0;
+            const int role = w < WS ? 0 : (w == WS ? 1 : 2);
+            if (b == 0) simd[w] = (int)((o[3] >> 36) & 3);   // HW_ID SIMD_ID of workgroup 0's waves
             work[role] += o[0] / G;
             wmax[role] = std::max(wmax[role], o[0] / G);
+            per_wave[w] += o[0] / G / grid;
+            per_wave_max[w] = std::max(per_wave_max[w], o[0] / G);
+            if (role == 1) {
+                chain_steps += (o[1] & 0xffffffffu) / G;
+                chain_lds += (o[1] >> 32) / G;
+            }
             cnt[role]++;
             total += o[2] / G;
         }
     fprintf(stderr,
-            "coop2 stamps [cycles per period]: total %.0f | pre %.0f (max %.0f) | chain %.0f (max %.0f) | "
-            "post %.0f (max %.0f)\n",
-            total / (grid * nwaves), work[0] / cnt[0], wmax[0], work[1] / cnt[1], wmax[1], work[2] / cnt[2], wmax[2]);
+            "coop2 stamps [cycles per period]: total %.0f | pre %.0f (max %.0f) | chain %.0f (max %.0f; steps %.0f, "
+            "of which constants wait %.0f) | post %.0f (max %.0f)\n",
+            total / (grid * nwaves), work[0] / cnt[0], wmax[0], work[1] / cnt[1], wmax[1], chain_steps / cnt[1],
+            chain_lds / cnt[1], work[2] / cnt[2], wmax[2]);
+    fprintf(stderr, "coop2 stamps per wave (mean/max):");
+    for (int w = 0; w < nwaves; w++) fprintf(stderr, " %d:%.0f/%.0f@simd%d", w, per_wave[w], per_wave_max[w], simd[w]);
+    fprintf(stderr, "\n");
 }
 
+template <int WS>
 int launch_ws(const Coop2Args &a, int grid, bool stamped, hipStream_t s)
 {
-    constexpr int threads = 64 * (2 * WS2 + 1);
+    constexpr int threads = 64 * (2 * WS + 1);
     if (stamped)
-        hipLaunchKernelGGL((coop2_decode<7, WS2, true>), dim3(grid), dim3(threads), 0, s, a);
+        hipLaunchKernelGGL((coop2_decode<7, WS, true>), dim3(grid), dim3(threads), 0, s, a);
     else
-        hipLaunchKernelGGL((coop2_decode<7, WS2, false>), dim3(grid), dim3(threads), 0, s, a);
+        hipLaunchKernelGGL((coop2_decode<7, WS, false>), dim3(grid), dim3(threads), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -673,7 +706,9 @@ int coop2_upload(const ldpc_code *h, CoopCode *cc)
     *cc = CoopCode{};
     constexpr int D0 = 7, X = D0 - 2, RECW = Geo<D0>::RECW;
     if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return LDPC_OK;
-    const int S = 8 * WS2;
+    const int ws = env_int("LDPC_COOP2_WS", WS_DEFAULT);
+    if (ws != 3 && ws != 4) return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP2_WS must be 3 or 4");
+    const int S = 8 * ws;
     CoopPlan pl;
     if (coop_build_plan(h, S, R2, DIST, RECW, pl, true) != 0) return LDPC_OK;
     const int nw = (int)pl.first.size();
@@ -722,18 +757,20 @@ int launch_coop2(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.rmm = (uint32_t)(L.msg_max * 256 + 255) * 0x00010001u;
     a.coff = (uint32_t)(L.param * 256) * 0x00010001u;
     a.prio = env_int("LDPC_COOP2_PRIO", 1);
+    a.pre_prio = env_int("LDPC_COOP2_PRE_PRIO", 0);
+    a.post_prio = env_int("LDPC_COOP2_POST_PRIO", 0);
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0;
-    const int nwaves = 2 * WS2 + 1;
+    const int ws = cc.S / 8, nwaves = 2 * ws + 1;
     const bool stamped = env_int("LDPC_COOP2_STAMP", 0) != 0;
     if (stamped) {
         const size_t bytes = (size_t)grid * nwaves * 4 * sizeof(unsigned long long);
         if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
-    const int rc = launch_ws(a, grid, stamped, s);
+    const int rc = ws == 4 ? launch_ws<4>(a, grid, stamped, s) : launch_ws<3>(a, grid, stamped, s);
     if (stamped) {
-        if (rc == 0) report_stamps(a.stamps, grid, s);
+        if (rc == 0) (ws == 4 ? report_stamps<4>(a.stamps, grid, s) : report_stamps<3>(a.stamps, grid, s));
         (void)hipFree(a.stamps);
     }
     return rc;
