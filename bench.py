@@ -30,9 +30,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--code", default="dvbs2_r1_2")
-    ap.add_argument("--batch", type=int, default=4096, help="codewords per GPU")
-    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--dtype", default="i8", choices=("i8", "f32"),
+                    help="i8: configs[2] (default); f32: configs[1], float min-sum (defaults 648x324, batch 1024, 20 it)")
+    ap.add_argument("--code", default=None, help="default dvbs2_r1_2 (i8) / 648x324 (f32)")
+    ap.add_argument("--batch", type=int, default=None, help="codewords per GPU (default 4096 i8 / 1024 f32)")
+    ap.add_argument("--iters", type=int, default=None, help="default 50 (i8) / 20 (f32)")
     ap.add_argument("--ebn0", type=float, default=1.0, help="Eb/N0 (dB) of the synthetic channel")
     ap.add_argument("--kernel", type=int, default=0,
                     help="0 auto, 1 generic, 2 windowed, 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2 (packed pairs)")
@@ -40,7 +42,15 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    f32 = a.dtype == "f32"
+    if a.code is None:
+        a.code = "648x324" if f32 else "dvbs2_r1_2"
+    if a.batch is None:
+        a.batch = 1024 if f32 else 4096
+    if a.iters is None:
+        a.iters = 20 if f32 else 50
+    return a
 
 
 def hbm_peak_gbs():
@@ -76,6 +86,31 @@ def cpu_baseline(code_name, iters, budget_s, threads, seed):
                        % (code_name, iters, done, threads, el))
 
 
+def cpu_baseline_f32(code_name, iters, budget_s, seed):
+    """The reference has no float decoder (its decode(float*) is a no-op,
+    code/x86/CDecoder/template/CDecoder_fixed_SSE.cpp:35-40): time the
+    oracle's scalar float restatement (kind "port") on one core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    from ldpcgputegra_amd import channel, load_table
+    t = load_table(code_name)
+    sigma = channel.sigma_from_ebn0(1.0, t.k_info / t.n)
+    rng = np.random.default_rng(seed)
+    blk = 64
+    llr = (-1.0 + sigma * rng.standard_normal((blk, t.n))).astype(np.float32)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        O.decode_f32(t, llr, iters, O.OMS, 0.0)
+        done += blk
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return dict(value=round(done * t.n / el / 1e6, 3), unit="Mbit/s", cores=1, kind="port",
+                sample="%s %d it float min-sum (oracle restatement, scalar): %d codewords in %.2f s"
+                       % (code_name, iters, done, el))
+
+
 def main():
     a = parse()
     import numpy as np
@@ -90,23 +125,33 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
 
-    from ldpcgputegra_amd import Code, Decoder, channel, default_params
+    from ldpcgputegra_amd import ALGO_MS, Code, Decoder, channel, default_params
     from ldpcgputegra_amd.shard import reduce_results, shard_range
     code = Code(a.code)
     dec = Decoder(code, device=local, max_batch=a.batch, kernel=a.kernel)
     B, N = a.batch, code.n
     sigma = channel.sigma_from_ebn0(a.ebn0, code.k_info / code.n)
     table = channel.i8_table(sigma, 8, 31)
-    llr = torch.empty((B, N), dtype=torch.int8, device="cuda")
+    f32 = a.dtype == "f32"
     hard = torch.empty((B, N), dtype=torch.uint8, device="cuda")
     counts = torch.zeros(2, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     first_cw, _ = shard_range(rank, world, B * world)      # contiguous shard per rank
-    dec.awgn_i8_device(llr, first_cw=first_cw, seed=a.seed, table=table, stream=stream)
-    params = default_params()
+    if f32:
+        # float BPSK channel output y = -1 + sigma n of the all-zero codeword
+        # (positive LLR <-> bit 1, code/x86/CChanel/CChanelAWGN_MKL.cpp:139), used
+        # directly as the decoder input (no 2/sigma^2 scaling, as the reference)
+        g = torch.Generator(device="cuda").manual_seed(a.seed * 1000003 + first_cw)
+        llr = -1.0 + sigma * torch.randn((B, N), generator=g, device="cuda", dtype=torch.float32)
+        params = default_params(algo=ALGO_MS, beta=0.0)
+    else:
+        llr = torch.empty((B, N), dtype=torch.int8, device="cuda")
+        dec.awgn_i8_device(llr, first_cw=first_cw, seed=a.seed, table=table, stream=stream)
+        params = default_params()
+    decode = dec.decode_f32_device if f32 else dec.decode_i8_device
 
     def step():
-        dec.decode_i8_device(llr, hard, a.iters, params=params, stream=stream)
+        decode(llr, hard, a.iters, params=params, stream=stream)
         dec.count_errors_device(hard, code.k_info, counts, stream=stream)
 
     for _ in range(a.warmup):
@@ -136,7 +181,10 @@ def main():
         frames = world * B * a.steps
         value = frames * N / el / 1e6
         E = code.e
-        alg_bytes = B * (4.0 * E * a.iters + 2.0 * N)     # SURVEY.md 8(d), per launch
+        if f32:   # SURVEY.md 8(d), per launch: f32 msg rd+wr, V rd+wr per edge; f32 llr in, u8 hard out
+            alg_bytes = B * (16.0 * E * a.iters + 5.0 * N)
+        else:
+            alg_bytes = B * (4.0 * E * a.iters + 2.0 * N)
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9     # GB/s
         peak = hbm_peak_gbs()
         traffic = None
@@ -147,7 +195,8 @@ def main():
         except (OSError, ValueError):
             pass
         out = {
-            "metric": "decoded Mbit/s + BER@SNR, DVB-S2 N=64800 r=1/2, 50 iters, 1/2/4/8 MI355X",
+            "metric": ("decoded Mbit/s, configs[1]: %s float min-sum, %d iters" % (a.code, a.iters) if f32 else
+                       "decoded Mbit/s + BER@SNR, DVB-S2 N=64800 r=1/2, 50 iters, 1/2/4/8 MI355X"),
             "value": round(value, 3),
             "unit": "Mbit/s",
             "n_gpus": world,
@@ -157,11 +206,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int8",
+            "dtype": "f32" if f32 else "int8",
             "data": "synthetic (device AWGN generator, all-zero codeword, Eb/N0 %.2f dB)" % a.ebn0,
             "config": {
-                "workload": "DVB-S2 N=64800 r=1/2 layered int8 offset-min-sum (offset 1), %d iters, batch %d "
-                            "codewords per GPU" % (a.iters, B),
+                "workload": ("%s layered float min-sum, %d iters, batch %d codewords per GPU" % (a.code, a.iters, B)
+                             if f32 else
+                             "%s layered int8 offset-min-sum (offset 1), %d iters, batch %d codewords per GPU"
+                             % (a.code, a.iters, B)),
                 "code": a.code, "batch_per_gpu": B, "global_batch": B * world, "iters": a.iters,
                 "ebn0_db": a.ebn0, "kernel": dec.last_kernel,
                 "parallelism": "codeword shards x%d (no collective)" % world,
@@ -177,7 +228,8 @@ def main():
         }
         if world == 1 and a.cpu_seconds > 0:
             thr = a.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(a.code, a.iters, a.cpu_seconds, thr, a.seed)
+            out["cpu_baseline"] = (cpu_baseline_f32(a.code, a.iters, a.cpu_seconds, a.seed) if f32 else
+                                   cpu_baseline(a.code, a.iters, a.cpu_seconds, thr, a.seed))
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -132,6 +132,11 @@ int ldpc_code_coop_plan(const ldpc_code *h, int S, int R, int *first, int *count
  * apart; reads written dist+1 .. R+dist windows earlier are forwarded). */
 int ldpc_code_coop_plan_dist(const ldpc_code *h, int S, int R, int dist, int *first, int *count, int max_windows,
                              int *n_windows, int *tail, int *n_fwd);
+/* Layer plan of the LDS-resident kernel (kernel 7): maximal runs of
+ * consecutive same-group checks sharing no variable (one block row of a
+ * quasi-cyclic code).  lds_i8 / lds_f32: 1 if a codeword's state fits the
+ * kernel's LDS budget for that element type. */
+int ldpc_code_layer_info(const ldpc_code *h, int *n_layers, int *max_width, int *lds_i8, int *lds_f32);
 void ldpc_code_destroy(ldpc_code *h);
 
 /* ---- decoder context --------------------------------------------------- */
@@ -141,11 +146,12 @@ int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
 /* Select kernel family: 0 = auto, 1 = generic (per-edge messages),
  * 2 = windowed layered kernel (compressed messages), 3 / 4 = windowed2
  * (S = 16 / 32), 5 = workgroup-cooperative DVB-S2 kernel, 6 = its packed-pair
- * variant (two codewords per lane; first-group degree 7, no early termination). */
+ * variant (two codewords per lane; first-group degree 7, no early termination),
+ * 7 = LDS-resident short-code kernel (whole state in LDS; int8 and float). */
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel family the last decode actually ran (1 generic, 2 windowed,
- * 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2; 0 before the first decode). */
+ * 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2, 7 lds; 0 before the first decode). */
 int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel timing (bench / profiling): when enabled, every decode records HIP
  * events around the decode kernel on the stream it is launched on;

@@ -45,6 +45,7 @@ SIGNATURES = {
     "ldpc_code_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "ldpc_code_edges": (I, [P, P, P, P]),
     "ldpc_code_plan_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "ldpc_code_layer_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "ldpc_code_window_plan": (I, [P, I, I, P, P, I, C.POINTER(I)]),
     "ldpc_code_coop_plan": (I, [P, I, I, P, P, I, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "ldpc_code_coop_plan_dist": (I, [P, I, I, I, P, P, I, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),

@@ -31,6 +31,7 @@ ALIASES = {
     "64800x21600": "dvbs2_r2_3",
     "64800x7200": "dvbs2_r8_9",
     "64800x6480": "dvbs2_r9_10",
+    "80211n_648": "648x324",
 }
 
 
@@ -181,6 +182,12 @@ class Code:
         s, w, hz = C.c_int(), C.c_int(), C.c_int()
         _lib.check(_lib.lib().ldpc_code_plan_info(self._h, C.byref(s), C.byref(w), C.byref(hz)))
         return dict(staircase=bool(s.value), n_windows=w.value, min_hazard=hz.value, windowed=w.value > 0)
+
+    def layer_info(self):
+        """Layer plan of the LDS-resident kernel (kernel 7)."""
+        nl, w, i8, f32 = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        _lib.check(_lib.lib().ldpc_code_layer_info(self._h, C.byref(nl), C.byref(w), C.byref(i8), C.byref(f32)))
+        return dict(n_layers=nl.value, max_width=w.value, lds_i8=bool(i8.value), lds_f32=bool(f32.value))
 
     def encode(self, info):
         """DVB-S2 IRA encoding of info bits [batch, K] -> codewords [batch, N]."""

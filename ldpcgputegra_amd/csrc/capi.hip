@@ -17,6 +17,7 @@
 #include "ldpc_internal.h"
 #include "windowed.h"
 #include "coop.h"
+#include "lds.h"
 
 #define HIP_TRY(expr)                                                                          \
     do {                                                                                       \
@@ -30,7 +31,7 @@ struct ldpc_ctx {
     int device = 0;
     int max_batch = 0;
     int max_stride = 0;
-    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop, 6 coop2
+    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop, 6 coop2, 7 lds
     int last_kernel = 0;
     hipStream_t stream = nullptr;
     // device copy of the code
@@ -40,6 +41,7 @@ struct ldpc_ctx {
     Windowed2Code w16{}, w32{};     // windowed2.hip tables, S = 16 and S = 32
     CoopCode coop{};                // coop.hip tables (workgroup-cooperative DVB-S2 path)
     CoopCode coop2{};               // coop2.hip tables (packed-pair variant, D0 = 7)
+    LdsCode lds{};                  // lds.hip tables (LDS-resident short-code decoder)
     // scratch (lazily sized)
     void *d_V = nullptr;
     size_t V_bytes = 0;
@@ -116,6 +118,7 @@ extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ld
     if ((rc = windowed2_upload(h, 32, 1, &c->w32)) != LDPC_OK) return fail(rc);
     if ((rc = coop_upload(h, &c->coop)) != LDPC_OK) return fail(rc);
     if ((rc = coop2_upload(h, &c->coop2)) != LDPC_OK) return fail(rc);
+    if ((rc = lds_upload(h, &c->lds)) != LDPC_OK) return fail(rc);
     *out = c;
     return LDPC_OK;
 }
@@ -130,6 +133,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     windowed2_free(&c->w32);
     coop_free(&c->coop);
     coop_free(&c->coop2);
+    lds_free(&c->lds);
     for (auto &pr : c->events) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -154,9 +158,9 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 6) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 6");
+    if (!c || k < 0 || k > 7) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 7");
     if ((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid) ||
-        (k == 5 && !c->coop.valid) || (k == 6 && !c->coop2.valid))
+        (k == 5 && !c->coop.valid) || (k == 6 && !c->coop2.valid) || (k == 7 && !c->lds.valid))
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
     c->kernel = k;
     return LDPC_OK;
@@ -227,10 +231,13 @@ static int check_params(const ldpc_ctx *c, int batch, int n_iter, const ldpc_par
 }
 
 // kernel family for this call: 1 generic, 2 windowed, 3 windowed2/S16,
-// 4 windowed2/S32, 5 coop (workgroup-cooperative), 6 coop2 (packed pairs)
+// 4 windowed2/S32, 5 coop (workgroup-cooperative), 6 coop2 (packed pairs),
+// 7 lds (LDS-resident short codes, int8 and float)
 static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, int stride)
 {
-    if (is_float) return 1;
+    const bool ld = lds_applicable(c->code, c->lds, is_float);
+    if (c->kernel == 7) return ld ? 7 : -1;
+    if (is_float) return (c->kernel == 0 && lds_preferred(c->code, c->lds, true)) ? 7 : (c->kernel <= 1 ? 1 : -1);
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
     const bool w2 = windowed2_params_ok(p);
     const bool co = c->coop.valid && coop_params_ok(p);
@@ -246,6 +253,7 @@ static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, i
         if (co2) return 6;
         if (co) return 5;
         if (w2 && c->w16.valid) return 3;
+        if (lds_preferred(c->code, c->lds, false)) return 7;
         if (w1) return 2;
         return 1;
     }
@@ -265,8 +273,34 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     const int kern = pick_kernel(c, p, is_float, stride);
     if (kern < 0)
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d selected but not applicable to these params", c->kernel);
-    const bool win = kern >= 2;
     c->last_kernel = kern;
+    if (kern == 7) {   // LDS-resident: frame-major in and out, no scratch, no transposes
+        DecodeLaunch L{};
+        L.batch = batch;
+        L.iters = n_iter;
+        L.is_float = is_float;
+        L.algo = (p->algo == LDPC_ALGO_MS) ? LDPC_ALGO_OMS : p->algo;
+        L.param = (p->algo == LDPC_ALGO_NMS) ? p->factor : (p->algo == LDPC_ALGO_MS ? 0 : p->offset);
+        L.var_min = p->var_min;
+        L.msg_max = p->msg_max;
+        L.early = p->early_term;
+        L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
+        L.iters_used = d_iters;
+        hipEvent_t ev0 = nullptr, ev1 = nullptr;
+        if (c->profile) {
+            HIP_TRY(hipEventCreate(&ev0));
+            HIP_TRY(hipEventCreate(&ev1));
+            HIP_TRY(hipEventRecord(ev0, s));
+        }
+        const int lr = launch_lds(c->lds, h, d_llr, d_hard, d_soft, batch, n_iter, L, s);
+        if (c->profile) {
+            HIP_TRY(hipEventRecord(ev1, s));
+            c->events.emplace_back(ev0, ev1);
+        }
+        if (lr) return ldpc_set_error(LDPC_EDEVICE, "lds decode launch: %s", hipGetErrorString(hipGetLastError()));
+        return LDPC_OK;
+    }
+    const bool win = kern >= 2;
     // + a sink row / sink words for the masked stores of the coop kernel
     const size_t msg_need = (kern == 6 ? coop2_msg_bytes(h, stride)
                              : win    ? windowed_msg_bytes(h, stride)

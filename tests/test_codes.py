@@ -42,6 +42,56 @@ def test_dvbs2_structure():
     assert info["min_hazard"] >= 60          # measured: 62 (SURVEY / plan.cpp)
 
 
+def gf2_rank(h):
+    h = h.copy()
+    r = 0
+    for c in range(h.shape[1]):
+        piv = np.nonzero(h[r:, c])[0]
+        if piv.size == 0:
+            continue
+        p = r + piv[0]
+        h[[r, p]] = h[[p, r]]
+        rows = np.nonzero(h[:, c])[0]
+        rows = rows[rows != r]
+        h[rows] ^= h[r]
+        r += 1
+        if r == h.shape[0]:
+            break
+    return r
+
+
+def test_80211n_648_structure():
+    """The 802.11n N=648 R=1/2 table (tools/make_qc_codes.py, entered from
+    the standard; absent from the reference): degrees, full rank, the
+    dual-diagonal parity part, and a systematic encoder that satisfies H."""
+    t = load_table("80211n_648")
+    assert (t.n, t.m, t.e) == (648, 324, 2376)
+    assert t.groups == [(8, 108), (7, 216)]
+    H = np.zeros((t.m, t.n), dtype=np.uint8)
+    for i, (_, vs) in enumerate(t.checks()):
+        H[i, vs] = 1
+    assert H.sum() == t.e                          # no repeated edge
+    assert gf2_rank(H) == t.m
+    colw = H.sum(axis=0)
+    assert colw.min() >= 2 and colw[t.n - t.m:].max() <= 3   # parity columns: weight 3 (first), 2 (diagonal)
+    # systematic encoding by elimination on the parity part: H = [A | B], B p = A u
+    A, B = H[:, : t.n - t.m], H[:, t.n - t.m:]
+    assert gf2_rank(B) == t.m
+    rng = np.random.default_rng(5)
+    u = rng.integers(0, 2, t.n - t.m, dtype=np.uint8)
+    aug = np.concatenate([B, (A.astype(np.int64) @ u % 2).astype(np.uint8)[:, None]], axis=1)
+    # Gauss-Jordan on [B | A u]
+    r = 0
+    for c in range(t.m):
+        p = r + np.nonzero(aug[r:, c])[0][0]
+        aug[[r, p]] = aug[[p, r]]
+        rows = np.nonzero(aug[:, c])[0]
+        aug[rows[rows != r]] ^= aug[r]
+        r += 1
+    cw = np.concatenate([u, aug[:, -1]])
+    assert not (H.astype(np.int64) @ cw % 2).any()
+
+
 def test_generic_codes_have_no_staircase():
     assert not Code("576x288").plan_info()["staircase"]
 

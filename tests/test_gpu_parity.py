@@ -30,7 +30,8 @@ def decoder(code, kernel=0, max_batch=4096):
 def kernels_for(code):
     """Kernel families that can run this code: 1 generic, 2 windowed,
     3 windowed2 (S=16), 4 windowed2 (S=32), 5 coop (workgroup-cooperative),
-    6 coop2 (its packed-pair variant, first-group degree 7)."""
+    6 coop2 (its packed-pair variant, first-group degree 7), 7 lds (LDS-resident
+    short codes)."""
     ks = [1]
     c = Code(code)
     if c.plan_info()["windowed"]:
@@ -41,6 +42,8 @@ def kernels_for(code):
         ks.append(5)
     if c.coop_plan(24, 3) is not None and c.max_deg == 7:
         ks.append(6)
+    if c.layer_info()["lds_i8"]:
+        ks.append(7)
     return ks
 
 
@@ -70,7 +73,7 @@ def _torch():
     return torch
 
 
-@pytest.mark.parametrize("code", ["576x288", "1944x972", "2048x384", "1024x518", "1200x600", "200x100",
+@pytest.mark.parametrize("code", ["576x288", "648x324", "1944x972", "2048x384", "1024x518", "1200x600", "200x100",
                                   "dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r9_10", "16200x7560"])
 @pytest.mark.parametrize("batch", [1, 37, 64])
 def test_soft_output_bit_exact_vs_oracle(code, batch):
@@ -99,11 +102,12 @@ def test_algorithms_vs_oracle(algo, param):
     o_param = param if algo != ALGO_MS else 0
     exp = O.decode_i8(t, llr, 12, o_algo, o_param)
     p = default_params(algo=algo, offset=param, factor=param)
-    got = decoder("1944x972", 1, 64).decode_i8(llr, 12, p)
-    assert np.array_equal(got, exp)
+    for k in (1, 7):
+        got = decoder("1944x972", k, 64).decode_i8(llr, 12, p)
+        assert np.array_equal(got, exp), "kernel %d" % k
 
 
-@pytest.mark.parametrize("code", ["576x288", "dvbs2_r1_2"])
+@pytest.mark.parametrize("code", ["576x288", "648x324", "dvbs2_r1_2"])
 def test_early_termination_vs_oracle(code):
     torch = _torch()
     t = load_table(code)
@@ -126,27 +130,30 @@ def test_early_termination_vs_oracle(code):
         assert np.array_equal(d_soft.cpu().numpy(), ref_soft), "kernel %d" % k
 
 
-@pytest.mark.parametrize("code,algo,beta", [("1944x972", ALGO_MS, 0.0), ("576x288", ALGO_OMS, 0.15),
-                                            ("576x288", ALGO_NMS, 0.75), ("dvbs2_r1_2", ALGO_MS, 0.0)])
-def test_float_decoder_vs_oracle(code, algo, beta):
+@pytest.mark.parametrize("code,algo,beta,batch", [("1944x972", ALGO_MS, 0.0, 33), ("576x288", ALGO_OMS, 0.15, 33),
+                                                  ("576x288", ALGO_NMS, 0.75, 33), ("dvbs2_r1_2", ALGO_MS, 0.0, 33),
+                                                  ("648x324", ALGO_MS, 0.0, 1024)])
+def test_float_decoder_vs_oracle(code, algo, beta, batch):
+    """648x324 at batch 1024 / 20 it / float min-sum is BASELINE.json configs[1]."""
     torch = _torch()
     t = load_table(code)
     rng = np.random.default_rng(5)
-    batch = 33
     sigma = channel.sigma_from_ebn0(1.2, t.k_info / t.n)
     llr = (-1.0 + sigma * rng.standard_normal((batch, t.n))).astype(np.float32)
     iters = 5 if t.n > 10000 else 20
     o_algo = O.NMS if algo == ALGO_NMS else O.OMS
     ref_hard, ref_soft, _ = O.decode_f32(t, llr, iters, o_algo, beta)
-    dec = decoder(code, 0, 64)
-    d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
-    d_soft = torch.empty((batch, t.n), dtype=torch.float32, device="cuda")
-    dec.decode_f32_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=default_params(algo=algo, beta=beta),
-                          soft=d_soft)
-    torch.cuda.synchronize()
-    soft = d_soft.cpu().numpy()
-    assert np.max(np.abs(soft - ref_soft)) <= FLOAT_TOL
-    assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
+    ks = [1] + ([7] if Code(code).layer_info()["lds_f32"] else [])
+    for k in ks:
+        dec = decoder(code, k, max(64, batch))
+        d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+        d_soft = torch.empty((batch, t.n), dtype=torch.float32, device="cuda")
+        dec.decode_f32_device(torch.from_numpy(llr).cuda(), d_hard, iters,
+                              params=default_params(algo=algo, beta=beta), soft=d_soft)
+        torch.cuda.synchronize()
+        soft = d_soft.cpu().numpy()
+        assert np.max(np.abs(soft - ref_soft)) <= FLOAT_TOL, "kernel %d" % k
+        assert np.array_equal(d_hard.cpu().numpy(), ref_hard), "kernel %d" % k
 
 
 def test_device_channel_matches_host_generator():
