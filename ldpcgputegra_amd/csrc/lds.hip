@@ -110,11 +110,119 @@ LDPC_DEV void lds_check_f32(float *V, float *msg, const uint16_t *tab, int cnt, 
     }
 }
 
+// Two lanes per check (SPLIT): lane half h takes edges h, h + 2, ...; the
+// partial (min1, min2, sign) of the two halves are exchanged with one DPP
+// swap of neighbouring lanes and merged: min1 = min(a1, b1), min2 =
+// min(a2, b2, max(a1, b1)) is exactly the smallest / second smallest of the
+// whole multiset, so the messages are those of the serial loop above.
+LDPC_DEV int swap_pair(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }   // quad_perm [1,0,3,2]
+LDPC_DEV float swap_pair(float x) { return __int_as_float(swap_pair(__float_as_int(x))); }
+
+template <int D>
+LDPC_DEV void lds_check_i8_split(int8_t *V, int8_t *msg, const uint16_t *tab, int cnt, bool later, int h,
+                                 const LdsArgs &a)
+{
+    constexpr int DH = (D + 1) / 2;
+    int c[DH], av[DH], idx[DH];
+    int sign = 0, min1 = 127, min2 = 127;
+#pragma unroll
+    for (int k = 0; k < DH; k++) {
+        const int j = 2 * k + h;
+        const bool ok = (D % 2 == 0) || k < DH - 1 || h == 0;
+        idx[k] = ok ? tab[j * cnt] : 0;
+        const int cj = ok ? max(sat8((int)V[idx[k]] - (int)msg[j * cnt]), a.var_min) : 0;
+        const int aj = ok ? (later ? abs8(min(cj, a.msg_max)) : min(abs8(cj), a.msg_max)) : 127;
+        sign ^= cj & 0x80;
+        c[k] = cj;
+        av[k] = aj;
+        const int t = min1;
+        min1 = min(aj, min1);
+        min2 = min(min2, max(aj, t));
+    }
+    const int p1 = swap_pair(min1), p2 = swap_pair(min2), ps = swap_pair(sign);
+    min2 = min(min(min2, p2), max(min1, p1));
+    min1 = min(min1, p1);
+    sign ^= ps;
+    int cst1, cst2;
+    check_constants(a.algo, a.param, a.msg_max, min1, min2, cst1, cst2);
+    sign ^= (D & 1) ? 0xC0 : 0x40;
+#pragma unroll
+    for (int k = 0; k < DH; k++) {
+        const int j = 2 * k + h;
+        const bool ok = (D % 2 == 0) || k < DH - 1 || h == 0;
+        const int r = (av[k] == min1) ? cst1 : cst2;
+        const int sig = as_i8(sign ^ (c[k] & 0x80));
+        const int m = sig < 0 ? as_i8(-r) : r;
+        if (ok) {
+            msg[j * cnt] = (int8_t)m;
+            V[idx[k]] = (int8_t)max(sat8(c[k] + m), a.var_min);
+        }
+    }
+}
+
+template <int D>
+LDPC_DEV void lds_check_f32_split(float *V, float *msg, const uint16_t *tab, int cnt, int h, const LdsArgs &a)
+{
+    constexpr int DH = (D + 1) / 2;
+    float c[DH], av[DH];
+    int idx[DH];
+    int sign = 0;
+    float min1 = __builtin_huge_valf(), min2 = __builtin_huge_valf();
+#pragma unroll
+    for (int k = 0; k < DH; k++) {
+        const int j = 2 * k + h;
+        const bool ok = (D % 2 == 0) || k < DH - 1 || h == 0;
+        idx[k] = ok ? tab[j * cnt] : 0;
+        const float cj = ok ? V[idx[k]] - msg[j * cnt] : 0.0f;
+        const float aj = ok ? fabsf(cj) : __builtin_huge_valf();
+        sign ^= (cj < 0.0f);
+        c[k] = cj;
+        av[k] = aj;
+        const float t = min1;
+        min1 = fminf(aj, min1);
+        min2 = fminf(min2, fmaxf(aj, t));
+    }
+    const float p1 = swap_pair(min1), p2 = swap_pair(min2);
+    const int ps = swap_pair(sign);
+    min2 = fminf(fminf(min2, p2), fmaxf(min1, p1));
+    min1 = fminf(min1, p1);
+    sign ^= ps ^ (D & 1);
+    float cst1, cst2;
+    if (a.algo == 1) {
+        cst1 = min2 * a.beta;
+        cst2 = min1 * a.beta;
+    } else {
+        cst1 = fmaxf(min2 - a.beta, 0.0f);
+        cst2 = fmaxf(min1 - a.beta, 0.0f);
+    }
+#pragma unroll
+    for (int k = 0; k < DH; k++) {
+        const int j = 2 * k + h;
+        const bool ok = (D % 2 == 0) || k < DH - 1 || h == 0;
+        const float r = (av[k] == min1) ? cst1 : cst2;
+        const float m = (sign ^ (c[k] < 0.0f)) ? -r : r;
+        if (ok) {
+            msg[j * cnt] = m;
+            V[idx[k]] = c[k] + m;
+        }
+    }
+}
+
 // the checks li, li + LPC, ... of one layer (lane li of its codeword)
-template <typename T, int D>
+template <typename T, int D, bool SPLIT>
 LDPC_DEV void lds_layer(T *V, T *msg, const uint16_t *tab, int base, int cnt, bool later, int li, int lpc,
                         const LdsArgs &a)
 {
+    if constexpr (SPLIT) {   // lanes 2i, 2i+1: check i (the pair stays together through the loop)
+        const int h = li & 1;
+        for (int i = li >> 1; i < cnt; i += lpc >> 1) {
+            if constexpr (sizeof(T) == 1)
+                lds_check_i8_split<D>((int8_t *)V, (int8_t *)msg + base + i, tab + base + i, cnt, later, h, a);
+            else
+                lds_check_f32_split<D>((float *)V, (float *)msg + base + i, tab + base + i, cnt, h, a);
+        }
+        return;
+    }
     for (int i = li; i < cnt; i += lpc) {
         if constexpr (sizeof(T) == 1)
             lds_check_i8<D>((int8_t *)V, (int8_t *)msg + base + i, tab + base + i, cnt, later, a);
@@ -127,7 +235,7 @@ LDPC_DEV void lds_layer(T *V, T *msg, const uint16_t *tab, int base, int cnt, bo
     X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) \
     X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
 
-template <typename T>
+template <typename T, bool SPLIT>
 __global__ void __launch_bounds__(64) lds_decode(LdsArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -178,7 +286,7 @@ __global__ void __launch_bounds__(64) lds_decode(LdsArgs a)
             if (live) {
                 switch (L.z) {
 #define X(DD) \
-    case DD: lds_layer<T, DD>(V, msg, tab, L.x, L.y, L.w != 0 && a.algo != 1, li, lpc, a); break;
+    case DD: lds_layer<T, DD, SPLIT>(V, msg, tab, L.x, L.y, L.w != 0 && a.algo != 1, li, lpc, a); break;
                     LDPC_LDS_DEG_CASES(X)
 #undef X
                 default: break;
@@ -239,6 +347,8 @@ static void lds_plan(const ldpc_code *h, std::vector<int4> &layers, int &maxw)
         i = j;
     }
 }
+
+constexpr int kLdsSimds = 256 * 4;   // MI355X: 256 CUs x 4 SIMDs
 
 static int lpc_log2_of(int maxw) { return maxw <= 8 ? 3 : maxw <= 16 ? 4 : maxw <= 32 ? 5 : 6; }
 
@@ -331,7 +441,14 @@ int launch_lds(const LdsCode &lc, const ldpc_code *h, const void *llr, uint8_t *
     a.e = h->e;
     a.batch = batch;
     a.iters = iters;
-    a.lpc_log2 = lc.lpc_log2;
+    // lanes per codeword: at least the widest layer; more (down to one
+    // codeword per wave, two lanes per check) while that still leaves two
+    // waves per SIMD of the 256-CU chip -- the kernel is latency-bound, so
+    // small batches go faster spread over more waves
+    int lg = lc.lpc_log2;
+    while (lg < 6 && (batch << lg) / 64 < 2 * kLdsSimds) lg++;
+    const bool split = (1 << lg) >= 2 * lc.max_width;
+    a.lpc_log2 = lg;
     a.algo = L.algo;
     a.param = L.param;
     a.var_min = L.var_min;
@@ -340,12 +457,12 @@ int launch_lds(const LdsCode &lc, const ldpc_code *h, const void *llr, uint8_t *
     a.beta = L.beta;
     a.iters_used = L.iters_used;
     a.tab_bytes = lc.tab_bytes;
-    const int cpw = 64 >> lc.lpc_log2;
-    const size_t shm = lds_bytes(h, lc, L.is_float);
+    const int cpw = 64 >> lg;
+    const size_t shm = lds_bytes_of(h, lg, L.is_float ? 4 : 1);
     dim3 grid((batch + cpw - 1) / cpw), block(64);
     if (L.is_float)
-        hipLaunchKernelGGL(lds_decode<float>, grid, block, shm, s, a);
+        hipLaunchKernelGGL((split ? lds_decode<float, true> : lds_decode<float, false>), grid, block, shm, s, a);
     else
-        hipLaunchKernelGGL(lds_decode<int8_t>, grid, block, shm, s, a);
+        hipLaunchKernelGGL((split ? lds_decode<int8_t, true> : lds_decode<int8_t, false>), grid, block, shm, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

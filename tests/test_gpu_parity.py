@@ -94,6 +94,33 @@ def test_soft_output_bit_exact_vs_oracle(code, batch):
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard), "kernel %d" % k
 
 
+@pytest.mark.parametrize("code,batch,is_float", [("816x408", 4096, False), ("648x324", 4096, True),
+                                                 ("648x324", 3000, False), ("200x100", 9000, True)])
+def test_lds_kernel_large_batches(code, batch, is_float):
+    """Kernel 7 packs several codewords per wave at large batches (with and
+    without two lanes per check): bit-exact soft output vs the oracle."""
+    torch = _torch()
+    t = load_table(code)
+    iters = 8
+    dec = decoder(code, 7, batch)
+    if is_float:
+        rng = np.random.default_rng(11)
+        sigma = channel.sigma_from_ebn0(1.5, t.k_info / t.n)
+        llr = (-1.0 + sigma * rng.standard_normal((batch, t.n))).astype(np.float32)
+        _, ref_soft, _ = O.decode_f32(t, llr, iters, O.OMS, 0.0)
+        d_soft = torch.empty((batch, t.n), dtype=torch.float32, device="cuda")
+        dec.decode_f32_device(torch.from_numpy(llr).cuda(), None, iters, params=default_params(algo=ALGO_MS),
+                              soft=d_soft)
+    else:
+        llr = channel.awgn_i8_host(t.n, batch, seed=9, table=channel.i8_table(0.8))
+        _, ref_soft, _ = O.decode_i8(t, llr, iters, O.OMS, 1, return_soft=True)
+        d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
+        dec.decode_i8_device(torch.from_numpy(llr).cuda(), None, iters, soft=d_soft)
+    torch.cuda.synchronize()
+    assert dec.last_kernel == "lds"
+    assert np.array_equal(d_soft.cpu().numpy(), ref_soft)
+
+
 @pytest.mark.parametrize("algo,param", [(ALGO_OMS, 0), (ALGO_OMS, 3), (ALGO_NMS, 24), (ALGO_MS, 0)])
 def test_algorithms_vs_oracle(algo, param):
     t = load_table("1944x972")
