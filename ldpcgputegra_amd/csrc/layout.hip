@@ -78,24 +78,26 @@ __global__ void __launch_bounds__(256) awgn_i8_k(int8_t *__restrict__ llr, int n
     }
 }
 
-__global__ void __launch_bounds__(256) count_errors_k(const uint8_t *__restrict__ hard, int n, int k,
-                                                      const uint8_t *__restrict__ ref,
-                                                      unsigned long long *counts)
+// one wave per codeword: hard decisions are 0/1 bytes, so the errors of a
+// dword are popcount((h ^ r) & 0x01010101); dword loads when the row allows
+__global__ void __launch_bounds__(64) count_errors_k(const uint8_t *__restrict__ hard, int n, int k,
+                                                     const uint8_t *__restrict__ ref,
+                                                     unsigned long long *counts)
 {
     const int b = blockIdx.x;
     const uint8_t *h = hard + (size_t)b * n;
     const uint8_t *r = ref ? ref + (size_t)b * n : nullptr;
     int errs = 0;
-    for (int i = threadIdx.x; i < k; i += 256) errs += (h[i] != (r ? r[i] : 0));
-    __shared__ int red[256];
-    red[threadIdx.x] = errs;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
+    if ((n & 3) == 0 && (k & 3) == 0) {
+        const uint32_t *h4 = (const uint32_t *)h, *r4 = (const uint32_t *)r;
+        for (int i = threadIdx.x; i < k / 4; i += 64)
+            errs += __builtin_popcount((h4[i] ^ (r4 ? r4[i] : 0u)) & 0x01010101u);
+    } else {
+        for (int i = threadIdx.x; i < k; i += 64) errs += (h[i] != (r ? r[i] : 0));
     }
-    if (threadIdx.x == 0 && red[0]) {
-        atomicAdd(&counts[0], (unsigned long long)red[0]);
+    for (int off = 32; off > 0; off >>= 1) errs += __shfl_xor(errs, off);
+    if (threadIdx.x == 0 && errs) {
+        atomicAdd(&counts[0], (unsigned long long)errs);
         atomicAdd(&counts[1], 1ull);
     }
 }
@@ -173,6 +175,6 @@ int launch_count_errors(const uint8_t *hard, int n, int batch, int k, const uint
                         unsigned long long *counts, hipStream_t s)
 {
     if (batch <= 0) return 0;
-    hipLaunchKernelGGL(count_errors_k, dim3(batch), dim3(256), 0, s, hard, n, k, ref, counts);
+    hipLaunchKernelGGL(count_errors_k, dim3(batch), dim3(64), 0, s, hard, n, k, ref, counts);
     return ok();
 }

@@ -206,6 +206,19 @@ def test_error_counter():
     dec.count_errors_device(torch.from_numpy(hard).cuda(), 288, counts)
     torch.cuda.synchronize()
     assert counts.cpu().tolist() == [3, 2]
+    # against a reference codeword, dword path (n, k multiples of 4) and byte path
+    rng = np.random.default_rng(4)
+    for code, n, k in (("576x288", 576, 288), ("9972x4986", 9972, 4986)):   # k % 4 == 2: byte path
+        dec = decoder(code, 1, 64)                 # the row length is the context's code length
+        ref = rng.integers(0, 2, (6, n), dtype=np.uint8)
+        hard = ref.copy()
+        hard[0, :k] ^= 1                       # k errors
+        hard[2, k - 1] ^= 1
+        hard[5, k:] ^= 1                       # beyond k: not counted
+        counts.zero_()
+        dec.count_errors_device(torch.from_numpy(hard).cuda(), k, counts, ref=torch.from_numpy(ref).cuda())
+        torch.cuda.synchronize()
+        assert counts.cpu().tolist() == [k + 1, 2]
 
 
 def test_dvbs2_full_batch_properties():
