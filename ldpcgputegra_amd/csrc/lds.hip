@@ -44,8 +44,8 @@ struct LdsArgs {
     int tab_bytes;            // LDS bytes of the table, 16-B aligned
 };
 
-template <int D>
-LDPC_DEV void lds_check_i8(int8_t *V, int8_t *msg, const uint16_t *tab, int cnt, bool later, const LdsArgs &a)
+template <int D, bool LATER>
+LDPC_DEV void lds_check_i8(int8_t *V, int8_t *msg, const uint16_t *tab, int cnt, const LdsArgs &a)
 {
     int c[D], av[D], idx[D];
     int sign = 0, min1 = 127, min2 = 127;
@@ -53,7 +53,7 @@ LDPC_DEV void lds_check_i8(int8_t *V, int8_t *msg, const uint16_t *tab, int cnt,
     for (int j = 0; j < D; j++) {
         idx[j] = tab[j * cnt];
         const int cj = max(sat8((int)V[idx[j]] - (int)msg[j * cnt]), a.var_min);
-        const int aj = later ? abs8(min(cj, a.msg_max)) : min(abs8(cj), a.msg_max);
+        const int aj = LATER ? abs8(min(cj, a.msg_max)) : min(abs8(cj), a.msg_max);
         sign ^= cj & 0x80;
         c[j] = cj;
         av[j] = aj;
@@ -118,9 +118,8 @@ LDPC_DEV void lds_check_f32(float *V, float *msg, const uint16_t *tab, int cnt, 
 LDPC_DEV int swap_pair(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }   // quad_perm [1,0,3,2]
 LDPC_DEV float swap_pair(float x) { return __int_as_float(swap_pair(__float_as_int(x))); }
 
-template <int D>
-LDPC_DEV void lds_check_i8_split(int8_t *V, int8_t *msg, const uint16_t *tab, int cnt, bool later, int h,
-                                 const LdsArgs &a)
+template <int D, bool LATER>
+LDPC_DEV void lds_check_i8_split(int8_t *V, int8_t *msg, const uint16_t *tab, int cnt, int h, const LdsArgs &a)
 {
     constexpr int DH = (D + 1) / 2;
     int c[DH], av[DH], idx[DH];
@@ -131,7 +130,7 @@ LDPC_DEV void lds_check_i8_split(int8_t *V, int8_t *msg, const uint16_t *tab, in
         const bool ok = (D % 2 == 0) || k < DH - 1 || h == 0;
         idx[k] = ok ? tab[j * cnt] : 0;
         const int cj = ok ? max(sat8((int)V[idx[k]] - (int)msg[j * cnt]), a.var_min) : 0;
-        const int aj = ok ? (later ? abs8(min(cj, a.msg_max)) : min(abs8(cj), a.msg_max)) : 127;
+        const int aj = ok ? (LATER ? abs8(min(cj, a.msg_max)) : min(abs8(cj), a.msg_max)) : 127;
         sign ^= cj & 0x80;
         c[k] = cj;
         av[k] = aj;
@@ -209,15 +208,16 @@ LDPC_DEV void lds_check_f32_split(float *V, float *msg, const uint16_t *tab, int
 }
 
 // the checks li, li + LPC, ... of one layer (lane li of its codeword)
-template <typename T, int D, bool SPLIT>
-LDPC_DEV void lds_layer(T *V, T *msg, const uint16_t *tab, int base, int cnt, bool later, int li, int lpc,
-                        const LdsArgs &a)
+// LATER (int8 only): the later-degree-group rule of a2, a template
+// parameter so that the edge loop is straight-line and its LDS loads batch
+template <typename T, int D, bool SPLIT, bool LATER>
+LDPC_DEV void lds_layer(T *V, T *msg, const uint16_t *tab, int base, int cnt, int li, int lpc, const LdsArgs &a)
 {
     if constexpr (SPLIT) {   // lanes 2i, 2i+1: check i (the pair stays together through the loop)
         const int h = li & 1;
         for (int i = li >> 1; i < cnt; i += lpc >> 1) {
             if constexpr (sizeof(T) == 1)
-                lds_check_i8_split<D>((int8_t *)V, (int8_t *)msg + base + i, tab + base + i, cnt, later, h, a);
+                lds_check_i8_split<D, LATER>((int8_t *)V, (int8_t *)msg + base + i, tab + base + i, cnt, h, a);
             else
                 lds_check_f32_split<D>((float *)V, (float *)msg + base + i, tab + base + i, cnt, h, a);
         }
@@ -225,7 +225,7 @@ LDPC_DEV void lds_layer(T *V, T *msg, const uint16_t *tab, int base, int cnt, bo
     }
     for (int i = li; i < cnt; i += lpc) {
         if constexpr (sizeof(T) == 1)
-            lds_check_i8<D>((int8_t *)V, (int8_t *)msg + base + i, tab + base + i, cnt, later, a);
+            lds_check_i8<D, LATER>((int8_t *)V, (int8_t *)msg + base + i, tab + base + i, cnt, a);
         else
             lds_check_f32<D>((float *)V, (float *)msg + base + i, tab + base + i, cnt, a);
     }
@@ -286,7 +286,12 @@ __global__ void __launch_bounds__(64) lds_decode(LdsArgs a)
             if (live) {
                 switch (L.z) {
 #define X(DD) \
-    case DD: lds_layer<T, DD, SPLIT>(V, msg, tab, L.x, L.y, L.w != 0 && a.algo != 1, li, lpc, a); break;
+    case DD:                                                                                  \
+        if (sizeof(T) == 1 && L.w != 0 && a.algo != 1)                                        \
+            lds_layer<T, DD, SPLIT, sizeof(T) == 1>(V, msg, tab, L.x, L.y, li, lpc, a);       \
+        else                                                                                  \
+            lds_layer<T, DD, SPLIT, false>(V, msg, tab, L.x, L.y, li, lpc, a);                \
+        break;
                     LDPC_LDS_DEG_CASES(X)
 #undef X
                 default: break;
