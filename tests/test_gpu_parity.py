@@ -94,6 +94,28 @@ def test_soft_output_bit_exact_vs_oracle(code, batch):
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard), "kernel %d" % k
 
 
+def test_config1_single_codeword_float_sweep():
+    """BASELINE.json configs[0] shape on the GPU path: 802.11n N=648 r1/2, one
+    codeword, 10 iterations, float min-sum, Eb/N0 0.5 .. 3.0 dB (SURVEY.md
+    8(d) "Config 1"), every point equal to the oracle's float decode."""
+    torch = _torch()
+    t = load_table("648x324")
+    rng = np.random.default_rng(21)
+    for ebn0 in (0.5, 1.0, 1.5, 2.0, 2.5, 3.0):
+        sigma = channel.sigma_from_ebn0(ebn0, t.k_info / t.n)
+        llr = (-1.0 + sigma * rng.standard_normal((1, t.n))).astype(np.float32)
+        ref_hard, ref_soft, _ = O.decode_f32(t, llr, 10, O.OMS, 0.0)
+        for k in (0, 1, 7):
+            dec = decoder("648x324", k, 64)
+            d_hard = torch.empty((1, t.n), dtype=torch.uint8, device="cuda")
+            d_soft = torch.empty((1, t.n), dtype=torch.float32, device="cuda")
+            dec.decode_f32_device(torch.from_numpy(llr).cuda(), d_hard, 10, params=default_params(algo=ALGO_MS),
+                                  soft=d_soft)
+            torch.cuda.synchronize()
+            assert np.max(np.abs(d_soft.cpu().numpy() - ref_soft)) <= FLOAT_TOL, (ebn0, k)
+            assert np.array_equal(d_hard.cpu().numpy(), ref_hard), (ebn0, k)
+
+
 @pytest.mark.parametrize("code,batch,is_float", [("816x408", 4096, False), ("648x324", 4096, True),
                                                  ("648x324", 3000, False), ("200x100", 9000, True)])
 def test_lds_kernel_large_batches(code, batch, is_float):
