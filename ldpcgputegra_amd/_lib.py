@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libldpc_mi355x.so")
+# LDPC_MI355X_LIB: an alternative build of the same library (kernel variants, tools/variants.sh)
+LIB_PATH = os.environ.get("LDPC_MI355X_LIB") or os.path.join(_HERE, "libldpc_mi355x.so")
 
 LDPC_OK, LDPC_EINVAL, LDPC_EUNSUPPORTED, LDPC_EDEVICE, LDPC_ENOMEM, LDPC_EIO = 0, -1, -2, -3, -4, -5
 ALGO_OMS, ALGO_NMS, ALGO_MS = 0, 1, 2

@@ -62,7 +62,10 @@ namespace {
 constexpr int CW = 16;     // codewords per workgroup
 constexpr int NP = 8;      // codeword pairs per workgroup = lanes per slot
 constexpr int WS_DEFAULT = 3;   // slab waves per role (S = 8 WS checks per window); LDPC_COOP2_WS = 3 | 4
-constexpr int R2 = 3;      // prefetch depth (windows)
+#ifndef LDPC_COOP2_R
+#define LDPC_COOP2_R 3
+#endif
+constexpr int R2 = LDPC_COOP2_R;   // prefetch depth (windows)
 constexpr int DIST = 2;    // windows closer than DIST + 1 share no information variable (plan rule)
 constexpr int DPER = 3;    // a window table's LDS-DMA is waited for DPER periods after its issue
 constexpr int KAHEAD = R2 + 2 + DPER;   // ... which is KAHEAD windows ahead of the chain
@@ -599,17 +602,12 @@ __global__ void __launch_bounds__(64 * (2 * WS + 1)) coop2_decode(Coop2Args a)
         };
         const int np = G + 1, nfull = np / U;
         int p = 0;
-        for (int i = 0; i < nfull; i++, p += U) {
-            step(std::integral_constant<int, 0>{}, p);
-            step(std::integral_constant<int, 1>{}, p + 1);
-            step(std::integral_constant<int, 2>{}, p + 2);
-            step(std::integral_constant<int, 3>{}, p + 3);
-        }
-        static_assert(U == 4, "unroll");
+        for (int i = 0; i < nfull; i++, p += U)
+            static_for<0, U>([&](auto jc) { step(jc, p + decltype(jc)::value); });
         const int rem = np - nfull * U;
-        if (rem > 0) step(std::integral_constant<int, 0>{}, p);
-        if (rem > 1) step(std::integral_constant<int, 1>{}, p + 1);
-        if (rem > 2) step(std::integral_constant<int, 2>{}, p + 2);
+        static_for<0, U - 1>([&](auto jc) {
+            if (rem > decltype(jc)::value) step(jc, p + decltype(jc)::value);
+        });
     } else {
         // ----------------------------------------------------- post waves
         if (a.post_prio) __builtin_amdgcn_s_setprio(1);
