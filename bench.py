@@ -117,7 +117,7 @@ MIXED_CODES = ("dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r8_9", "dvbs2_r9_10")
 MIXED_EBN0 = {"dvbs2_r1_2": 1.0, "dvbs2_r2_3": 2.2, "dvbs2_r8_9": 4.6, "dvbs2_r9_10": 5.0}
 
 
-def bench_mixed(a, rank, world, torch, dist):
+def bench_mixed(a, rank, world, local, torch, dist):
     """configs[4]: one batch of B codewords per GPU mixing the DVB-S2 normal
     frame rates the reference ships (3/4 and 5/6 are absent from it), codeword
     c using rate c % 4, each rate at its own Eb/N0 near the waterfall, int8
@@ -132,14 +132,14 @@ def bench_mixed(a, rank, world, torch, dist):
     B = a.batch
     codes = [Code(n) for n in MIXED_CODES]
     N = codes[0].n
-    mx = MixedDecoder(codes, device=int(os.environ.get("LOCAL_RANK", "0")), max_batch=B)
+    mx = MixedDecoder(codes, device=local, max_batch=B)
     ids = np.arange(B, dtype=np.int32) % len(codes)
     first_cw, _ = shard_range(rank, world, B * world)
     llr = torch.empty((B, N), dtype=torch.int8, device="cuda")
     for c, code in enumerate(codes):      # all-zero codeword per rate (CFakeEncoder), own channel
         sel = torch.from_numpy(np.where(ids == c)[0]).cuda()
         tmp = torch.empty((sel.numel(), N), dtype=torch.int8, device="cuda")
-        gen = Decoder(code, device=int(os.environ.get("LOCAL_RANK", "0")), max_batch=max(1, sel.numel()))
+        gen = Decoder(code, device=local, max_batch=max(1, sel.numel()))
         table = channel.i8_table(channel.sigma_from_ebn0(MIXED_EBN0[code.name], code.k_info / code.n), 8, 31)
         gen.awgn_i8_device(tmp, first_cw=first_cw + c * B, seed=a.seed, table=table)
         llr[sel] = tmp
@@ -212,12 +212,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # "gloo" rehearses N ranks on fewer GPUs (ranks share devices round-robin);
+    # the driver's runs use RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("LDPC_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     if a.mixed:
-        bench_mixed(a, rank, world, torch, dist)
+        bench_mixed(a, rank, world, local, torch, dist)
         if world > 1:
             dist.destroy_process_group()
         return
