@@ -475,12 +475,31 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
 // `arret` test, CDecoder_OMS_fixed_SSE.cpp:551-553; the oracle's early_term).
 // Block = 64 consecutive codewords (coalesced V rows) x a chunk of checks;
 // the H indices are wave-uniform (scalar loads).
+// 1 if any of the 4 consecutive degree-D checks at ev fails
+template <int D>
+__device__ __forceinline__ int parity4(const int8_t *V, const uint32_t *ev, int stride, int b)
+{
+    int8_t x[4 * D];
+#pragma unroll
+    for (int j = 0; j < 4 * D; j++) x[j] = V[(size_t)ev[j] * stride + b];
+    int bad = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int par = 0;
+#pragma unroll
+        for (int j = 0; j < D; j++) par ^= x[i * D + j] > 0;
+        bad |= par;
+    }
+    return bad;
+}
+
 __global__ void __launch_bounds__(64) syndrome_k(const int8_t *V, int stride, int batch, const uint32_t *ev,
                                                  const int *gdeg, const int *gcnt, int ngroups, int m, int chunk,
                                                  const uint8_t *live, uint32_t *bad)
 {
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= batch || !live[b]) return;
+    if (__hip_atomic_load(&bad[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;   // another chunk failed
     const int c0 = blockIdx.y * chunk, c1 = min(m, c0 + chunk);
     int g = 0, gfirst = 0, e = 0;
     while (g < ngroups && c0 >= gfirst + gcnt[g]) {
@@ -492,16 +511,25 @@ __global__ void __launch_bounds__(64) syndrome_k(const int8_t *V, int stride, in
     e += (c0 - gfirst) * d;
     int gend = gfirst + gcnt[g];
     int badv = 0;
-    for (int c = c0; c < c1; c++) {
+    for (int c = c0; c < c1;) {
         if (c == gend) {
             g++;
             d = gdeg[g];
             gend += gcnt[g];
         }
-        int par = 0;
-        for (int j = 0; j < d; j++) par ^= V[(size_t)ev[e + j] * stride + b] > 0;
-        badv |= par;
-        e += d;
+        // four checks of the coop degrees at a time: all their gathers in flight at once
+        if (c + 4 <= min(c1, gend) && (d == 7 || d == 10)) {
+            badv = d == 7 ? parity4<7>(V, ev + e, stride, b) : parity4<10>(V, ev + e, stride, b);
+            c += 4;
+            e += 4 * d;
+        } else {
+            int par = 0;
+            for (int j = 0; j < d; j++) par ^= V[(size_t)ev[e + j] * stride + b] > 0;
+            badv = par;
+            c++;
+            e += d;
+        }
+        if (badv) break;   // one failing check decides: live codewords stop early
     }
     if (badv) atomicOr(&bad[b], 1u);
 }

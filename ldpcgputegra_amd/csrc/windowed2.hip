@@ -380,19 +380,25 @@ LDPC_DEV int run_group(const W2Args &a, const uint32_t *tab, int wb, int we, int
     return carry;
 }
 
+// 1 if a check of these windows fails for codeword row `row` (its S lanes
+// see the same answer); the row stops at its first failing window -- a live
+// codeword almost always fails early, so only converging codewords scan all
 template <int D, int S>
-LDPC_DEV int syndrome_part(const W2Args &a, const uint32_t *tab, int nwin, int slot, int b)
+LDPC_DEV int syndrome_part(const W2Args &a, const uint32_t *tab, int nwin, int slot, int row, int b)
 {
+    constexpr unsigned long long RM = (S == 64) ? ~0ull : ((1ull << S) - 1);
     int bad = 0;
     for (int w = 0; w < nwin; w++) {
         const uint32_t *p = tab + (size_t)w * (D + 1) * S + slot;
-        if (!((p[D * S] >> 24) & F_ACT)) continue;
         int par = 0;
+        if ((p[D * S] >> 24) & F_ACT) {
 #pragma unroll
-        for (int j = 0; j < D; j++) par ^= (a.V[p[j * S] * (uint32_t)a.stride + b] > 0);
+            for (int j = 0; j < D; j++) par ^= (a.V[p[j * S] * (uint32_t)a.stride + b] > 0);
+        }
         bad |= par;
+        if ((__ballot(bad) >> (row * S)) & RM) return 1;
     }
-    return bad;
+    return 0;
 }
 
 template <int D0, int S, int P>
@@ -413,9 +419,8 @@ __global__ void __launch_bounds__(64) windowed2_decode(W2Args a)
         it++;
         if (a.early) {
             if (live) {
-                int bad = syndrome_part<D0, S>(a, tab0, a.g0_end, slot, b) |
-                          syndrome_part<D0 - 1, S>(a, tab1, a.n_windows - a.g0_end, slot, b);
-                for (int m = 1; m < S; m <<= 1) bad |= __shfl_xor(bad, m, 64);
+                int bad = syndrome_part<D0, S>(a, tab0, a.g0_end, slot, row, b);
+                if (!bad) bad = syndrome_part<D0 - 1, S>(a, tab1, a.n_windows - a.g0_end, slot, row, b);
                 if (!bad) {
                     live = false;
                     if (slot == 0 && a.iters_used) a.iters_used[b] = it;
