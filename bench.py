@@ -120,7 +120,8 @@ MIXED_EBN0 = {"dvbs2_r1_2": 1.0, "dvbs2_r2_3": 2.2, "dvbs2_r8_9": 4.6, "dvbs2_r9
 def bench_mixed(a, rank, world, local, torch, dist):
     """configs[4]: one batch of B codewords per GPU mixing the DVB-S2 normal
     frame rates the reference ships (3/4 and 5/6 are absent from it), codeword
-    c using rate c % 4, each rate at its own Eb/N0 near the waterfall, int8
+    c using rate c % 4, each rate at its own Eb/N0 (r1/2 and
+    r2/3 in the waterfall, r8/9 and r9/10 just past it: FER 0 at 2 x 1024 frames), int8
     OMS with early termination (per-codeword syndrome after every iteration),
     at most a.iters iterations.  A step = the mixed decode of the whole batch
     (per-rate gather, concurrent per-rate decodes on their own streams,

@@ -35,6 +35,7 @@
 //   stores and later loads of one workgroup are ordered by issue order (the
 //   gfx950 workgroup-scope memory model needs no vmcnt wait for that).
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "coop.h"
@@ -804,7 +805,14 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     if (!L.live || !L.bad || !L.iters_used) return -1;
     const int nb = (L.batch + 255) / 256;
     hipLaunchKernelGGL(early_init_k, dim3(nb), dim3(256), 0, s, L.batch, L.live, L.bad, L.iters_used, L.iters);
-    constexpr int kChunk = 512;
+    // checks per syndrome thread: a codeword that is still failing late in
+    // the decode often has few unsatisfied checks, so its threads walk whole
+    // chunks; short chunks keep that walk (dependent gather rounds) short
+    static const int kChunk = [] {
+        const char *e = getenv("LDPC_SYND_CHUNK");
+        const int v = (e && *e) ? atoi(e) : 64;
+        return v >= 4 && v <= 4096 ? v : 64;
+    }();
     const dim3 sgrid((L.batch + 63) / 64, (L.m + kChunk - 1) / kChunk);
     for (int it = 0; it < L.iters; it++) {
         if (launch_coop_iters(L, cc, 1, L.live, s)) return -1;

@@ -3,6 +3,8 @@
 // group into a contiguous staging batch, decode the groups concurrently on
 // their contexts' streams (forked from and joined back to the caller's
 // stream with events), scatter hard decisions / iterations back.
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "kernels.h"
@@ -12,6 +14,7 @@ struct ldpc_mixed {
     int device = 0, n = 0, max_batch = 0;
     std::vector<ldpc_ctx *> ctx;
     std::vector<hipStream_t> stream;
+    std::vector<bool> own_stream;     // created here (priority streams), destroyed here
     std::vector<int8_t *> d_in;
     std::vector<uint8_t *> d_out;
     std::vector<int32_t *> d_idx, d_its;
@@ -33,6 +36,7 @@ extern "C" void ldpc_mixed_destroy(ldpc_mixed *mx)
         (void)hipFree(mx->d_its[c]);
         if (mx->h_idx[c]) (void)hipHostFree(mx->h_idx[c]);
         if (mx->done[c]) (void)hipEventDestroy(mx->done[c]);
+        if (mx->own_stream[c]) (void)hipStreamDestroy(mx->stream[c]);
         ldpc_ctx_destroy(mx->ctx[c]);
     }
     if (mx->fork) (void)hipEventDestroy(mx->fork);
@@ -62,6 +66,17 @@ extern "C" int ldpc_mixed_create(const ldpc_code *const *codes, int n_codes, int
     mx->h_idx.assign(nc, nullptr);
     mx->done.assign(nc, nullptr);
     mx->pending.assign(nc, false);
+    mx->own_stream.assign(nc, false);
+    // LDPC_MIXED_PRIO=1: the codes with the most checks (longest serial chain
+    // per iteration, so the longest latency under early termination) get
+    // high-priority streams, so their per-iteration launches are dispatched
+    // ahead of the high-rate codes' pending workgroups
+    const char *pe = getenv("LDPC_MIXED_PRIO");
+    const int prio = pe ? atoi(pe) : 0;   // 2: the reverse (fewest checks first), for experiments
+    std::vector<int> ms;
+    for (int c = 0; c < n_codes; c++) ms.push_back(codes[c]->m);
+    std::sort(ms.begin(), ms.end());
+    const int m_hi = ms[ms.size() / 2];
     for (int c = 0; c < n_codes; c++) {
         int rc = ldpc_ctx_create(codes[c], device, max_batch, &mx->ctx[c]);
         if (rc != LDPC_OK) {
@@ -71,6 +86,18 @@ extern "C" int ldpc_mixed_create(const ldpc_code *const *codes, int n_codes, int
         void *s;
         ldpc_ctx_stream(mx->ctx[c], &s);
         mx->stream[c] = (hipStream_t)s;
+        if (prio) {
+            int least = 0, greatest = 0;
+            hipStream_t ps = nullptr;
+            if (hipSetDevice(device) != hipSuccess || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                hipStreamCreateWithPriority(&ps, hipStreamNonBlocking, (codes[c]->m >= m_hi) == (prio == 1) ? greatest : least) !=
+                    hipSuccess) {
+                ldpc_mixed_destroy(mx);
+                return ldpc_set_error(LDPC_EDEVICE, "mixed: priority stream");
+            }
+            mx->stream[c] = ps;
+            mx->own_stream[c] = true;
+        }
         const size_t bytes = (size_t)max_batch * mx->n;
         if (hipMalloc(&mx->d_in[c], bytes) != hipSuccess || hipMalloc(&mx->d_out[c], bytes) != hipSuccess ||
             hipMalloc(&mx->d_idx[c], 4ull * max_batch) != hipSuccess ||

@@ -303,3 +303,47 @@ def test_mixed_rate_batch_with_early_termination():
         eh, _, eit = O.decode_i8(load_table(name), llr[sel], 20, early_term=True, return_soft=True)
         assert np.array_equal(hard[sel], eh), name
         assert np.array_equal(its[sel], eit), name
+
+
+def test_device_calls_ordered_with_torch_default_stream():
+    """Device-pointer calls made while torch is on its default stream are
+    fenced against it: a torch op issued right after the generator / decoder
+    sees their complete output (regression: the NULL stream used to mean the
+    context's own non-blocking stream, unordered with torch's work, which
+    corrupted bench.py --mixed's per-rate inputs)."""
+    torch = _torch()
+    from ldpcgputegra_amd.decoder import MixedDecoder
+    names = ("dvbs2_r1_2", "dvbs2_r8_9")
+    codes = [Code(n) for n in names]
+    n, per = codes[0].n, 64
+    ids = np.arange(2 * per, dtype=np.int32) % 2
+    llr = torch.zeros((2 * per, n), dtype=torch.int8, device="cuda")
+    host = np.empty((2 * per, n), dtype=np.int8)
+    for c, code in enumerate(codes):
+        sel = np.where(ids == c)[0]
+        table = channel.i8_table(channel.sigma_from_ebn0(1.0 + 3 * c, code.k_info / n), 8, 31)
+        gen = Decoder(code, max_batch=per)
+        for rep in range(3):   # reused allocator blocks: a stale tmp would show
+            tmp = torch.empty((per, n), dtype=torch.int8, device="cuda")
+            gen.awgn_i8_device(tmp, first_cw=c * 1000, seed=11, table=table)
+            llr[torch.from_numpy(sel).cuda()] = tmp
+        gen.close()
+        host[sel] = channel.awgn_i8_host(n, per, 11, table, first_cw=c * 1000)
+    assert np.array_equal(llr.cpu().numpy(), host)
+    mx = MixedDecoder(codes, max_batch=2 * per)
+    hard = torch.empty((2 * per, n), dtype=torch.uint8, device="cuda")
+    its = torch.empty(2 * per, dtype=torch.int32, device="cuda")
+    p = default_params(early_term=1)
+    mx.decode_i8_device(llr, hard, ids, 20, params=p, iters_used=its)
+    got_h, got_i = hard.cpu().numpy(), its.cpu().numpy()   # no explicit synchronize
+    for c, code in enumerate(codes):
+        sel = np.where(ids == c)[0]
+        dec = Decoder(code, max_batch=per)
+        x = llr[torch.from_numpy(sel).cuda()].contiguous()
+        h2 = torch.empty((per, n), dtype=torch.uint8, device="cuda")
+        i2 = torch.empty(per, dtype=torch.int32, device="cuda")
+        dec.decode_i8_device(x, h2, 20, params=p, iters_used=i2)
+        assert np.array_equal(h2.cpu().numpy(), got_h[sel])
+        assert np.array_equal(i2.cpu().numpy(), got_i[sel])
+        dec.close()
+    mx.close()
