@@ -51,6 +51,8 @@ struct ldpc_ctx {
     size_t io_bytes = 0;
     void *d_early = nullptr;        // coop early termination: live[stride] u8, bad[stride] u32, iters[stride]
     size_t early_bytes = 0;
+    void *d_Vs = nullptr;           // coop2 early termination: V snapshot [N+1][stride]
+    size_t Vs_bytes = 0;
     // kernel timing (ldpc_ctx_profile)
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -145,6 +147,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     (void)hipFree(c->d_msg);
     (void)hipFree(c->d_io);
     (void)hipFree(c->d_early);
+    (void)hipFree(c->d_Vs);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -339,12 +342,16 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     L.early = p->early_term;
     L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
     L.iters_used = d_iters;
-    if (kern == 5 && p->early_term) {
+    if ((kern == 5 || kern == 6) && p->early_term) {
         // live u8 | bad u32 | iterations used i32 (when the caller passed none)
         if ((rc = ensure(&c->d_early, &c->early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
         L.bad = (uint32_t *)c->d_early;
         if (!L.iters_used) L.iters_used = (int32_t *)((char *)c->d_early + (size_t)stride * 4);
         L.live = (uint8_t *)c->d_early + (size_t)stride * 8;
+        if (kern == 6) {
+            if ((rc = ensure(&c->d_Vs, &c->Vs_bytes, (size_t)(h->n + 1) * stride)) != LDPC_OK) return rc;
+            L.Vs = (int8_t *)c->d_Vs;
+        }
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (c->profile) {

@@ -17,6 +17,12 @@ bool coop_params_ok(const ldpc_params *p);
 int coop_upload(const ldpc_code *h, CoopCode *cc);
 void coop_free(CoopCode *cc);
 int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
+// early termination around per-iteration launches (coop and coop2): init,
+// syndrome after iteration `it` (0-based; with L.Vs, snapshot of the codewords
+// converging now), and the final merge of the snapshots into V (L.Vs only)
+int coop_early_begin(const DecodeLaunch &L, hipStream_t s);
+int coop_early_after_iter(const DecodeLaunch &L, int it, hipStream_t s);
+int coop_early_end(const DecodeLaunch &L, hipStream_t s);
 // host-side plan (tests: ldpc_code_coop_plan)
 int coop_plan_windows(const ldpc_code *h, int S, int R, int dist, std::vector<int> &first, std::vector<int> &count,
                       int *tail, int *n_fwd);

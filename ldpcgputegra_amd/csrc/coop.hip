@@ -552,6 +552,28 @@ __global__ void fill_iters_k(int batch, int32_t *iters_used, int iters)
     if (b < batch) iters_used[b] = iters;
 }
 
+// codewords converging after this iteration (live, no failing check): copy
+// their V column; block = 64 codewords x a chunk of rows
+constexpr int kSnapRows = 512;
+__global__ void __launch_bounds__(64) snapshot_k(const int8_t *V, int8_t *Vs, int stride, int batch, int rows,
+                                                 const uint8_t *live, const uint32_t *bad)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= batch || !live[b] || bad[b]) return;
+    const int r0 = blockIdx.y * kSnapRows, r1 = min(rows, r0 + kSnapRows);
+    for (int r = r0; r < r1; r++) Vs[(size_t)r * stride + b] = V[(size_t)r * stride + b];
+}
+
+// after the last iteration: converged codewords take their snapshot back
+__global__ void __launch_bounds__(64) merge_snapshot_k(int8_t *V, const int8_t *Vs, int stride, int batch, int rows,
+                                                       const uint8_t *live)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= batch || live[b]) return;
+    const int r0 = blockIdx.y * kSnapRows, r1 = min(rows, r0 + kSnapRows);
+    for (int r = r0; r < r1; r++) V[(size_t)r * stride + b] = Vs[(size_t)r * stride + b];
+}
+
 __global__ void early_init_k(int batch, uint8_t *live, uint32_t *bad, int32_t *iters_used, int iters)
 {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -802,9 +824,23 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     }
     // early termination: one launch per iteration (V, messages and the chain
     // input V[p_0] carry the state), then the syndrome of the live codewords
+    if (coop_early_begin(L, s)) return -1;
+    for (int it = 0; it < L.iters; it++)
+        if (launch_coop_iters(L, cc, 1, L.live, s) || coop_early_after_iter(L, it, s)) return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int coop_early_begin(const DecodeLaunch &L, hipStream_t s)
+{
     if (!L.live || !L.bad || !L.iters_used) return -1;
     const int nb = (L.batch + 255) / 256;
     hipLaunchKernelGGL(early_init_k, dim3(nb), dim3(256), 0, s, L.batch, L.live, L.bad, L.iters_used, L.iters);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int coop_early_after_iter(const DecodeLaunch &L, int it, hipStream_t s)
+{
+    const int nb = (L.batch + 255) / 256;
     // checks per syndrome thread: a codeword that is still failing late in
     // the decode often has few unsatisfied checks, so its threads walk whole
     // chunks; short chunks keep that walk (dependent gather rounds) short
@@ -814,12 +850,20 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
         return v >= 4 && v <= 4096 ? v : 64;
     }();
     const dim3 sgrid((L.batch + 63) / 64, (L.m + kChunk - 1) / kChunk);
-    for (int it = 0; it < L.iters; it++) {
-        if (launch_coop_iters(L, cc, 1, L.live, s)) return -1;
-        hipLaunchKernelGGL(syndrome_k, sgrid, dim3(64), 0, s, (const int8_t *)L.V, L.stride, L.batch, L.d_edge_var,
-                           L.d_group_deg, L.d_group_cnt, L.n_groups, L.m, kChunk, (const uint8_t *)L.live, L.bad);
-        hipLaunchKernelGGL(syndrome_finish_k, dim3(nb), dim3(256), 0, s, L.batch, L.live, L.bad, L.iters_used,
-                           it + 1);
-    }
+    hipLaunchKernelGGL(syndrome_k, sgrid, dim3(64), 0, s, (const int8_t *)L.V, L.stride, L.batch, L.d_edge_var,
+                       L.d_group_deg, L.d_group_cnt, L.n_groups, L.m, kChunk, (const uint8_t *)L.live, L.bad);
+    if (L.Vs)
+        hipLaunchKernelGGL(snapshot_k, dim3((L.batch + 63) / 64, (L.n + kSnapRows - 1) / kSnapRows), dim3(64), 0, s,
+                           (const int8_t *)L.V, L.Vs, L.stride, L.batch, L.n, (const uint8_t *)L.live,
+                           (const uint32_t *)L.bad);
+    hipLaunchKernelGGL(syndrome_finish_k, dim3(nb), dim3(256), 0, s, L.batch, L.live, L.bad, L.iters_used, it + 1);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int coop_early_end(const DecodeLaunch &L, hipStream_t s)
+{
+    if (!L.Vs) return 0;
+    hipLaunchKernelGGL(merge_snapshot_k, dim3((L.batch + 63) / 64, (L.n + kSnapRows - 1) / kSnapRows), dim3(64), 0, s,
+                       (int8_t *)L.V, (const int8_t *)L.Vs, L.stride, L.batch, L.n, (const uint8_t *)L.live);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -34,8 +34,10 @@
 //   for every information edge.
 // The workgroup owns 16 codewords: 8 pairs = 8 lanes per slot, 8 slots per
 // slab wave, S = 8 WS checks per window.  With WS = 3 every wave has a SIMD of
-// its own.  Early termination stays on coop.hip (a converged codeword may
-// share a lane with a live one).
+// its own.  Early termination: one launch per iteration (coop.hip's syndrome
+// driver); a converged codeword may share a lane with a live one, so instead
+// of masking its stores it keeps iterating and its V column is snapshot when
+// it converges and merged back at the end (snapshot_k / merge_snapshot_k).
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -174,6 +176,7 @@ struct Coop2Args {
     uint8_t *Mc;                   // [pitch / 16][mrows][8 pairs][2] u32; row m is the sink
     const uint32_t *tab;           // [nw][S][RECW] slot records
     unsigned long long *stamps;    // diagnostic build: [grid][waves][4]
+    const uint8_t *live;           // early termination: [pitch] 0 = converged (NULL: all live)
     int pitch, G, nw, tail, mrows, n, remap, prio, off;
     int pre_prio, post_prio;       // s_setprio of the pre / post waves (the chain wave: prio ? 2 : 0)
     uint32_t rmm, coff;            // R(msg_max), C(offset) per half
@@ -506,6 +509,9 @@ __global__ void __launch_bounds__(64 * (2 * WS + 1)) coop2_decode(Coop2Args a)
     const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
     const int G = a.G;
     if (G == 0) return;
+    // early termination: a workgroup whose 16 codewords all converged skips
+    // the iteration (the others iterate all 16; converged ones were snapshot)
+    if (a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
     unsigned long long sA = 0, sB = 0, sL = 0, t0 = 0, tx = 0;
     auto write_stamps = [&]() {
         if (STAMP && lane == 0) {
@@ -692,7 +698,7 @@ int launch_ws(const Coop2Args &a, int grid, bool stamped, hipStream_t s)
 
 }  // namespace
 
-bool coop2_params_ok(const ldpc_params *p) { return coop_params_ok(p) && !p->early_term; }
+bool coop2_params_ok(const ldpc_params *p) { return coop_params_ok(p); }
 
 // the V descriptor's record stride is a 14-bit byte count
 bool coop2_stride_ok(int stride) { return stride > 0 && stride % 64 == 0 && stride < (1 << 14); }
@@ -735,18 +741,37 @@ int coop2_upload(const ldpc_code *h, CoopCode *cc)
     return LDPC_OK;
 }
 
+static int launch_coop2_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
+                              hipStream_t s);
+
 int launch_coop2(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
 {
-    if (!cc.valid || L.early || !coop2_stride_ok(L.stride)) return -1;
+    if (!cc.valid || !coop2_stride_ok(L.stride)) return -1;
+    if (L.early) {
+        // one launch per iteration as coop.hip; converged codewords keep
+        // iterating inside live workgroups, so their V is snapshot when they
+        // converge and merged back at the end (L.Vs)
+        if (!L.Vs || coop_early_begin(L, s)) return -1;
+        for (int it = 0; it < L.iters; it++)
+            if (launch_coop2_iters(L, cc, 1, L.live, s) || coop_early_after_iter(L, it, s)) return -1;
+        return coop_early_end(L, s);
+    }
     if (L.iters_used)
         hipLaunchKernelGGL(fill_iters2_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used,
                            L.iters);
+    return launch_coop2_iters(L, cc, L.iters, nullptr, s);
+}
+
+static int launch_coop2_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
+                              hipStream_t s)
+{
     Coop2Args a{};
+    a.live = live;
     a.V = (int8_t *)L.V;
     a.Mc = (uint8_t *)L.msg;
     a.tab = cc.d_tab;
     a.pitch = L.stride;
-    a.G = cc.nw * L.iters;
+    a.G = cc.nw * iters;
     a.nw = cc.nw;
     a.tail = cc.tail;
     a.mrows = L.m + 1;

@@ -23,6 +23,10 @@ struct DecodeLaunch {
     // early-termination scratch of the coop kernel ([stride] each)
     uint8_t *live;
     uint32_t *bad;
+    // coop2 early termination: V snapshot taken when a codeword converges
+    // (coop2 keeps iterating converged codewords that share a workgroup with
+    // live ones; the snapshot is merged back before the hard decisions)
+    int8_t *Vs;
 };
 
 int launch_generic(const DecodeLaunch &L, hipStream_t s);

@@ -166,8 +166,6 @@ def test_early_termination_vs_oracle(code):
     ref_hard, ref_soft, ref_its = O.decode_i8(t, llr, 30, O.OMS, 1, early_term=True, return_soft=True)
     assert ref_its.min() < 30                                # some codewords stop early
     for k in kernels_for(code):
-        if k == 6:          # coop2 has no early termination (auto selection falls back to coop)
-            continue
         dec = decoder(code, k, max_batch=64)
         d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
         d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
