@@ -554,14 +554,27 @@ __global__ void fill_iters_k(int batch, int32_t *iters_used, int iters)
 
 // codewords converging after this iteration (live, no failing check): copy
 // their V column; block = 64 codewords x a chunk of rows
-constexpr int kSnapRows = 512;
+constexpr int kSnapRows = 128;
+// rows [r0, r1) of column b, 16 loads in flight per round (a lone thread's
+// strided column copy is latency-bound otherwise)
+__device__ __forceinline__ void copy_column(const int8_t *src, int8_t *dst, int stride, int b, int r0, int r1)
+{
+    int r = r0;
+    for (; r + 16 <= r1; r += 16) {
+        int8_t x[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) x[i] = src[(size_t)(r + i) * stride + b];
+#pragma unroll
+        for (int i = 0; i < 16; i++) dst[(size_t)(r + i) * stride + b] = x[i];
+    }
+    for (; r < r1; r++) dst[(size_t)r * stride + b] = src[(size_t)r * stride + b];
+}
 __global__ void __launch_bounds__(64) snapshot_k(const int8_t *V, int8_t *Vs, int stride, int batch, int rows,
                                                  const uint8_t *live, const uint32_t *bad)
 {
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= batch || !live[b] || bad[b]) return;
-    const int r0 = blockIdx.y * kSnapRows, r1 = min(rows, r0 + kSnapRows);
-    for (int r = r0; r < r1; r++) Vs[(size_t)r * stride + b] = V[(size_t)r * stride + b];
+    copy_column(V, Vs, stride, b, blockIdx.y * kSnapRows, min(rows, (int)(blockIdx.y + 1) * kSnapRows));
 }
 
 // after the last iteration: converged codewords take their snapshot back
@@ -570,8 +583,7 @@ __global__ void __launch_bounds__(64) merge_snapshot_k(int8_t *V, const int8_t *
 {
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= batch || live[b]) return;
-    const int r0 = blockIdx.y * kSnapRows, r1 = min(rows, r0 + kSnapRows);
-    for (int r = r0; r < r1; r++) V[(size_t)r * stride + b] = Vs[(size_t)r * stride + b];
+    copy_column(Vs, V, stride, b, blockIdx.y * kSnapRows, min(rows, (int)(blockIdx.y + 1) * kSnapRows));
 }
 
 __global__ void early_init_k(int batch, uint8_t *live, uint32_t *bad, int32_t *iters_used, int iters)
