@@ -146,7 +146,7 @@ int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
 /* Select kernel family: 0 = auto, 1 = generic (per-edge messages),
  * 2 = windowed layered kernel (compressed messages), 3 / 4 = windowed2
  * (S = 16 / 32), 5 = workgroup-cooperative DVB-S2 kernel, 6 = its packed-pair
- * variant (two codewords per lane; first-group degree 7, no early termination),
+ * variant (two codewords per lane; first-group degree 7; early termination by per-iteration launches),
  * 7 = LDS-resident short-code kernel (whole state in LDS; int8 and float). */
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);

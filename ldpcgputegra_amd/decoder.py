@@ -54,7 +54,7 @@ class Decoder:
     def set_kernel(self, kernel):
         """0 = auto, 1 = generic (per-edge messages), 2 = windowed, 3/4 =
         windowed2 (S = 16/32), 5 = workgroup-cooperative DVB-S2 kernel, 6 = its
-        packed-pair variant (two codewords per lane; DVB-S2 r1/2, no early termination),
+        packed-pair variant (two codewords per lane; DVB-S2 r1/2, early termination by per-iteration launches),
         7 = LDS-resident short-code kernel (int8 and float)."""
         _lib.check(_lib.lib().ldpc_ctx_set_kernel(self._ctx, int(kernel)))
 
