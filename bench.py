@@ -18,6 +18,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md).
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -42,7 +43,7 @@ def parse():
                     help="0 auto, 1 generic, 2 windowed, 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2 (packed pairs)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (cgroup quota / affinity)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     a = ap.parse_args()
     f32 = a.dtype == "f32"
@@ -60,38 +61,77 @@ def hbm_peak_gbs():
     return 8000.0
 
 
-def cpu_baseline(code_name, iters, budget_s, threads, seed):
-    """Time the reference's own SSE decoder (oracle/_ref, kind "reference")
-    or, if it was not built, the oracle port, on the host cores."""
+def host_cpu_info():
+    """CPU model, physical cores, logical CPUs and the CPU share this process
+    may use (the GPU box grants a cgroup quota of 16 CPUs per GPU on a larger
+    host: threads beyond it are throttled, not run)."""
+    info = {"model": None, "physical_cores": None, "logical_cpus": os.cpu_count(), "cpu_quota": None}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {}
+        for line in out.splitlines():
+            if ":" in line:
+                k, v = line.split(":", 1)
+                kv[k.strip()] = v.strip()
+        info["model"] = kv.get("Model name")
+        if kv.get("Core(s) per socket") and kv.get("Socket(s)"):
+            info["physical_cores"] = int(kv["Core(s) per socket"]) * int(kv["Socket(s)"])
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
+    import oracle as O
+    info["cpu_quota"] = O.host_threads()
+    return info
+
+
+def cpu_baseline(code_name, iters, budget_s, threads, seed):
+    """Time the reference's own SSE decoder (oracle/_ref, kind "reference";
+    one decoder object per thread decoding 16 frames per call, as
+    code/x86/main_p.cpp:473-576) or, if it was not built, the oracle port, on
+    `threads` host threads (default: the whole CPU share of this process)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from ldpcgputegra_amd import channel, load_table
     t = load_table(code_name)
     table = channel.i8_table(channel.sigma_from_ebn0(1.0, t.k_info / t.n))
     kind = "reference" if O.ref_available(code_name) else "port"
-    blk = 16 * threads                     # one 16-frame decode() call per thread per round
-    llr = channel.awgn_i8_host(t.n, blk, seed, table)
-    done, t0 = 0, time.perf_counter()
-    while True:
-        if kind == "reference":
-            O.ref_decode_mt(code_name, llr, iters, 1, threads)
-        else:
-            O.decode_i8_mt(t, llr, iters, 1, threads)
-        done += blk
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
+
+    def rate(thr, budget):
+        blk = 16 * thr                     # one 16-frame decode() call per thread per round
+        llr = channel.awgn_i8_host(t.n, blk, seed, table)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            if kind == "reference":
+                O.ref_decode_mt(code_name, llr, iters, 1, thr)
+            else:
+                O.decode_i8_mt(t, llr, iters, 1, thr)
+            done += blk
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done, el
+
+    host = host_cpu_info()
+    done1, el1 = rate(1, max(1.0, budget_s * 0.2))            # per-thread rate, for the all-core projection
+    done, el = rate(threads, budget_s)
     mbps = done * t.n / el / 1e6
+    per_thread = done1 * t.n / el1 / 1e6
     return dict(value=round(mbps, 3), unit="Mbit/s", cores=threads, kind=kind,
-                sample="%s %d it int8 OMS offset 1: %d codewords (%d threads x 16-frame decode() calls) in %.2f s"
-                       % (code_name, iters, done, threads, el))
+                threads=threads, cpu_model=host["model"], host_physical_cores=host["physical_cores"],
+                host_logical_cpus=host["logical_cpus"], cpu_quota=host["cpu_quota"],
+                per_thread_mbps=round(per_thread, 3),
+                all_physical_cores_projection_mbps=(round(per_thread * host["physical_cores"], 1)
+                                                    if host["physical_cores"] else None),
+                sample="%s %d it int8 OMS offset 1: %d codewords (%d threads x 16-frame decode() calls) in %.2f s; "
+                       "1 thread: %d codewords in %.2f s. Threads = this process's CPU share (cgroup quota %s of "
+                       "%s logical CPUs); the all-core figure is per-thread rate x physical cores, a projection, "
+                       "not a measurement" % (code_name, iters, done, threads, el, done1, el1, host["cpu_quota"],
+                                              host["logical_cpus"]))
 
 
-def cpu_baseline_f32(code_name, iters, budget_s, seed):
+def cpu_baseline_f32(code_name, iters, budget_s, threads, seed):
     """The reference has no float decoder (its decode(float*) is a no-op,
     code/x86/CDecoder/template/CDecoder_fixed_SSE.cpp:35-40): time the
-    oracle's scalar float restatement (kind "port") on one core."""
+    oracle's scalar float restatement (kind "port") on `threads` threads."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
@@ -99,18 +139,20 @@ def cpu_baseline_f32(code_name, iters, budget_s, seed):
     t = load_table(code_name)
     sigma = channel.sigma_from_ebn0(1.0, t.k_info / t.n)
     rng = np.random.default_rng(seed)
-    blk = 64
+    blk = 64 * threads
     llr = (-1.0 + sigma * rng.standard_normal((blk, t.n))).astype(np.float32)
     done, t0 = 0, time.perf_counter()
     while True:
-        O.decode_f32(t, llr, iters, O.OMS, 0.0)
+        O.decode_f32(t, llr, iters, O.OMS, 0.0, threads=threads)
         done += blk
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    return dict(value=round(done * t.n / el / 1e6, 3), unit="Mbit/s", cores=1, kind="port",
-                sample="%s %d it float min-sum (oracle restatement, scalar): %d codewords in %.2f s"
-                       % (code_name, iters, done, el))
+    host = host_cpu_info()
+    return dict(value=round(done * t.n / el / 1e6, 3), unit="Mbit/s", cores=threads, kind="port", threads=threads,
+                cpu_model=host["model"], host_physical_cores=host["physical_cores"], cpu_quota=host["cpu_quota"],
+                sample="%s %d it float min-sum (oracle restatement, scalar, one decoder per thread): %d codewords "
+                       "in %.2f s on %d threads" % (code_name, iters, done, el, threads))
 
 
 MIXED_CODES = ("dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r8_9", "dvbs2_r9_10")
@@ -333,8 +375,10 @@ def main():
             },
         }
         if world == 1 and a.cpu_seconds > 0:
-            thr = a.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = (cpu_baseline_f32(a.code, a.iters, a.cpu_seconds, a.seed) if f32 else
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            thr = a.cpu_threads or O.host_threads()
+            out["cpu_baseline"] = (cpu_baseline_f32(a.code, a.iters, a.cpu_seconds, thr, a.seed) if f32 else
                                    cpu_baseline(a.code, a.iters, a.cpu_seconds, thr, a.seed))
         else:
             out["cpu_baseline"] = None

@@ -166,10 +166,11 @@ int ldpc_decode_i8(ldpc_ctx *ctx, const int8_t *llr, uint8_t *hard, int batch, i
 int ldpc_decode_f32(ldpc_ctx *ctx, const float *llr, uint8_t *hard, int batch, int n_iter,
                     const ldpc_params *p);
 
-/* Device buffers, asynchronous on `hip_stream` (NULL = the context stream, a
- * non-blocking stream: it is NOT ordered with the legacy default stream, so a
- * caller working on the default stream passes a stream of its own and fences
- * it, as ldpcgputegra_amd.decoder.Decoder._on_stream does).
+/* Device buffers, asynchronous on `hip_stream`.  NULL means HIP's null
+ * stream, i.e. the legacy default stream, ordered with all blocking streams
+ * (the reference's decode_stream callers, code/gpu_fixed/test.cpp:347-393, and
+ * torch's default stream); the context's own non-blocking stream
+ * (ldpc_ctx_stream) is used only when passed explicitly.
  * soft (optional): final V per bit; iters_used (optional): per codeword. */
 int ldpc_decode_i8_async(ldpc_ctx *ctx, void *hip_stream, const int8_t *d_llr, uint8_t *d_hard,
                          int8_t *d_soft, int32_t *d_iters_used, int batch, int n_iter,

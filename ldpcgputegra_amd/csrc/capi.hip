@@ -269,7 +269,6 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     if (rc != LDPC_OK) return rc;
     if (batch == 0) return LDPC_OK;
     HIP_TRY(hipSetDevice(c->device));
-    if (!s) s = c->stream;
     const ldpc_code *h = c->code;
     const int stride = (batch + 63) / 64 * 64;
     const size_t esz = is_float ? 4 : 1;
@@ -434,7 +433,7 @@ extern "C" int ldpc_awgn_i8_async(ldpc_ctx *c, void *s, int8_t *d_llr, int batch
     HIP_TRY(hipSetDevice(c->device));
     AwgnTable t;
     memcpy(t.t, table, sizeof(t.t));
-    if (launch_awgn_i8(d_llr, c->code->n, batch, first_cw, seed, t, d_codeword, s ? (hipStream_t)s : c->stream))
+    if (launch_awgn_i8(d_llr, c->code->n, batch, first_cw, seed, t, d_codeword, (hipStream_t)s))
         return ldpc_set_error(LDPC_EDEVICE, "awgn: %s", hipGetErrorString(hipGetLastError()));
     return LDPC_OK;
 }
@@ -445,7 +444,7 @@ extern "C" int ldpc_count_errors_async(ldpc_ctx *c, void *s, const uint8_t *d_ha
     if (!c || !d_hard || !d_counts || batch < 0 || k < 0 || k > c->code->n)
         return ldpc_set_error(LDPC_EINVAL, "count_errors args");
     HIP_TRY(hipSetDevice(c->device));
-    if (launch_count_errors(d_hard, c->code->n, batch, k, d_ref, d_counts, s ? (hipStream_t)s : c->stream))
+    if (launch_count_errors(d_hard, c->code->n, batch, k, d_ref, d_counts, (hipStream_t)s))
         return ldpc_set_error(LDPC_EDEVICE, "count_errors: %s", hipGetErrorString(hipGetLastError()));
     return LDPC_OK;
 }

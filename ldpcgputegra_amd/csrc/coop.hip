@@ -586,11 +586,14 @@ __global__ void __launch_bounds__(64) merge_snapshot_k(int8_t *V, const int8_t *
     copy_column(Vs, V, stride, b, blockIdx.y * kSnapRows, min(rows, (int)(blockIdx.y + 1) * kSnapRows));
 }
 
-__global__ void early_init_k(int batch, uint8_t *live, uint32_t *bad, int32_t *iters_used, int iters)
+// live[] covers the padded stride: padding columns are never live, so a
+// workgroup's skip test (any live codeword) does not read stale bytes
+__global__ void early_init_k(int batch, int stride, uint8_t *live, uint32_t *bad, int32_t *iters_used, int iters)
 {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= stride) return;
+    live[b] = b < batch;
     if (b >= batch) return;
-    live[b] = 1;
     bad[b] = 0;
     iters_used[b] = iters;
 }
@@ -845,8 +848,9 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
 int coop_early_begin(const DecodeLaunch &L, hipStream_t s)
 {
     if (!L.live || !L.bad || !L.iters_used) return -1;
-    const int nb = (L.batch + 255) / 256;
-    hipLaunchKernelGGL(early_init_k, dim3(nb), dim3(256), 0, s, L.batch, L.live, L.bad, L.iters_used, L.iters);
+    const int nb = (L.stride + 255) / 256;
+    hipLaunchKernelGGL(early_init_k, dim3(nb), dim3(256), 0, s, L.batch, L.stride, L.live, L.bad, L.iters_used,
+                       L.iters);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

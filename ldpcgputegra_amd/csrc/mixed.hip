@@ -132,7 +132,8 @@ extern "C" int ldpc_decode_i8_mixed_async(ldpc_mixed *mx, void *hip_stream, cons
         cnt[code_id[b]]++;
     }
     if (hipSetDevice(mx->device) != hipSuccess) return ldpc_set_error(LDPC_EDEVICE, "hipSetDevice");
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : mx->stream[0];
+    // NULL = HIP's null stream (ordered with the legacy default stream)
+    hipStream_t s = (hipStream_t)hip_stream;
     // previous call's index uploads must have finished before we rewrite h_idx
     for (int c = 0; c < nc; c++)
         if (mx->pending[c]) {
@@ -142,24 +143,36 @@ extern "C" int ldpc_decode_i8_mixed_async(ldpc_mixed *mx, void *hip_stream, cons
     std::vector<int> fill(nc, 0);
     for (int b = 0; b < batch; b++) mx->h_idx[code_id[b]][fill[code_id[b]]++] = b;
     if (hipEventRecord(mx->fork, s) != hipSuccess) return ldpc_set_error(LDPC_EDEVICE, "event record");
+    // on a failure after some streams were forked: every forked stream still
+    // records its done event (the next call waits for its h_idx upload) and
+    // the caller's stream is joined with all of them before returning
+    auto join_all = [&](int upto, int rc) {
+        for (int c = 0; c <= upto && c < nc; c++) {
+            if (!cnt[c] || !mx->pending[c]) continue;
+            (void)hipEventRecord(mx->done[c], mx->stream[c]);
+            (void)hipStreamWaitEvent(s, mx->done[c], 0);
+        }
+        return rc;
+    };
     for (int c = 0; c < nc; c++) {
         if (!cnt[c]) continue;
         hipStream_t cs = mx->stream[c];
         const int n = mx->n;
-        if (hipStreamWaitEvent(cs, mx->fork, 0) != hipSuccess ||
-            hipMemcpyAsync(mx->d_idx[c], mx->h_idx[c], 4ull * cnt[c], hipMemcpyHostToDevice, cs) != hipSuccess)
-            return ldpc_set_error(LDPC_EDEVICE, "mixed: fork");
+        if (hipStreamWaitEvent(cs, mx->fork, 0) != hipSuccess)
+            return join_all(c - 1, ldpc_set_error(LDPC_EDEVICE, "mixed: fork"));
+        if (hipMemcpyAsync(mx->d_idx[c], mx->h_idx[c], 4ull * cnt[c], hipMemcpyHostToDevice, cs) != hipSuccess)
+            return join_all(c - 1, ldpc_set_error(LDPC_EDEVICE, "mixed: index upload"));
+        mx->pending[c] = true;   // h_idx[c] is in flight from here on
         if (launch_gather_rows(d_llr, mx->d_in[c], mx->d_idx[c], cnt[c], n, cs))
-            return ldpc_set_error(LDPC_EDEVICE, "mixed: gather");
+            return join_all(c, ldpc_set_error(LDPC_EDEVICE, "mixed: gather"));
         int rc = ldpc_decode_i8_async(mx->ctx[c], cs, mx->d_in[c], mx->d_out[c], nullptr,
                                       d_iters_used ? mx->d_its[c] : nullptr, cnt[c], n_iter, p);
-        if (rc != LDPC_OK) return rc;
+        if (rc != LDPC_OK) return join_all(c, rc);
         if (launch_scatter_rows(mx->d_out[c], d_hard, mx->d_idx[c], cnt[c], n, cs) ||
             (d_iters_used && launch_scatter_rows(mx->d_its[c], d_iters_used, mx->d_idx[c], cnt[c], 4, cs)))
-            return ldpc_set_error(LDPC_EDEVICE, "mixed: scatter");
+            return join_all(c, ldpc_set_error(LDPC_EDEVICE, "mixed: scatter"));
         if (hipEventRecord(mx->done[c], cs) != hipSuccess || hipStreamWaitEvent(s, mx->done[c], 0) != hipSuccess)
-            return ldpc_set_error(LDPC_EDEVICE, "mixed: join");
-        mx->pending[c] = true;
+            return join_all(c, ldpc_set_error(LDPC_EDEVICE, "mixed: join"));
     }
     return LDPC_OK;
 }

@@ -25,18 +25,6 @@ import numpy as np
 from . import _lib
 from .codes import Code
 
-_SIDE = {}
-
-
-def _side_stream(device):
-    """One torch side stream per device for launches made while torch is on
-    its default stream (see Decoder._on_stream)."""
-    import torch
-    if device not in _SIDE:
-        _SIDE[device] = torch.cuda.Stream(device=device)
-    return _SIDE[device]
-
-
 class Decoder:
     """One C-ABI decoder context (device scratch for ``max_batch`` codewords)."""
 
@@ -113,23 +101,14 @@ class Decoder:
         return None if t is None else C.c_void_p(t.data_ptr())
 
     @staticmethod
-    def _on_stream(stream, launch):
-        """Run launch(hip_stream) ordered after, and before, the work on
-        torch's current stream.  The C-ABI maps a NULL stream to the
-        context's own non-blocking stream, which does not synchronise with
-        the legacy default stream; so when torch is on its default stream
-        (handle 0) the launch goes to a side stream fenced both ways."""
-        if stream is not None:
-            return launch(C.c_void_p(stream))
-        import torch
-        cur = torch.cuda.current_stream()
-        if cur.cuda_stream != 0:
-            return launch(C.c_void_p(cur.cuda_stream))
-        side = _side_stream(cur.device)
-        side.wait_stream(cur)
-        r = launch(C.c_void_p(side.cuda_stream))
-        cur.wait_stream(side)
-        return r
+    def _on_stream(stream, launch, device=None):
+        """Run launch(hip_stream) on `stream`, default torch's current stream
+        of `device`.  Handle 0 (torch's default stream) is HIP's null stream,
+        which the C-ABI keeps as is (ordered with the legacy default stream)."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(device).cuda_stream
+        return launch(C.c_void_p(stream) if stream else None)
 
     def decode_i8_device(self, llr, hard, n_iter, params=None, soft=None, iters_used=None, stream=None):
         B = llr.shape[0]
@@ -137,7 +116,7 @@ class Decoder:
         p = params or _lib.default_params()
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_decode_i8_async(
             self._ctx, s, self._ptr(llr), self._ptr(hard), self._ptr(soft), self._ptr(iters_used), B, n_iter,
-            C.byref(p))))
+            C.byref(p))), self.device)
 
     def decode_f32_device(self, llr, hard, n_iter, params=None, soft=None, iters_used=None, stream=None):
         B = llr.shape[0]
@@ -145,16 +124,16 @@ class Decoder:
         p = params or _lib.default_params(algo=_lib.ALGO_MS)
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_decode_f32_async(
             self._ctx, s, self._ptr(llr), self._ptr(hard), self._ptr(soft), self._ptr(iters_used), B, n_iter,
-            C.byref(p))))
+            C.byref(p))), self.device)
 
     def awgn_i8_device(self, llr, first_cw, seed, table, codeword=None, stream=None):
         t = np.ascontiguousarray(table, dtype=np.uint32)
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_awgn_i8_async(
-            self._ctx, s, self._ptr(llr), llr.shape[0], first_cw, seed, t.ctypes.data, self._ptr(codeword))))
+            self._ctx, s, self._ptr(llr), llr.shape[0], first_cw, seed, t.ctypes.data, self._ptr(codeword))), self.device)
 
     def count_errors_device(self, hard, k, counts, ref=None, stream=None):
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_count_errors_async(
-            self._ctx, s, self._ptr(hard), hard.shape[0], k, self._ptr(ref), self._ptr(counts))))
+            self._ctx, s, self._ptr(hard), hard.shape[0], k, self._ptr(ref), self._ptr(counts))), self.device)
 
     def close(self):
         if getattr(self, "_ctx", None) is not None and _lib._lib is not None:
@@ -176,6 +155,7 @@ class MixedDecoder:
         _lib.check(_lib.lib().ldpc_mixed_create(arr, len(self.codes), device, max_batch, C.byref(h)))
         self._mx = h
         self.n = self.codes[0].n
+        self.device = device
 
     def decode_i8_device(self, llr, hard, code_id, n_iter, params=None, iters_used=None, stream=None):
         """llr/hard: device tensors [B, N]; code_id: host int array [B]."""
@@ -183,7 +163,7 @@ class MixedDecoder:
         p = params or _lib.default_params()
         Decoder._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_decode_i8_mixed_async(
             self._mx, s, Decoder._ptr(llr), Decoder._ptr(hard), Decoder._ptr(iters_used), ids.ctypes.data,
-            ids.size, n_iter, C.byref(p))))
+            ids.size, n_iter, C.byref(p))), self.device)
 
     def close(self):
         if getattr(self, "_mx", None) is not None and _lib._lib is not None:

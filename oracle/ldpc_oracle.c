@@ -260,19 +260,28 @@ typedef struct {
     const oracle_code *h;
     const int8_t *llr;
     uint8_t *hard;
-    int batch, iters, offset, rc;
+    int8_t *soft;
+    int32_t *iters_used;
+    const float *fllr;
+    float *fsoft;
+    int batch, iters, algo, param, early_term, rc;
+    float beta;
 } mt_job;
 
 static void *mt_worker(void *p)
 {
     mt_job *j = (mt_job *)p;
-    j->rc = oracle_decode_i8(j->h, j->llr, j->hard, NULL, j->batch, j->iters, ORACLE_OMS,
-                             j->offset, -127, 127, 31, 0, NULL);
+    if (j->fllr)
+        j->rc = oracle_decode_f32(j->h, j->fllr, j->hard, j->fsoft, j->batch, j->iters, j->algo, j->beta,
+                                  j->early_term, j->iters_used);
+    else
+        j->rc = oracle_decode_i8(j->h, j->llr, j->hard, j->soft, j->batch, j->iters, j->algo, j->param,
+                                 -127, 127, 31, j->early_term, j->iters_used);
     return NULL;
 }
 
-int oracle_decode_i8_mt(const oracle_code *h, const int8_t *llr, uint8_t *hard,
-                        int batch, int iters, int offset, int threads)
+/* split `batch` codewords over `threads` pthreads, contiguous ranges */
+static int run_mt(mt_job proto, int batch, int threads, int n)
 {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
@@ -281,7 +290,14 @@ int oracle_decode_i8_mt(const oracle_code *h, const int8_t *llr, uint8_t *hard,
     int per = (batch + threads - 1) / threads, t = 0;
     for (int s = 0; s < batch; s += per, t++) {
         int cnt = (batch - s < per) ? batch - s : per;
-        jobs[t] = (mt_job){h, llr + (size_t)s * h->n, hard + (size_t)s * h->n, cnt, iters, offset, 0};
+        jobs[t] = proto;
+        jobs[t].batch = cnt;
+        jobs[t].hard = proto.hard + (size_t)s * n;
+        if (proto.llr) jobs[t].llr = proto.llr + (size_t)s * n;
+        if (proto.fllr) jobs[t].fllr = proto.fllr + (size_t)s * n;
+        if (proto.soft) jobs[t].soft = proto.soft + (size_t)s * n;
+        if (proto.fsoft) jobs[t].fsoft = proto.fsoft + (size_t)s * n;
+        if (proto.iters_used) jobs[t].iters_used = proto.iters_used + s;
         pthread_create(&tid[t], NULL, mt_worker, &jobs[t]);
     }
     int rc = 0;
@@ -290,4 +306,27 @@ int oracle_decode_i8_mt(const oracle_code *h, const int8_t *llr, uint8_t *hard,
         rc |= jobs[i].rc;
     }
     return rc;
+}
+
+int oracle_decode_i8_mt(const oracle_code *h, const int8_t *llr, uint8_t *hard,
+                        int batch, int iters, int offset, int threads)
+{
+    mt_job j = {h, llr, hard, NULL, NULL, NULL, NULL, batch, iters, ORACLE_OMS, offset, 0, 0, 0.0f};
+    return run_mt(j, batch, threads, h->n);
+}
+
+int oracle_decode_i8_mt_ex(const oracle_code *h, const int8_t *llr, uint8_t *hard, int8_t *v_out,
+                           int batch, int iters, int algo, int param, int early_term,
+                           int32_t *iters_used, int threads)
+{
+    mt_job j = {h, llr, hard, v_out, iters_used, NULL, NULL, batch, iters, algo, param, early_term, 0, 0.0f};
+    return run_mt(j, batch, threads, h->n);
+}
+
+int oracle_decode_f32_mt(const oracle_code *h, const float *llr, uint8_t *hard, float *v_out,
+                         int batch, int iters, int algo, float beta, int early_term,
+                         int32_t *iters_used, int threads)
+{
+    mt_job j = {h, NULL, hard, NULL, iters_used, llr, v_out, batch, iters, algo, 0, early_term, 0, beta};
+    return run_mt(j, batch, threads, h->n);
 }

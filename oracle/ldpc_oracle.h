@@ -72,6 +72,16 @@ int oracle_syndrome(const oracle_code *h, const uint8_t *hard);
 int oracle_decode_i8_mt(const oracle_code *h, const int8_t *llr, uint8_t *hard,
                         int batch, int iters, int offset, int threads);
 
+/* The same split for oracle_decode_i8 / oracle_decode_f32 with every output
+ * (soft values, early termination, iterations used): tests check whole
+ * BASELINE-sized batches with it, and the float cpu_baseline uses all cores. */
+int oracle_decode_i8_mt_ex(const oracle_code *h, const int8_t *llr, uint8_t *hard, int8_t *v_out,
+                           int batch, int iters, int algo, int param, int early_term,
+                           int32_t *iters_used, int threads);
+int oracle_decode_f32_mt(const oracle_code *h, const float *llr, uint8_t *hard, float *v_out,
+                         int batch, int iters, int algo, float beta, int early_term,
+                         int32_t *iters_used, int threads);
+
 #ifdef __cplusplus
 }
 #endif

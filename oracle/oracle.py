@@ -51,6 +51,10 @@ def lib():
                                        C.c_int, C.c_int, C.c_int, P]
         L.oracle_decode_f32.argtypes = [C.POINTER(_Code), P, P, P, C.c_int, C.c_int, C.c_int, C.c_float, C.c_int, P]
         L.oracle_decode_i8_mt.argtypes = [C.POINTER(_Code), P, P, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.oracle_decode_i8_mt_ex.argtypes = [C.POINTER(_Code), P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             P, C.c_int]
+        L.oracle_decode_f32_mt.argtypes = [C.POINTER(_Code), P, P, P, C.c_int, C.c_int, C.c_int, C.c_float, C.c_int,
+                                           P, C.c_int]
         L.oracle_quantize.argtypes = [P, P, C.c_long, C.c_int, C.c_int, C.c_int]
         L.oracle_quantize.restype = None
         L.oracle_syndrome.argtypes = [C.POINTER(_Code), P]
@@ -69,17 +73,35 @@ class OracleCode:
                        self._ev.ctypes.data_as(C.POINTER(C.c_uint32)))
 
 
+def host_threads():
+    """Threads for the oracle on this host: the CPU share the process may
+    use (the GPU box grants 16 CPUs of a larger machine through its cgroup)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def decode_i8(table, llr, iters, algo=OMS, param=1, var_min=-127, var_max=127, msg_max=31, early_term=False,
-              return_soft=False):
+              return_soft=False, threads=1):
     oc = OracleCode(table)
     llr = np.ascontiguousarray(llr, dtype=np.int8).reshape(-1, table.n)
     B = llr.shape[0]
     hard = np.empty_like(llr, dtype=np.uint8)
     soft = np.empty_like(llr) if return_soft else None
     its = np.empty(B, dtype=np.int32)
-    rc = lib().oracle_decode_i8(C.byref(oc.c), llr.ctypes.data, hard.ctypes.data,
-                                soft.ctypes.data if soft is not None else None, B, iters, algo, param, var_min,
-                                var_max, msg_max, int(early_term), its.ctypes.data)
+    if threads > 1 and var_min == -127 and var_max == 127 and msg_max == 31:
+        rc = lib().oracle_decode_i8_mt_ex(C.byref(oc.c), llr.ctypes.data, hard.ctypes.data,
+                                          soft.ctypes.data if soft is not None else None, B, iters, algo, param,
+                                          int(early_term), its.ctypes.data, threads)
+    else:
+        rc = lib().oracle_decode_i8(C.byref(oc.c), llr.ctypes.data, hard.ctypes.data,
+                                    soft.ctypes.data if soft is not None else None, B, iters, algo, param, var_min,
+                                    var_max, msg_max, int(early_term), its.ctypes.data)
     if rc != 0:
         raise ValueError("oracle rejected parameters")
     if return_soft:
@@ -87,15 +109,19 @@ def decode_i8(table, llr, iters, algo=OMS, param=1, var_min=-127, var_max=127, m
     return hard
 
 
-def decode_f32(table, llr, iters, algo=OMS, beta=0.0, early_term=False):
+def decode_f32(table, llr, iters, algo=OMS, beta=0.0, early_term=False, threads=1):
     oc = OracleCode(table)
     llr = np.ascontiguousarray(llr, dtype=np.float32).reshape(-1, table.n)
     B = llr.shape[0]
     hard = np.empty(llr.shape, dtype=np.uint8)
     soft = np.empty_like(llr)
     its = np.empty(B, dtype=np.int32)
-    rc = lib().oracle_decode_f32(C.byref(oc.c), llr.ctypes.data, hard.ctypes.data, soft.ctypes.data, B, iters,
-                                 algo, beta, int(early_term), its.ctypes.data)
+    if threads > 1:
+        rc = lib().oracle_decode_f32_mt(C.byref(oc.c), llr.ctypes.data, hard.ctypes.data, soft.ctypes.data, B,
+                                        iters, algo, beta, int(early_term), its.ctypes.data, threads)
+    else:
+        rc = lib().oracle_decode_f32(C.byref(oc.c), llr.ctypes.data, hard.ctypes.data, soft.ctypes.data, B, iters,
+                                     algo, beta, int(early_term), its.ctypes.data)
     if rc != 0:
         raise ValueError("oracle rejected parameters")
     return hard, soft, its
