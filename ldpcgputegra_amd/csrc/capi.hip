@@ -10,6 +10,7 @@
 // stream -- created once, not per call as the reference's decode_stream does
 // (code/gpu_fixed/decoder_ms/CGPU_Decoder_MS_SIMD.cu:223-224).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -31,7 +32,7 @@ struct ldpc_ctx {
     int device = 0;
     int max_batch = 0;
     int max_stride = 0;
-    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop, 6 coop2, 7 lds
+    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop, 6 coop2, 7 lds, 8 coop3
     int last_kernel = 0;
     hipStream_t stream = nullptr;
     // device copy of the code
@@ -41,6 +42,7 @@ struct ldpc_ctx {
     Windowed2Code w16{}, w32{};     // windowed2.hip tables, S = 16 and S = 32
     CoopCode coop{};                // coop.hip tables (workgroup-cooperative DVB-S2 path)
     CoopCode coop2{};               // coop2.hip tables (packed-pair variant, D0 = 7)
+    CoopCode coop3{};               // coop3.hip tables (pre + post slab waves, i16 chain, D0 = 7)
     LdsCode lds{};                  // lds.hip tables (LDS-resident short-code decoder)
     // scratch (lazily sized)
     void *d_V = nullptr;
@@ -57,6 +59,12 @@ struct ldpc_ctx {
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
 };
+
+static int getenv_int(const char *name, int def)
+{
+    const char *e = getenv(name);
+    return (e && *e) ? atoi(e) : def;
+}
 
 static int ensure(void **p, size_t *have, size_t need)
 {
@@ -120,6 +128,7 @@ extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ld
     if ((rc = windowed2_upload(h, 32, 1, &c->w32)) != LDPC_OK) return fail(rc);
     if ((rc = coop_upload(h, &c->coop)) != LDPC_OK) return fail(rc);
     if ((rc = coop2_upload(h, &c->coop2)) != LDPC_OK) return fail(rc);
+    if ((rc = coop3_upload(h, &c->coop3)) != LDPC_OK) return fail(rc);
     if ((rc = lds_upload(h, &c->lds)) != LDPC_OK) return fail(rc);
     *out = c;
     return LDPC_OK;
@@ -135,6 +144,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     windowed2_free(&c->w32);
     coop_free(&c->coop);
     coop_free(&c->coop2);
+    coop_free(&c->coop3);
     lds_free(&c->lds);
     for (auto &pr : c->events) {
         (void)hipEventDestroy(pr.first);
@@ -161,9 +171,10 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 7) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 7");
+    if (!c || k < 0 || k > 8) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 8");
     if ((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid) ||
-        (k == 5 && !c->coop.valid) || (k == 6 && !c->coop2.valid) || (k == 7 && !c->lds.valid))
+        (k == 5 && !c->coop.valid) || (k == 6 && !c->coop2.valid) || (k == 7 && !c->lds.valid) ||
+        (k == 8 && !c->coop3.valid))
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
     c->kernel = k;
     return LDPC_OK;
@@ -235,7 +246,8 @@ static int check_params(const ldpc_ctx *c, int batch, int n_iter, const ldpc_par
 
 // kernel family for this call: 1 generic, 2 windowed, 3 windowed2/S16,
 // 4 windowed2/S32, 5 coop (workgroup-cooperative), 6 coop2 (packed pairs),
-// 7 lds (LDS-resident short codes, int8 and float)
+// 7 lds (LDS-resident short codes, int8 and float), 8 coop3 (slab waves doing
+// pre + post, i16 chain)
 static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, int stride)
 {
     const bool ld = lds_applicable(c->code, c->lds, is_float);
@@ -245,6 +257,7 @@ static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, i
     const bool w2 = windowed2_params_ok(p);
     const bool co = c->coop.valid && coop_params_ok(p);
     const bool co2 = c->coop2.valid && coop2_params_ok(p) && coop2_stride_ok(stride);
+    const bool co3 = c->coop3.valid && coop3_params_ok(p) && coop2_stride_ok(stride);
     switch (c->kernel) {
     case 1: return 1;
     case 2: return w1 ? 2 : -1;
@@ -252,7 +265,9 @@ static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, i
     case 4: return (w2 && c->w32.valid) ? 4 : -1;
     case 5: return co ? 5 : -1;
     case 6: return co2 ? 6 : -1;
+    case 8: return co3 ? 8 : -1;
     default:
+        if (co3 && getenv_int("LDPC_DEFAULT_COOP3", 0)) return 8;
         if (co2) return 6;
         if (co) return 5;
         if (w2 && c->w16.valid) return 3;
@@ -304,7 +319,7 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     }
     const bool win = kern >= 2;
     // + a sink row / sink words for the masked stores of the coop kernel
-    const size_t msg_need = (kern == 6 ? coop2_msg_bytes(h, stride)
+    const size_t msg_need = (kern == 6 || kern == 8 ? coop2_msg_bytes(h, stride)
                              : win    ? windowed_msg_bytes(h, stride)
                                       : (size_t)h->e * stride * esz) +
                             4096;
@@ -341,13 +356,13 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     L.early = p->early_term;
     L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
     L.iters_used = d_iters;
-    if ((kern == 5 || kern == 6) && p->early_term) {
+    if ((kern == 5 || kern == 6 || kern == 8) && p->early_term) {
         // live u8 | bad u32 | iterations used i32 (when the caller passed none)
         if ((rc = ensure(&c->d_early, &c->early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
         L.bad = (uint32_t *)c->d_early;
         if (!L.iters_used) L.iters_used = (int32_t *)((char *)c->d_early + (size_t)stride * 4);
         L.live = (uint8_t *)c->d_early + (size_t)stride * 8;
-        if (kern == 6) {
+        if (kern == 6 || kern == 8) {
             if ((rc = ensure(&c->d_Vs, &c->Vs_bytes, (size_t)(h->n + 1) * stride)) != LDPC_OK) return rc;
             L.Vs = (int8_t *)c->d_Vs;
         }
@@ -358,7 +373,8 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
         HIP_TRY(hipEventCreate(&ev1));
         HIP_TRY(hipEventRecord(ev0, s));
     }
-    int lr = kern == 6   ? launch_coop2(L, c->coop2, s)
+    int lr = kern == 8   ? launch_coop3(L, c->coop3, s)
+             : kern == 6 ? launch_coop2(L, c->coop2, s)
              : kern == 5 ? launch_coop(L, c->coop, s)
              : kern == 4 ? launch_windowed2(L, c->w32, s)
              : kern == 3 ? launch_windowed2(L, c->w16, s)

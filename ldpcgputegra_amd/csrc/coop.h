@@ -53,3 +53,8 @@ bool coop2_stride_ok(int stride);                    // V row pitch fits the buf
 size_t coop2_msg_bytes(const ldpc_code *h, int stride);
 int coop2_upload(const ldpc_code *h, CoopCode *cc);
 int launch_coop2(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
+
+// ---- coop3.hip: slab waves doing pre + post, i16 chain (D0 = 7) ----
+bool coop3_params_ok(const ldpc_params *p);
+int coop3_upload(const ldpc_code *h, CoopCode *cc);
+int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);

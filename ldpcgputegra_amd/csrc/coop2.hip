@@ -46,23 +46,10 @@
 
 #include "coop.h"
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x2 __attribute__((ext_vector_type(2)));
-
-// structured buffer access, address = base + index * stride + offset
-__device__ uint32_t sbuf_load_u32(i32x4 rsrc, int index, int offset, int soffset, int aux)
-    __asm("llvm.amdgcn.struct.buffer.load.i32");
-__device__ void sbuf_store_u16(unsigned short v, i32x4 rsrc, int index, int offset, int soffset, int aux)
-    __asm("llvm.amdgcn.struct.buffer.store.i16");
-__device__ i32x2 sbuf_load_v2(i32x4 rsrc, int index, int offset, int soffset, int aux)
-    __asm("llvm.amdgcn.struct.buffer.load.v2i32");
-__device__ void sbuf_store_v2(i32x2 v, i32x4 rsrc, int index, int offset, int soffset, int aux)
-    __asm("llvm.amdgcn.struct.buffer.store.v2i32");
+#include "pk16.h"
 
 namespace {
 
-constexpr int CW = 16;     // codewords per workgroup
-constexpr int NP = 8;      // codeword pairs per workgroup = lanes per slot
 constexpr int WS_DEFAULT = 3;   // slab waves per role (S = 8 WS checks per window); LDPC_COOP2_WS = 3 | 4
 #ifndef LDPC_COOP2_R
 #define LDPC_COOP2_R 3
@@ -74,102 +61,6 @@ constexpr int KAHEAD = R2 + 2 + DPER;   // ... which is KAHEAD windows ahead of 
 constexpr int TQ = 16;     // window-table slots in LDS (>= KAHEAD + 2)
 constexpr int RING = 8;    // forwarding ring windows (>= R2 + DIST)
 constexpr int NSB = 3;     // pre -> post state buffers (a window's state lives 3 periods)
-constexpr int MREC = 64;   // message bytes per check and workgroup (8 pairs x 8 B)
-
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-// descriptor from wave-uniform values (kernel arguments, block index)
-LDPC_DEV i32x4 buffer_rsrc(const void *base, uint32_t stride, uint32_t records)
-{
-    const uint64_t a = (uint64_t)base;
-    i32x4 r;
-    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-    r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) | (stride << 16)));
-    r.z = __builtin_amdgcn_readfirstlane((int)records);
-    r.w = 0x00020000;
-    return r;
-}
-
-LDPC_DEV s16x2 sv(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
-LDPC_DEV uint32_t us(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
-LDPC_DEV uint32_t pk_sub_sat(uint32_t a, uint32_t b) { return us(__builtin_elementwise_sub_sat(sv(a), sv(b))); }
-LDPC_DEV uint32_t pk_add_sat(uint32_t a, uint32_t b) { return us(__builtin_elementwise_add_sat(sv(a), sv(b))); }
-LDPC_DEV uint32_t pk_max(uint32_t a, uint32_t b) { return us(__builtin_elementwise_max(sv(a), sv(b))); }
-LDPC_DEV uint32_t pk_min(uint32_t a, uint32_t b) { return us(__builtin_elementwise_min(sv(a), sv(b))); }
-LDPC_DEV uint32_t pk_sub(uint32_t a, uint32_t b) { return us(sv(a) - sv(b)); }
-LDPC_DEV uint32_t pk_sra15(uint32_t a) { return us(sv(a) >> (short)15); }
-LDPC_DEV uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
-LDPC_DEV uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) { return __builtin_amdgcn_perm(s0, s1, sel); }
-// hide a value from the optimiser: keeps sign-splat masks as bit masks (v_bfi_b32)
-// instead of per-half compare/select, and constants in VGPRs (no op_sel / literal splits)
-LDPC_DEV uint32_t opaque(uint32_t x)
-{
-    asm volatile("" : "+v"(x));
-    return x;
-}
-LDPC_DEV int hi8(uint32_t x, int h) { return __builtin_amdgcn_sbfe((int)x, 8 + 16 * h, 8); }   // half h's value
-
-constexpr uint32_t RNEG127 = 0x81FF81FFu;   // R(-127) per half
-constexpr uint32_t R127 = 0x7FFF7FFFu;      // R(127)
-constexpr uint32_t R0 = 0x00FF00FFu;        // R(0)
-constexpr uint32_t C510 = 0x01FE01FEu;      // |R(x)| = max(R, 510 - R)
-constexpr uint32_t HIBYTES = 0xFF00FF00u;   // R -> C
-constexpr uint32_t SIGNS = 0x80008000u;
-
-LDPC_DEV uint32_t unpack_v(uint32_t raw, uint32_t sel) { return perm(raw, raw, sel); }   // V dword -> R pair
-LDPC_DEV uint32_t pack_v(uint32_t r) { return perm(r, r, 0x0c0c0301u); }           // R pair -> u16 [b0 b1]
-LDPC_DEV uint32_t abs_r(uint32_t r, uint32_t c510) { return pk_max(r, pk_sub(c510, r)); }
-
-// the packed-math constants, held in VGPRs: as SGPR operands hipcc splats
-// them with op_sel_hi, and gfx950 then needs a wait state before the result
-// is read
-struct PkK {
-    uint32_t neg127, r0, c510, rmm, coff;   // R(-127), R(0), 510, R(msg_max), C(offset) per half
-};
-
-// byte tables [+cst1, -cst1, +cst2, -cst2] of the two codewords of a pair
-struct MsgTab {
-    uint32_t t0, t1;
-};
-LDPC_DEV MsgTab msg_tab(uint32_t MB)
-{
-    const uint32_t p0 = perm(MB, MB, 0x0c010c00u), p1 = perm(MB, MB, 0x0c030c02u);   // (cst1, cst2) as u16
-    return {perm(pk_sub(0u, p0), p0, 0x06020400u), perm(pk_sub(0u, p1), p1, 0x06020400u)};
-}
-
-// old message of edge J (C pair): byte 1 = t0[code0], byte 3 = t1[code1]
-template <int J>
-LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t)
-{
-    uint32_t sh;
-    if constexpr (J <= 4)
-        sh = MA << (8 - 2 * J);
-    else
-        sh = MA >> (2 * J - 8);
-    return perm(t.t1, t.t0, (sh & 0x03000300u) | 0x040c000cu);
-}
-
-// new message of edge J: its code into MA, the new V (R pair) returned
-template <int J>
-LDPC_DEV uint32_t new_msg(uint32_t c, uint32_t a, uint32_t min1, uint32_t k1, uint32_t k2, uint32_t P, uint32_t &MA,
-                          uint32_t neg127)
-{
-    const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));   // -1: a > min1, the edge gets cst2
-    const uint32_t rr = bfi(neq, k2, k1);
-    const uint32_t sgn = pk_sra15(c ^ P);             // -1: the message is negative
-    MA |= (sgn & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
-    return pk_max(pk_add_sat(c, pk_sub(rr ^ sgn, sgn)), neg127);
-}
-
-template <int I, int N, typename F>
-LDPC_DEV void static_for(F &&f)
-{
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
 
 struct Coop2Args {
     int8_t *V;                     // V[n + 1][pitch]; row n is the sink of inactive slots
@@ -461,18 +352,6 @@ LDPC_DEV void chain_steps2(Smem2<D0, WS> &sm, int buf, int c, int &Y, unsigned l
               "v"(q1[i].y));
         if ((k & 3) == 3) *(int4 *)&sm.xin[buf][c][k - 3] = make_int4(xv[0], xv[1], xv[2], xv[3]);
     }
-}
-
-// LDS-DMA: every active lane copies 16 B from gsrc to lds_dst + 16 * lane,
-// without passing through VGPRs (the compiler neither counts nor waits for
-// it: the chain wave waits with an explicit vmcnt)
-LDPC_DEV void dma16(const void *gsrc, uint32_t lds_dst)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_dst)
-                 : "memory");
 }
 
 LDPC_DEV unsigned long long stamp()

@@ -1,0 +1,649 @@
+// coop3.hip -- the DVB-S2 staircase-code decoder, third generation: the
+// BASELINE.json headline path (DVB-S2 r1/2, 50 iterations, int8 OMS).
+// Bit-exact with the reference's CDecoder_OMS_fixed_SSE::decode_8bits
+// (code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:172-546), like coop.hip /
+// coop2.hip, whose window plan (coop_build_plan), message format and
+// packed-pair arithmetic (pk16.h) it shares.  What changes is the workgroup's
+// organisation, built from what bounds coop2 on MI355X:
+//
+// * slab waves do BOTH halves of a check (pre: gather V + old messages,
+//   contributions, min1 / min2 / signs and the chain constants; post: new
+//   messages and V) for the same 8 slots, so a window's state stays in VGPRs
+//   between its pre (period g-1) and its post (period g+1): no pre -> post
+//   LDS round trip (coop2 moved 64 B per lane and period through LDS);
+// * the chain (the serial staircase recurrence, one step per check) runs in
+//   i16: v_pk_mad_i16 evaluates eps*Y + A and eps*Y + B at once, two
+//   v_med3_i16 with op_sel apply the offset dead zone and the [L, H] clamp --
+//   3 dependent instructions per check (coop2: 5), constants from ONE
+//   ds_read_b128 per step; step outputs are written alternately into the low
+//   / high halves of four VGPRs (op_sel dst), so 8 steps' x inputs leave in
+//   one ds_write_b128;
+// * WS = 4 slab waves (S = 32 checks per window) use all four SIMDs; the
+//   chain wave shares one with the highest priority (WS = 3: S = 24, the
+//   chain has a SIMD of its own).
+//
+// Period p (one s_barrier): chain = steps of window p; slab waves = post of
+// window p-1, pre of window p+1, V / message loads of window p+1+R.  The plan
+// (dist 2) keeps windows closer than 3 free of shared information variables;
+// values written 3 .. R+2 windows before a pre are forwarded through the LDS
+// ring as in coop2.
+//
+// The chain recurrence (check i, x edge input Y = V[p_{i-1}]):
+//   V[p_i] = clamp(c_o + eps * sign(c_x) * min(max(|c_x| - off, 0), T), +-127)
+//   c_x = Y - m_x, c_o = V[p_i] - m_o (old messages), eps = sign parity of the
+//   information edges (odd-degree flip included), T = cst(min over them);
+// = med3(med3(eps*Y + A, c_o, eps*Y + B), L, H) with A = c_o - eps*m_x - off,
+//   B = c_o - eps*m_x + off, L = max(c_o - T, -127), H = min(c_o + T, 127).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+#include <vector>
+
+#include "coop.h"
+
+#include "pk16.h"
+
+namespace {
+
+constexpr int D0 = 7, X = D0 - 2;   // first-group check degree, information edges per check
+constexpr int NFW = (X + 1) / 2;    // forwarding-code dwords per record
+constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;
+constexpr int DIST = 2;
+constexpr int DPER = 3;             // a window table's LDS-DMA is waited for DPER periods after its issue
+constexpr int TQ = 16;              // window-table slots in LDS
+
+constexpr int lcm3(int a) { return (a % 3 == 0) ? a : 3 * a; }
+
+template <int WS, int R>
+struct Cfg {
+    static constexpr int S = 8 * WS;                   // checks per window
+    static constexpr int KAHEAD = R + 2 + DPER;        // tables staged KAHEAD windows ahead of the chain
+    static constexpr int RING = (R + 1 <= 4) ? 4 : 8;  // forwarding ring windows (>= R + 1)
+    static constexpr int U = lcm3(R + 1);              // periods unrolled: prefetch slots (R+1) x states (3)
+    static_assert(TQ >= KAHEAD + 2, "table ring");
+};
+
+template <int WS, int R>
+struct alignas(16) Smem3 {
+    static constexpr int S = Cfg<WS, R>::S, RING = Cfg<WS, R>::RING;
+    uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
+    uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
+                                      // codeword 2q + h at [h][q]   (pre -> chain)
+    uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post)
+    uint32_t ring[RING][S][X][NP];    // new V pairs (R form) of the last windows, for forwarding
+};
+
+struct Coop3Args {
+    int8_t *V;                        // V[n + 1][pitch]; row n is the sink of inactive slots
+    uint8_t *Mc;                      // [pitch / 16][mrows][8 pairs][2] u32; row m is the sink
+    const uint32_t *tab;              // [nw][S][RECW] slot records
+    unsigned long long *stamps;       // diagnostic build: [grid][waves][4]
+    const uint8_t *live;              // early termination: [pitch] 0 = converged (NULL: all live)
+    int pitch, G, nw, tail, mrows, n, remap, prio;
+    uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
+};
+
+struct Pf3 {                          // prefetched raw inputs of one window
+    uint32_t v[D0 - 1];               // V dwords (this pair + its neighbour): info edges, then record entry D0-1
+    uint32_t ma, mb;
+};
+
+struct St3 {                          // one window's state from pre to post (R / C pairs)
+    uint32_t c[D0 - 1];               // contributions (info, o); tail: new V
+    uint32_t a[D0 - 1];               // |c| (not clipped: min1 / min2 are, where the constants are made)
+    uint32_t mn1, mn2, sacc, mx;      // min1 / min2 / sign parity over info + o; x-edge old message
+                                      // tail: mn1 = MA, mn2 = MB
+};
+
+LDPC_DEV uint32_t pk_ashr8(uint32_t a) { return us(sv(a) >> (short)8); }
+LDPC_DEV uint32_t pk_add(uint32_t a, uint32_t b) { return us(sv(a) + sv(b)); }
+
+constexpr uint32_t V127 = 0x007F007Fu, VNEG127 = 0xFF81FF81u;   // +-127 per half (value form)
+
+template <int WS, int R>
+struct Slab3 {
+    using SM = Smem3<WS, R>;
+    static constexpr int S = SM::S, RING = SM::RING;
+    SM &sm;
+    const Coop3Args &a;
+    i32x4 vr, mr;                     // V rows of this group (stride pitch), message rows (stride 64)
+    int k, q, tail;
+    uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
+    PkK K;
+
+    LDPC_DEV uint32_t ldv(uint32_t var) const { return sbuf_load_u32(vr, (int)var, 4 * (q >> 1), 0, 0); }
+    LDPC_DEV void stv(uint32_t var, uint32_t r) const
+    {
+#ifdef C3X_NOSTORE   // timing experiment only: results are wrong
+        asm volatile("" ::"v"(pack_v(r)), "v"(var));
+#else
+        sbuf_store_u16((unsigned short)pack_v(r), vr, (int)var, 2 * q, 0, 0);
+#endif
+    }
+
+    // issue the loads of the window in table slot ts
+    LDPC_DEV void prefetch(int ts, Pf3 &pf) const
+    {
+        const uint32_t *r = sm.tab[ts][k];
+        uint32_t var[D0];
+#pragma unroll
+        for (int j = 0; j < D0; j++) var[j] = r[j];
+        const uint32_t meta = r[D0];
+#pragma unroll
+        for (int j = 0; j < X; j++) pf.v[j] = ldv(var[j]);
+        pf.v[X] = ldv(var[D0 - 1]);   // o edge (tail: its last edge, swapped by the upload)
+        const i32x2 m = sbuf_load_v2(mr, (int)(meta & COOP_CHK_MASK), 8 * q, 0, 0);
+        pf.ma = (uint32_t)m.x;
+        pf.mb = (uint32_t)m.y;
+    }
+
+    // V pairs written 3 .. R+2 windows ago replace the loaded ones (per lane)
+    LDPC_DEV void forward(int ts, int g, uint32_t *v) const
+    {
+        const uint32_t *r = sm.tab[ts][k];
+        uint32_t fw[NFW];
+#pragma unroll
+        for (int i = 0; i < NFW; i++) fw[i] = r[D0 + 1 + i];
+#pragma unroll
+        for (int j = 0; j < X; j++) {
+            const uint32_t code = (fw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
+            const int dw = (int)(code >> 9);
+            if (code != COOP_FWD_NONE && g >= dw)
+                v[j] = sm.ring[(g - dw) & (RING - 1)][(code >> 3) & 63][code & 7][q];
+        }
+    }
+
+    // pre of window g (local index u): chain constants -> cst[g & 1], state -> s
+    LDPC_DEV void pre(int g, int u, const Pf3 &pf, St3 &s) const
+    {
+        const int ts = g & (TQ - 1), cb = g & 1;
+        const uint32_t meta = sm.tab[ts][k][D0];
+        uint32_t v[D0 - 1];
+#pragma unroll
+        for (int j = 0; j < D0 - 1; j++) v[j] = unpack_v(pf.v[j], usel);
+        if (__any((meta & COOP_M_FWD) != 0)) forward(ts, g, v);
+        const MsgTab t = msg_tab(pf.mb);
+        const uint32_t MA = pf.ma, neg127 = K.neg127, c510 = K.c510;
+        uint32_t min1 = R127, min2 = R127, sacc = 0;
+        uint32_t A, B, EPS, COV, L, H;
+        if (u != tail) {
+            // first degree group (OMS_fixed_SSE.cpp:201-218); a = |c| here, the
+            // msg_max clip is applied to min1 / min2 (a_j == min1 decides the
+            // same edges either way, and min1 == msg_max implies cst1 == cst2)
+            static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int J = decltype(jc)::value;
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
+                const uint32_t aj = abs_r(c, c510);
+                s.c[J] = c;
+                s.a[J] = aj;
+                sacc ^= c;
+                min2 = pk_max(min1, pk_min(aj, min2));
+                min1 = pk_min(min1, aj);
+            });
+            const uint32_t T = pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0);   // cst over the info edges
+            const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
+            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), neg127);
+            const uint32_t ao = abs_r(cor, c510);
+            s.c[X] = cor;
+            s.a[X] = ao;
+            s.sacc = sacc ^ cor;
+            s.mn2 = pk_max(min1, pk_min(ao, min2));
+            s.mn1 = pk_min(min1, ao);
+            const uint32_t mx = old_msg<X>(MA, t);
+            s.mx = mx;
+            // chain constants in value form (R >> 8, C >> 8), both codewords at once
+            COV = pk_ashr8(cor);
+            const uint32_t TV = pk_ashr8(T), EM = pk_sra15(kb);   // EM: -1 where eps = -1
+            EPS = EM | 0x00010001u;
+            const uint32_t base = pk_sub(COV, pk_sub(pk_ashr8(mx) ^ EM, EM));   // c_o - eps * m_x
+            A = pk_sub(base, a.offp);
+            B = pk_add(base, a.offp);
+            L = pk_max(pk_sub(COV, TV), VNEG127);
+            H = pk_min(pk_add(COV, TV), V127);
+        } else {
+            // the tail check (later degree group: a = |min(c, msg_max)|,
+            // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
+            static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int J = decltype(jc)::value;
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
+                const uint32_t aj = abs_r(pk_min(c, K.rmm), c510);
+                s.c[J] = c;
+                s.a[J] = aj;
+                sacc ^= c;
+                min2 = pk_max(min1, pk_min(aj, min2));
+                min1 = pk_min(min1, aj);
+            });
+            const uint32_t k1 = pk_min(pk_max(pk_sub(min2, K.coff), K.r0), K.rmm) & HIBYTES;
+            const uint32_t k2 = pk_min(pk_max(pk_sub(min1, K.coff), K.r0), K.rmm) & HIBYTES;
+            const uint32_t P = (sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u)) & SIGNS;
+            uint32_t MAn = 0;
+            static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int J = decltype(jc)::value;
+                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn, neg127);
+            });
+            s.mx = 0;
+            s.sacc = 0;
+            s.mn1 = MAn;
+            s.mn2 = perm(k2, k1, 0x07030501u);
+            // the chain passes V[p_0] (the tail's last edge) on: A = B = c_o = L = H = y
+            const uint32_t Y = pk_ashr8(s.c[X]);
+            A = B = COV = L = H = Y;
+            EPS = 0;
+        }
+        if (!(meta & COOP_M_ACT)) {   // pass-through slot: Y' = Y
+            A = B = COV = 0;
+            EPS = 0x00010001u;
+            L = VNEG127;
+            H = V127;
+        }
+        // per codeword records: (A, B), (eps, c_o), (L, H) as i16 pairs
+        uint4 r0, r1;
+        r0.x = perm(B, A, 0x05040100u);
+        r1.x = perm(B, A, 0x07060302u);
+        r0.y = perm(COV, EPS, 0x05040100u);
+        r1.y = perm(COV, EPS, 0x07060302u);
+        r0.z = perm(H, L, 0x05040100u);
+        r1.z = perm(H, L, 0x07060302u);
+        r0.w = r1.w = 0;
+        sm.cst[cb][k][0][q] = r0;
+        sm.cst[cb][k][1][q] = r1;
+    }
+
+    // post of window g (local index u): x inputs from xo[g & 1]
+    LDPC_DEV void post(int g, int u, const St3 &s) const
+    {
+        const int ts = g & (TQ - 1), xb = g & 1, rs = g & (RING - 1);
+        const uint32_t *r = sm.tab[ts][k];
+        uint32_t var[D0];
+#pragma unroll
+        for (int j = 0; j < D0; j++) var[j] = r[j];
+        const uint32_t meta = r[D0];
+        const unsigned short *xs = (const unsigned short *)&sm.xo[xb][k >> 3][0];
+        const uint32_t x0 = xs[(2 * q) * 8 + (k & 7)], x1 = xs[(2 * q + 1) * 8 + (k & 7)];
+        const uint32_t xr = perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127] -> R pair
+        uint32_t MA, MB;
+        if (u != tail) {
+            const uint32_t cx = pk_max(pk_sub_sat(xr, s.mx), K.neg127);
+            const uint32_t ax = abs_r(cx, K.c510);
+            const uint32_t sacc = s.sacc ^ cx;
+            const uint32_t min2 = pk_max(s.mn1, pk_min(ax, s.mn2)), min1 = pk_min(ax, s.mn1);
+            const uint32_t k1 = pk_max(pk_sub(pk_min(min2, K.rmm), K.coff), K.r0) & HIBYTES;
+            const uint32_t k2 = pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0) & HIBYTES;
+            const uint32_t P = (sacc ^ ((D0 & 1) ? SIGNS : 0u)) & SIGNS;
+            MA = 0;
+            static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int J = decltype(jc)::value;
+                const uint32_t vn = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
+                stv(var[J], vn);
+                sm.ring[rs][k][J][q] = vn;
+            });
+            stv(var[X], new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127));
+            // the o edge: message bits only (the next check rewrites V[o] as its x edge)
+            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
+            MB = perm(k2, k1, 0x07030501u);
+        } else {
+            static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int J = decltype(jc)::value;
+                stv(var[J], s.c[J]);
+                sm.ring[rs][k][J][q] = s.c[J];
+            });
+            stv(var[D0 - 1], s.c[X]);   // the tail's last edge (record entries X, D0-1 swapped)
+            stv(var[X], xr);            // V of the last group-0 check's o edge: only the chain had it
+            MA = s.mn1;
+            MB = s.mn2;
+        }
+        i32x2 m;
+        m.x = (int)MA;
+        m.y = (int)MB;
+        sbuf_store_v2(m, mr, (int)(meta & COOP_CHK_MASK), 8 * q, 0, 0);
+    }
+};
+
+// one chain step: input = half IH of xin, output = half OH of xout (the other
+// half of xout is kept); c = (K1, K2, K3) of the step
+#define C3_STEP_SAME(XW, KV)                                                                   \
+    asm volatile("v_pk_mad_i16 %1, %0, %3, %2 op_sel:[0,0,0] op_sel_hi:[0,0,1]\n\t"           \
+                 "v_med3_i16 %1, %1, %3, %1 op_sel:[0,1,1,0]\n\t"                             \
+                 "v_med3_i16 %0, %1, %4, %4 op_sel:[0,0,1,1]"                                 \
+                 : "+v"(XW), "=&v"(tmp)                                                       \
+                 : "v"((KV).x), "v"((KV).y), "v"((KV).z))
+#define C3_STEP_CROSS(XI, XO, KV)                                                              \
+    asm volatile("v_pk_mad_i16 %1, %2, %4, %3 op_sel:[1,0,0] op_sel_hi:[1,0,1]\n\t"           \
+                 "v_med3_i16 %1, %1, %4, %1 op_sel:[0,1,1,0]\n\t"                             \
+                 "v_med3_i16 %0, %1, %5, %5 op_sel:[0,0,1,0]"                                 \
+                 : "+v"(XO), "=&v"(tmp)                                                       \
+                 : "v"(XI), "v"((KV).x), "v"((KV).y), "v"((KV).z))
+
+// the chain steps of one window (lanes 0..15 = codewords).  Step k's input
+// sits at position k % 8 of w (w[i] low / high half = positions 2i, 2i+1) and
+// its output goes to position k+1, so after step 8j+6 positions 0..7 hold the
+// inputs of steps 8j .. 8j+7: the x inputs post needs, stored as one uint4.
+template <int WS, int R>
+LDPC_DEV void chain_window3(Smem3<WS, R> &sm, int buf, int c, uint32_t (&w)[4])
+{
+    constexpr int S = Cfg<WS, R>::S, NB = S / 8;
+    const uint4 *cp = &sm.cst[buf][0][c & 1][c >> 1];
+    constexpr int KST = 2 * NP;       // uint4 between steps
+    uint4 kq[2][8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) kq[0][i] = cp[i * KST];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        if (b + 1 < NB) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) kq[(b + 1) & 1][i] = cp[((b + 1) * 8 + i) * KST];
+        }
+        uint32_t tmp;
+        C3_STEP_SAME(w[0], kq[b & 1][0]);          // pos 0 -> 1
+        C3_STEP_CROSS(w[0], w[1], kq[b & 1][1]);   // pos 1 -> 2
+        C3_STEP_SAME(w[1], kq[b & 1][2]);          // 2 -> 3
+        C3_STEP_CROSS(w[1], w[2], kq[b & 1][3]);   // 3 -> 4
+        C3_STEP_SAME(w[2], kq[b & 1][4]);          // 4 -> 5
+        C3_STEP_CROSS(w[2], w[3], kq[b & 1][5]);   // 5 -> 6
+        C3_STEP_SAME(w[3], kq[b & 1][6]);          // 6 -> 7
+        sm.xo[buf][b][c] = make_uint4(w[0], w[1], w[2], w[3]);
+        C3_STEP_CROSS(w[3], w[0], kq[b & 1][7]);   // 7 -> 0 (the next block's first input)
+    }
+}
+
+LDPC_DEV unsigned long long stamp3()
+{
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+// Waves 0 .. WS-1: slab waves (slots 8w .. 8w+7), wave WS: the chain.
+template <int WS, int R, bool STAMP>
+__global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
+{
+    using SM = Smem3<WS, R>;
+    using CF = Cfg<WS, R>;
+    constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U;
+    __shared__ SM sm;
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int nb = gridDim.x, id = blockIdx.x;
+    const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
+    const int G = a.G;
+    if (G == 0) return;
+    if (a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
+    unsigned long long sA = 0, sB = 0, sC = 0, sD = 0, t0 = 0, tx = 0;
+    auto write_stamps = [&]() {
+        if (STAMP && lane == 0) {
+            unsigned long long *o = a.stamps + ((size_t)id * (WS + 1) + wave) * 4;
+            o[0] = sA;
+            o[1] = sB | (sC << 32);
+            o[2] = (stamp3() - t0) | (sD << 32);
+            o[3] = (unsigned long long)G | (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) << 32;
+        }
+    };
+
+    if (wave == WS) {
+        // ------------------------------------------------------------ chain wave
+        if (a.prio) __builtin_amdgcn_s_setprio(3);
+        constexpr int NCH = S * RECW / 4;   // 16-B chunks per window table
+        constexpr int CPL = (NCH + 63) / 64;
+        static_assert(CPL * DPER <= 63, "table staging");
+        const int c = lane & 15;
+        auto stage = [&](int u, int slot) {
+            const uint4 *src = (const uint4 *)(a.tab + (size_t)u * S * RECW);
+            const uint32_t dst = (uint32_t)(uintptr_t)&sm.tab[slot][0][0];
+#pragma unroll
+            for (int i = 0; i < CPL; i++)
+                if (lane + 64 * i < NCH) dma16(src + 64 * i + lane, dst + 1024 * i);
+        };
+        for (int w = 0; w < KAHEAD; w++) stage(w % a.nw, w);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t w4[4] = {0, 0, 0, 0};
+        w4[0] = (uint32_t)(int)a.V[(size_t)a.tab[X] * (uint32_t)a.pitch + (uint32_t)(wg * CW + c)] & 0xFFFFu;
+        int un = KAHEAD % a.nw;
+        __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 in LDS
+        __syncthreads();   // prologue 2: constants of window 0 in LDS
+        const bool cl = lane < CW;
+        if (STAMP) t0 = stamp3();
+        for (int p = 0; p <= G; p++) {
+            if (STAMP) tx = stamp3();
+            if (p < G && cl) chain_window3<WS, R>(sm, p & 1, c, w4);
+            if (STAMP) sB += stamp3() - tx;
+            stage(un, (p + KAHEAD) & (TQ - 1));
+            un = (un + 1 == a.nw) ? 0 : un + 1;
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPL * DPER) : "memory");
+            if (STAMP) sA += stamp3() - tx;
+            __syncthreads();
+        }
+        write_stamps();
+        return;
+    }
+
+    // ------------------------------------------------------------ slab waves
+    Slab3<WS, R> sl{sm,
+                    a,
+                    buffer_rsrc(a.V + (size_t)wg * CW, (uint32_t)a.pitch, (uint32_t)(a.n + 1)),
+                    buffer_rsrc(a.Mc + (size_t)wg * a.mrows * MREC, (uint32_t)MREC, (uint32_t)a.mrows),
+                    8 * wave + (lane >> 3),
+                    lane & 7,
+                    a.tail,
+                    0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
+                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)}};
+    auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
+    __syncthreads();   // prologue 1: tables in LDS
+    Pf3 pf[R + 1];
+    St3 st[3];
+#pragma unroll
+    for (int i = 0; i <= R; i++) sl.prefetch(i, pf[i]);   // nw > R + 3
+    sl.pre(0, 0, pf[0], st[0]);
+    // nothing in flight when the period loop is entered: hipcc's waitcnt
+    // insertion merges the loop-entry state with the back-edge state, and the
+    // prologue's just-issued loads would make every period wait for its own
+    // loads (measured: the period took 2x)
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    __syncthreads();   // prologue 2
+    if (STAMP) t0 = stamp3();
+    int uA = a.nw - 1;   // local index of window p-1
+    int uB = 1 % a.nw;   // local index of window p+1
+    // period p: post of window p-1 (state st[(p-1) % 3]), loads of window
+    // p+1+R into pf[(p+R+1) % (R+1)], pre of window p+1 from pf[(p+1) % (R+1)].
+    // The main loop runs only periods that do all three (1 <= p <= G-2) with
+    // no branch around any memory operation: hipcc's waitcnt insertion counts
+    // the vector memory operations of the path with the fewest, so a
+    // skippable post (its stores) made every pre wait for its own period's
+    // loads.  The edge periods run guarded outside the loop.
+    auto period = [&](auto sc, auto guarded, int p) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc)::value;   // p % U
+        constexpr bool GU = decltype(guarded)::value;
+        if (STAMP) tx = stamp3();
+        if (!GU || p + 1 < G) sl.prefetch((p + 1 + R) & (TQ - 1), pf[(s + R + 1) % (R + 1)]);
+        unsigned long long t1 = 0, t2 = 0;
+        if (STAMP) t1 = stamp3();
+        if (!GU || p >= 1) sl.post(p - 1, uA, st[(s + 2) % 3]);
+        if (STAMP) t2 = stamp3();
+        if (!GU || p + 1 < G) sl.pre(p + 1, uB, pf[(s + 1) % (R + 1)], st[(s + 1) % 3]);
+        if (STAMP) {
+            const unsigned long long t3 = stamp3();
+            sA += t3 - tx;
+            sB += t1 - tx;
+            sC += t2 - t1;
+            sD += t3 - t2;
+        }
+        __syncthreads();
+        next(uA);
+        next(uB);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    period(std::integral_constant<int, 0>{}, T{}, 0);
+    int p = 1;
+    // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U
+    for (; p + U - 1 <= G - 2; p += U)
+        static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
+            period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, F{}, p + decltype(jc)::value);
+        });
+    // the rest (at most U + 1 periods: p .. G), guarded
+    static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
+        if (p + decltype(jc)::value <= G)
+            period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
+    });
+    write_stamps();
+}
+
+__global__ void fill_iters3_k(int batch, int32_t *iters_used, int iters)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < batch) iters_used[b] = iters;
+}
+
+int env_int3(const char *name, int def)
+{
+    const char *e = getenv(name);
+    return (e && *e) ? atoi(e) : def;
+}
+
+// diagnostic build (LDPC_COOP3_STAMP=1): per-period cycles of each wave role
+template <int WS>
+void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
+{
+    constexpr int nwaves = WS + 1;
+    std::vector<unsigned long long> h((size_t)grid * nwaves * 4);
+    if (hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    double slab = 0, slab_max = 0, chain = 0, chain_steps = 0, total = 0, pf = 0, po = 0, pr = 0;
+    for (int b = 0; b < grid; b++)
+        for (int w = 0; w < nwaves; w++) {
+            const unsigned long long *o = &h[((size_t)b * nwaves + w) * 4];
+            const double G = (o[3] & 0xffffffffu) ? (double)(o[3] & 0xffffffffu) : 1.0;
+            if (w < WS) {
+                slab += o[0] / G;
+                slab_max = std::max(slab_max, o[0] / G);
+                pf += (o[1] & 0xffffffffu) / G;
+                po += (o[1] >> 32) / G;
+                pr += (o[2] >> 32) / G;
+            } else {
+                chain += o[0] / G;
+                chain_steps += (o[1] & 0xffffffffu) / G;
+            }
+            total += (o[2] & 0xffffffffu) / G;
+        }
+    fprintf(stderr,
+            "coop3 stamps [cycles per period]: total %.0f | slab %.0f (max %.0f; prefetch %.0f, post %.0f, pre %.0f) | "
+            "chain %.0f (steps %.0f)\n",
+            total / (grid * nwaves), slab / (grid * WS), slab_max, pf / (grid * WS), po / (grid * WS), pr / (grid * WS),
+            chain / grid, chain_steps / grid);
+}
+
+template <int WS, int R>
+int launch_wsr(const Coop3Args &a, int grid, bool stamped, hipStream_t s)
+{
+    constexpr int threads = 64 * (WS + 1);
+    if (stamped)
+        hipLaunchKernelGGL((coop3_decode<WS, R, true>), dim3(grid), dim3(threads), 0, s, a);
+    else
+        hipLaunchKernelGGL((coop3_decode<WS, R, false>), dim3(grid), dim3(threads), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace
+
+bool coop3_params_ok(const ldpc_params *p) { return coop_params_ok(p); }
+
+int coop3_upload(const ldpc_code *h, CoopCode *cc)
+{
+    *cc = CoopCode{};
+    if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return LDPC_OK;
+    const int ws = env_int3("LDPC_COOP3_WS", 4);
+    const int r = env_int3("LDPC_COOP3_R", 2);
+    if ((ws != 3 && ws != 4) || (r != 2 && r != 5))
+        return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 3 | 4 and LDPC_COOP3_R 2 | 5");
+    const int S = 8 * ws;
+    CoopPlan pl;
+    if (coop_build_plan(h, S, r, DIST, RECW, pl, true) != 0) return LDPC_OK;
+    const int nw = (int)pl.first.size();
+    for (int u = 0; u < nw; u++)
+        for (int k = 0; k < S; k++) {
+            uint32_t *rec = &pl.tab[((size_t)u * S + k) * RECW];
+            if (k >= pl.count[u]) {   // inactive slot: sink V row n, sink message row m, no flags
+                for (int j = 0; j < D0; j++) rec[j] = (uint32_t)h->n;
+                rec[D0] = (uint32_t)h->m;
+            } else if (u == pl.tail) {
+                std::swap(rec[X], rec[D0 - 1]);   // prefetch always loads record entry D0-1
+            }
+        }
+    if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop3 tables");
+    if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        coop_free(cc);
+        return ldpc_set_error(LDPC_EDEVICE, "coop3 table upload");
+    }
+    cc->valid = 1;
+    cc->d0 = D0;
+    cc->S = S;
+    cc->R = r;
+    cc->nw = nw;
+    cc->tail = pl.tail;
+    cc->n_fwd = pl.n_fwd;
+    return LDPC_OK;
+}
+
+static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
+                              hipStream_t s);
+
+int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
+{
+    if (!cc.valid || !coop2_stride_ok(L.stride)) return -1;
+    if (L.early) {
+        // one launch per iteration; converged codewords keep iterating inside
+        // live workgroups, so their V is snapshot when they converge and
+        // merged back at the end (L.Vs), as coop2
+        if (!L.Vs || coop_early_begin(L, s)) return -1;
+        for (int it = 0; it < L.iters; it++)
+            if (launch_coop3_iters(L, cc, 1, L.live, s) || coop_early_after_iter(L, it, s)) return -1;
+        return coop_early_end(L, s);
+    }
+    if (L.iters_used)
+        hipLaunchKernelGGL(fill_iters3_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used,
+                           L.iters);
+    return launch_coop3_iters(L, cc, L.iters, nullptr, s);
+}
+
+static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
+                              hipStream_t s)
+{
+    Coop3Args a{};
+    a.live = live;
+    a.V = (int8_t *)L.V;
+    a.Mc = (uint8_t *)L.msg;
+    a.tab = cc.d_tab;
+    a.pitch = L.stride;
+    a.G = cc.nw * iters;
+    a.nw = cc.nw;
+    a.tail = cc.tail;
+    a.mrows = L.m + 1;
+    a.n = L.n;
+    a.rmm = (uint32_t)(L.msg_max * 256 + 255) * 0x00010001u;
+    a.coff = (uint32_t)(L.param * 256) * 0x00010001u;
+    a.offp = (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
+    a.prio = env_int3("LDPC_COOP3_PRIO", 1);
+    const int grid = L.stride / CW;
+    a.remap = (grid % 8) == 0;
+    const int ws = cc.S / 8;
+    const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0;
+    if (stamped) {
+        const size_t bytes = (size_t)grid * (ws + 1) * 4 * sizeof(unsigned long long);
+        if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
+        (void)hipMemsetAsync(a.stamps, 0, bytes, s);
+    }
+    int rc;
+    if (ws == 4)
+        rc = cc.R == 5 ? launch_wsr<4, 5>(a, grid, stamped, s) : launch_wsr<4, 2>(a, grid, stamped, s);
+    else
+        rc = cc.R == 5 ? launch_wsr<3, 5>(a, grid, stamped, s) : launch_wsr<3, 2>(a, grid, stamped, s);
+    if (stamped) {
+        if (rc == 0) (ws == 4 ? report_stamps3<4>(a.stamps, grid, s) : report_stamps3<3>(a.stamps, grid, s));
+        (void)hipFree(a.stamps);
+    }
+    return rc;
+}

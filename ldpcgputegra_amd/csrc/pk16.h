@@ -1,0 +1,141 @@
+// pk16.h -- packed 16-bit helpers shared by the packed-pair DVB-S2 kernels
+// (coop2.hip, coop3.hip): two codewords per lane, one per 16-bit half.
+//
+// An int8 value x sits in a half as R(x) = 256 x + 255 (value in the high
+// byte, low byte all ones) and a message m as C(m) = 256 m.  Then
+// R(x) - C(m) = R(x - m), R(x) + C(m) = R(x + m) and the i16 saturation
+// 0x7FFF is R(127): the reference's _mm_subs_epi8 / _mm_adds_epi8 upper clamp
+// (code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:201-254) for free.
+// |x| = max(R, 510 - R) stays in R form; min / max / compares are monotone.
+#pragma once
+#include <type_traits>
+
+#include "kernels_common.h"
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+// structured buffer access, address = base + index * stride + offset
+__device__ uint32_t sbuf_load_u32(i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.load.i32");
+__device__ void sbuf_store_u16(unsigned short v, i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.store.i16");
+__device__ i32x2 sbuf_load_v2(i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.load.v2i32");
+__device__ void sbuf_store_v2(i32x2 v, i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.store.v2i32");
+
+namespace {
+
+constexpr int CW = 16;     // codewords per workgroup
+constexpr int NP = 8;      // codeword pairs per workgroup = lanes per slot
+constexpr int MREC = 64;   // message bytes per check and workgroup (8 pairs x 8 B)
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// descriptor from wave-uniform values (kernel arguments, block index)
+LDPC_DEV i32x4 buffer_rsrc(const void *base, uint32_t stride, uint32_t records)
+{
+    const uint64_t a = (uint64_t)base;
+    i32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) | (stride << 16)));
+    r.z = __builtin_amdgcn_readfirstlane((int)records);
+    r.w = 0x00020000;
+    return r;
+}
+
+LDPC_DEV s16x2 sv(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+LDPC_DEV uint32_t us(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+LDPC_DEV uint32_t pk_sub_sat(uint32_t a, uint32_t b) { return us(__builtin_elementwise_sub_sat(sv(a), sv(b))); }
+LDPC_DEV uint32_t pk_add_sat(uint32_t a, uint32_t b) { return us(__builtin_elementwise_add_sat(sv(a), sv(b))); }
+LDPC_DEV uint32_t pk_max(uint32_t a, uint32_t b) { return us(__builtin_elementwise_max(sv(a), sv(b))); }
+LDPC_DEV uint32_t pk_min(uint32_t a, uint32_t b) { return us(__builtin_elementwise_min(sv(a), sv(b))); }
+LDPC_DEV uint32_t pk_sub(uint32_t a, uint32_t b) { return us(sv(a) - sv(b)); }
+LDPC_DEV uint32_t pk_sra15(uint32_t a) { return us(sv(a) >> (short)15); }
+LDPC_DEV uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+LDPC_DEV uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) { return __builtin_amdgcn_perm(s0, s1, sel); }
+// hide a value from the optimiser: keeps sign-splat masks as bit masks (v_bfi_b32)
+// instead of per-half compare/select, and constants in VGPRs (no op_sel / literal splits)
+LDPC_DEV uint32_t opaque(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+LDPC_DEV int hi8(uint32_t x, int h) { return __builtin_amdgcn_sbfe((int)x, 8 + 16 * h, 8); }   // half h's value
+
+constexpr uint32_t RNEG127 = 0x81FF81FFu;   // R(-127) per half
+constexpr uint32_t R127 = 0x7FFF7FFFu;      // R(127)
+constexpr uint32_t R0 = 0x00FF00FFu;        // R(0)
+constexpr uint32_t C510 = 0x01FE01FEu;      // |R(x)| = max(R, 510 - R)
+constexpr uint32_t HIBYTES = 0xFF00FF00u;   // R -> C
+constexpr uint32_t SIGNS = 0x80008000u;
+
+LDPC_DEV uint32_t unpack_v(uint32_t raw, uint32_t sel) { return perm(raw, raw, sel); }   // V dword -> R pair
+LDPC_DEV uint32_t pack_v(uint32_t r) { return perm(r, r, 0x0c0c0301u); }           // R pair -> u16 [b0 b1]
+LDPC_DEV uint32_t abs_r(uint32_t r, uint32_t c510) { return pk_max(r, pk_sub(c510, r)); }
+
+// the packed-math constants, held in VGPRs: as SGPR operands hipcc splats
+// them with op_sel_hi, and gfx950 then needs a wait state before the result
+// is read
+struct PkK {
+    uint32_t neg127, r0, c510, rmm, coff;   // R(-127), R(0), 510, R(msg_max), C(offset) per half
+};
+
+// byte tables [+cst1, -cst1, +cst2, -cst2] of the two codewords of a pair
+struct MsgTab {
+    uint32_t t0, t1;
+};
+LDPC_DEV MsgTab msg_tab(uint32_t MB)
+{
+    const uint32_t p0 = perm(MB, MB, 0x0c010c00u), p1 = perm(MB, MB, 0x0c030c02u);   // (cst1, cst2) as u16
+    return {perm(pk_sub(0u, p0), p0, 0x06020400u), perm(pk_sub(0u, p1), p1, 0x06020400u)};
+}
+
+// old message of edge J (C pair): byte 1 = t0[code0], byte 3 = t1[code1]
+template <int J>
+LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t)
+{
+    uint32_t sh;
+    if constexpr (J <= 4)
+        sh = MA << (8 - 2 * J);
+    else
+        sh = MA >> (2 * J - 8);
+    return perm(t.t1, t.t0, (sh & 0x03000300u) | 0x040c000cu);
+}
+
+// new message of edge J: its code into MA, the new V (R pair) returned
+template <int J>
+LDPC_DEV uint32_t new_msg(uint32_t c, uint32_t a, uint32_t min1, uint32_t k1, uint32_t k2, uint32_t P, uint32_t &MA,
+                          uint32_t neg127)
+{
+    const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));   // -1: a > min1, the edge gets cst2
+    const uint32_t rr = bfi(neq, k2, k1);
+    const uint32_t sgn = pk_sra15(c ^ P);             // -1: the message is negative
+    MA |= (sgn & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
+    return pk_max(pk_add_sat(c, pk_sub(rr ^ sgn, sgn)), neg127);
+}
+
+template <int I, int N, typename F>
+LDPC_DEV void static_for(F &&f)
+{
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// LDS-DMA: every active lane copies 16 B from gsrc to lds_dst + 16 * lane,
+// without passing through VGPRs (the compiler neither counts nor waits for
+// it: the chain wave waits with an explicit vmcnt)
+LDPC_DEV void dma16(const void *gsrc, uint32_t lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+}  // namespace

@@ -43,7 +43,8 @@ class Decoder:
         """0 = auto, 1 = generic (per-edge messages), 2 = windowed, 3/4 =
         windowed2 (S = 16/32), 5 = workgroup-cooperative DVB-S2 kernel, 6 = its
         packed-pair variant (two codewords per lane; DVB-S2 r1/2, early termination by per-iteration launches),
-        7 = LDS-resident short-code kernel (int8 and float)."""
+        7 = LDS-resident short-code kernel (int8 and float), 8 = coop3 (slab waves
+        doing pre + post, i16 chain; the DVB-S2 r1/2 default)."""
         _lib.check(_lib.lib().ldpc_ctx_set_kernel(self._ctx, int(kernel)))
 
     @property
@@ -62,7 +63,7 @@ class Decoder:
         _lib.check(_lib.lib().ldpc_ctx_kernel_time(self._ctx, C.byref(ms), C.byref(n), int(reset)))
         return ms.value, n.value
 
-    KERNEL_NAMES = {0: "none", 1: "generic", 2: "windowed", 3: "windowed2_s16", 4: "windowed2_s32", 5: "coop", 6: "coop2", 7: "lds"}
+    KERNEL_NAMES = {0: "none", 1: "generic", 2: "windowed", 3: "windowed2_s16", 4: "windowed2_s32", 5: "coop", 6: "coop2", 7: "lds", 8: "coop3"}
 
     @property
     def last_kernel(self):

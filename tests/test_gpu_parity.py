@@ -31,7 +31,7 @@ def kernels_for(code):
     """Kernel families that can run this code: 1 generic, 2 windowed,
     3 windowed2 (S=16), 4 windowed2 (S=32), 5 coop (workgroup-cooperative),
     6 coop2 (its packed-pair variant, first-group degree 7), 7 lds (LDS-resident
-    short codes)."""
+    short codes), 8 coop3 (slab waves doing pre + post, i16 chain)."""
     ks = [1]
     c = Code(code)
     if c.plan_info()["windowed"]:
@@ -42,6 +42,8 @@ def kernels_for(code):
         ks.append(5)
     if c.coop_plan(24, 3) is not None and c.max_deg == 7:
         ks.append(6)
+    if c.coop_plan(32, 2, 2) is not None and c.max_deg == 7:
+        ks.append(8)
     if c.layer_info()["lds_i8"]:
         ks.append(7)
     return ks
@@ -259,7 +261,7 @@ def test_dvbs2_full_batch_vs_reference():
     s1 = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
     h2 = torch.empty_like(h1)
     dec.decode_i8_device(llr, h1, 50, soft=s1)
-    assert dec.last_kernel == "coop2"
+    assert dec.last_kernel in ("coop2", "coop3")
     dec.decode_i8_device(llr[:1000], h2[:1000], 50)           # ragged shard
     dec.decode_i8_device(llr[1000:], h2[1000:], 50)
     torch.cuda.synchronize()
@@ -280,15 +282,16 @@ def test_dvbs2_full_batch_vs_reference():
     assert np.array_equal(s1.cpu().numpy()[sel], ref_soft)
 
 
+@pytest.mark.parametrize("kernel", [6, 8])
 @pytest.mark.parametrize("batch,ebn0", [(40, 1.1), (64, 1.1), (1024, 1.0)])
-def test_coop2_early_termination_vs_oracle(batch, ebn0):
+def test_coop2_early_termination_vs_oracle(batch, ebn0, kernel):
     """coop2 (kernel 6) with early termination on whole and partial
     workgroups and, at batch 1024 (grid 64), with the XCD block remap on, as
     bench.py --mixed runs it: hard decisions, soft output and iterations used
     all equal the oracle's (syndrome after every iteration)."""
     torch = _torch()
     t = load_table("dvbs2_r1_2")
-    dec = decoder("dvbs2_r1_2", 6, max(64, batch))
+    dec = decoder("dvbs2_r1_2", kernel, max(64, batch))
     sigma = channel.sigma_from_ebn0(ebn0, t.k_info / t.n)
     llr = channel.awgn_i8_host(t.n, batch, seed=batch + 5, table=channel.i8_table(sigma))
     thr = O.host_threads()
@@ -301,7 +304,7 @@ def test_coop2_early_termination_vs_oracle(batch, ebn0):
         dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, 50, params=default_params(early_term=1),
                              soft=d_soft, iters_used=d_its)
         torch.cuda.synchronize()
-        assert dec.last_kernel == "coop2"
+        assert dec.last_kernel == {6: "coop2", 8: "coop3"}[kernel]
         assert np.array_equal(d_its.cpu().numpy(), ref_its), rep
         assert np.array_equal(d_soft.cpu().numpy(), ref_soft), rep
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard), rep
