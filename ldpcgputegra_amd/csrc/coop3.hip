@@ -44,34 +44,47 @@
 
 #include "pk16.h"
 
+__device__ void sbuf_store_v4(i32x4 v, i32x4 rsrc, int index, int offset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.store.v4i32");
+
 namespace {
 
 constexpr int D0 = 7, X = D0 - 2;   // first-group check degree, information edges per check
 constexpr int NFW = (X + 1) / 2;    // forwarding-code dwords per record
 constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;
-constexpr int DIST = 2;
 constexpr int DPER = 3;             // a window table's LDS-DMA is waited for DPER periods after its issue
 constexpr int TQ = 16;              // window-table slots in LDS
-
-constexpr int lcm3(int a) { return (a % 3 == 0) ? a : 3 * a; }
 
 template <int WS, int R>
 struct Cfg {
     static constexpr int S = 8 * WS;                   // checks per window
     static constexpr int KAHEAD = R + 2 + DPER;        // tables staged KAHEAD windows ahead of the chain
-    static constexpr int RING = (R + 1 <= 4) ? 4 : 8;  // forwarding ring windows (>= R + 1)
-    static constexpr int U = lcm3(R + 1);              // periods unrolled: prefetch slots (R+1) x states (3)
-    static_assert(TQ >= KAHEAD + 2, "table ring");
+    static constexpr int NI = R + 1;                   // LDS-DMA input windows in flight per slab wave
+    static constexpr int NS = R + 1 < 3 ? 3 : R + 1;   // window states in VGPRs (pre at p-1, post at p+1)
+    static constexpr int U = NS;                       // periods unrolled (multiple of NI and NS)
+    static constexpr int NR = (R + 1 <= 4) ? 4 : 8;    // staged-output windows (forwarding reads up to R + 2 later)
+    static constexpr int CHW = WS >= 3 ? 3 : WS;       // the chain wave (waves go to SIMDs 0,2,1,3,0,2,1: wave 3
+                                                       // has a SIMD of its own for WS = 3 and WS = 6)
+    static constexpr int NB = S / 8, NB1 = (NB + 1) / 2;   // chain blocks of 8 steps, before the mid barrier
+    static_assert(TQ >= KAHEAD + 2, "table ring: a window's records are read until its stores");
+    static_assert(U % NI == 0 && U % NS == 0, "unroll");
 };
 
 template <int WS, int R>
 struct alignas(16) Smem3 {
-    static constexpr int S = Cfg<WS, R>::S, RING = Cfg<WS, R>::RING;
+    using CF = Cfg<WS, R>;
+    static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
     uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
     uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post)
-    uint32_t ring[RING][S][X][NP];    // new V pairs (R form) of the last windows, for forwarding
+    struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA:
+        uint4 a[8][8];                //   [slot][0..5] V rows (info edges, record entry D0-1), [6..7] message 0..31 B
+        uint4 b[8][2];                //   [slot][0..1] message 32..63 B
+    } in[WS][NI];
+    uint4 stg[NR][S][8];              // new V of a window, [slot][record entry] x 16 codewords (int8): the V
+                                      // stores' staging and the forwarding ring
+    uint4 mst[WS][8][4];              // new messages of a window per slab wave, [slot] x 64 B
 };
 
 struct Coop3Args {
@@ -80,13 +93,8 @@ struct Coop3Args {
     const uint32_t *tab;              // [nw][S][RECW] slot records
     unsigned long long *stamps;       // diagnostic build: [grid][waves][4]
     const uint8_t *live;              // early termination: [pitch] 0 = converged (NULL: all live)
-    int pitch, G, nw, tail, mrows, n, remap, prio;
+    int pitch, G, nw, tail, mrows, n, remap, prio, slab_prio;
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
-};
-
-struct Pf3 {                          // prefetched raw inputs of one window
-    uint32_t v[D0 - 1];               // V dwords (this pair + its neighbour): info edges, then record entry D0-1
-    uint32_t ma, mb;
 };
 
 struct St3 {                          // one window's state from pre to post (R / C pairs)
@@ -101,73 +109,118 @@ LDPC_DEV uint32_t pk_add(uint32_t a, uint32_t b) { return us(sv(a) + sv(b)); }
 
 constexpr uint32_t V127 = 0x007F007Fu, VNEG127 = 0xFF81FF81u;   // +-127 per half (value form)
 
+// what a period reads from LDS, issued together at its start
+struct PreIn {
+    uint32_t v[D0 - 1];               // raw V dwords (info edges, entry D0-1)
+    uint32_t ma, mb;                  // old message record of this pair
+    uint4 mf;                         // record words D0 .. D0+3: meta, forwarding codes
+};
+struct StIn {                         // the stores of window p-2
+    uint4 vd, md;                     // staged V row piece (16 codewords), message piece
+    uint32_t row, chk;                // record entry q of the slot, its meta
+};
+struct PfIn {                         // the LDS-DMA gathers of window p+1+R
+    uint32_t rv, chk2;
+};
+
 template <int WS, int R>
 struct Slab3 {
     using SM = Smem3<WS, R>;
-    static constexpr int S = SM::S, RING = SM::RING;
+    static constexpr int S = SM::S, NR = SM::NR;
     SM &sm;
     const Coop3Args &a;
-    i32x4 vr, mr;                     // V rows of this group (stride pitch), message rows (stride 64)
-    int k, q, tail;
+    i32x4 vr, mr;                     // V rows of this group (stride pitch), message rows in 16-B units
+    int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
     uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
     PkK K;
+    // per-lane constants of the LDS-DMA gathers (lane (kl, j): j < 6 a V row, j >= 6 a message piece)
+    const char *g1base, *g2base;
+    uint32_t g1mul, g1mask, recsel;
+    uint32_t vrd, mrd;                // byte offsets of this lane's V dword / message pair in an In record
 
-    LDPC_DEV uint32_t ldv(uint32_t var) const { return sbuf_load_u32(vr, (int)var, 4 * (q >> 1), 0, 0); }
-    LDPC_DEV void stv(uint32_t var, uint32_t r) const
+    // ---- reads
+    LDPC_DEV void read_pre(int g, int ib, PreIn &in) const
     {
-#ifdef C3X_NOSTORE   // timing experiment only: results are wrong
-        asm volatile("" ::"v"(pack_v(r)), "v"(var));
-#else
-        sbuf_store_u16((unsigned short)pack_v(r), vr, (int)var, 2 * q, 0, 0);
-#endif
+        const char *inb = (const char *)&sm.in[w][ib];
+#pragma unroll
+        for (int j = 0; j < D0 - 1; j++) in.v[j] = *(const uint32_t *)(inb + vrd + 16 * j);
+        const uint2 mm = *(const uint2 *)(inb + mrd);
+        in.ma = mm.x;
+        in.mb = mm.y;
+        in.mf = *(const uint4 *)&sm.tab[g & (TQ - 1)][k][D0];
+    }
+    LDPC_DEV void read_st(int g, StIn &in) const
+    {
+        in.vd = sm.stg[g % NR][k][q];
+        in.md = sm.mst[w][kl][q & 3];
+        in.row = sm.tab[g & (TQ - 1)][k][q];
+        in.chk = sm.tab[g & (TQ - 1)][k][D0] & COOP_CHK_MASK;
+    }
+    LDPC_DEV void read_pf(int g, PfIn &in) const
+    {
+        in.rv = sm.tab[g & (TQ - 1)][k][recsel] & g1mask;
+        in.chk2 = sm.tab[g & (TQ - 1)][8 * w + ((lane >> 1) & 7)][D0] & COOP_CHK_MASK;
+    }
+    LDPC_DEV uint32_t read_x(int g) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
+    {
+        const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][k >> 3][0];
+        const uint32_t x0 = xs[(2 * q) * 8 + (k & 7)], x1 = xs[(2 * q + 1) * 8 + (k & 7)];
+        return perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127]
     }
 
-    // issue the loads of the window in table slot ts
-    LDPC_DEV void prefetch(int ts, Pf3 &pf) const
+    // ---- memory operations at the end of a period
+    // lane (kl, c): record entry c's 16 codewords (c < 6, the tail 7) and
+    // message piece c (c < 4) of its wave's slot kl
+    LDPC_DEV void stores(const StIn &in, bool tl) const
     {
-        const uint32_t *r = sm.tab[ts][k];
-        uint32_t var[D0];
-#pragma unroll
-        for (int j = 0; j < D0; j++) var[j] = r[j];
-        const uint32_t meta = r[D0];
-#pragma unroll
-        for (int j = 0; j < X; j++) pf.v[j] = ldv(var[j]);
-        pf.v[X] = ldv(var[D0 - 1]);   // o edge (tail: its last edge, swapped by the upload)
-        const i32x2 m = sbuf_load_v2(mr, (int)(meta & COOP_CHK_MASK), 8 * q, 0, 0);
-        pf.ma = (uint32_t)m.x;
-        pf.mb = (uint32_t)m.y;
+        if (q < (tl ? D0 : D0 - 1)) sbuf_store_v4(__builtin_bit_cast(i32x4, in.vd), vr, (int)in.row, 0, 0, 0);
+        if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
+    }
+    LDPC_DEV void gathers(const PfIn &in, int ib) const
+    {
+        const uint32_t base = (uint32_t)(uintptr_t)&sm.in[w][ib];
+        dma16(g1base + (size_t)in.rv * g1mul, base);
+        if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + (uint32_t)sizeof(sm.in[0][0].a));
     }
 
-    // V pairs written 3 .. R+2 windows ago replace the loaded ones (per lane)
-    LDPC_DEV void forward(int ts, int g, uint32_t *v) const
+    // V pairs written 2 .. R+2 windows ago replace the loaded ones (per
+    // lane): all five reads issued together, unused ones from the lane's own
+    // stage slot, then selected
+    LDPC_DEV void forward(int g, const uint4 &mf, uint32_t *v) const
     {
-        const uint32_t *r = sm.tab[ts][k];
-        uint32_t fw[NFW];
-#pragma unroll
-        for (int i = 0; i < NFW; i++) fw[i] = r[D0 + 1 + i];
+        const uint32_t fw[3] = {mf.y, mf.z, mf.w};
+        static_assert(NFW == 3 && (NR & (NR - 1)) == 0, "record layout, ring size");
+        const char *sbase = (const char *)&sm.stg[0][0][0];
+        uint32_t val[X];
+        bool use[X];
 #pragma unroll
         for (int j = 0; j < X; j++) {
             const uint32_t code = (fw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
             const int dw = (int)(code >> 9);
-            if (code != COOP_FWD_NONE && g >= dw)
-                v[j] = sm.ring[(g - dw) & (RING - 1)][(code >> 3) & 63][code & 7][q];
+            use[j] = code != COOP_FWD_NONE && g >= dw;
+            const uint32_t off = ((uint32_t)(g - dw) & (NR - 1)) * (uint32_t)sizeof(sm.stg[0]) +
+                                 ((code >> 3) & 63) * (uint32_t)sizeof(sm.stg[0][0]) + (code & 7) * 16u;
+            val[j] = *(const unsigned short *)(sbase + (use[j] ? off : 0u) + 2 * q);
         }
+#pragma unroll
+        for (int j = 0; j < X; j++)
+            if (use[j]) v[j] = perm(val[j], val[j], 0x010d000du);
     }
 
-    // pre of window g (local index u): chain constants -> cst[g & 1], state -> s
-    LDPC_DEV void pre(int g, int u, const Pf3 &pf, St3 &s) const
+    // pre of window g: chain constants -> cst[g & 1], state -> s
+    template <bool TL>
+    LDPC_DEV void pre(int g, const PreIn &in, St3 &s) const
     {
-        const int ts = g & (TQ - 1), cb = g & 1;
-        const uint32_t meta = sm.tab[ts][k][D0];
+        const uint32_t meta = in.mf.x;
         uint32_t v[D0 - 1];
 #pragma unroll
-        for (int j = 0; j < D0 - 1; j++) v[j] = unpack_v(pf.v[j], usel);
-        if (__any((meta & COOP_M_FWD) != 0)) forward(ts, g, v);
-        const MsgTab t = msg_tab(pf.mb);
-        const uint32_t MA = pf.ma, neg127 = K.neg127, c510 = K.c510;
+        for (int j = 0; j < D0 - 1; j++) v[j] = unpack_v(in.v[j], usel);
+        if (__any((meta & COOP_M_FWD) != 0)) forward(g, in.mf, v);
+        const MsgTab t = msg_tab(in.mb);
+        const uint32_t MA = in.ma, neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
         uint32_t A, B, EPS, COV, L, H;
-        if (u != tail) {
+        if constexpr (!TL) {
             // first degree group (OMS_fixed_SSE.cpp:201-218); a = |c| here, the
             // msg_max clip is applied to min1 / min2 (a_j == min1 decides the
             // same edges either way, and min1 == msg_max implies cst1 == cst2)
@@ -246,24 +299,19 @@ struct Slab3 {
         r0.z = perm(H, L, 0x05040100u);
         r1.z = perm(H, L, 0x07060302u);
         r0.w = r1.w = 0;
+        const int cb = g & 1;
         sm.cst[cb][k][0][q] = r0;
         sm.cst[cb][k][1][q] = r1;
     }
 
-    // post of window g (local index u): x inputs from xo[g & 1]
-    LDPC_DEV void post(int g, int u, const St3 &s) const
+    // post of window g (x inputs xr): new V pairs -> stg[g % NR], messages ->
+    // mst[w]; they leave in the stores of the same period
+    template <bool TL>
+    LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
     {
-        const int ts = g & (TQ - 1), xb = g & 1, rs = g & (RING - 1);
-        const uint32_t *r = sm.tab[ts][k];
-        uint32_t var[D0];
-#pragma unroll
-        for (int j = 0; j < D0; j++) var[j] = r[j];
-        const uint32_t meta = r[D0];
-        const unsigned short *xs = (const unsigned short *)&sm.xo[xb][k >> 3][0];
-        const uint32_t x0 = xs[(2 * q) * 8 + (k & 7)], x1 = xs[(2 * q + 1) * 8 + (k & 7)];
-        const uint32_t xr = perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127] -> R pair
+        unsigned short *st = (unsigned short *)&sm.stg[g % NR][k][0];   // [entry][8 pairs] u16
         uint32_t MA, MB;
-        if (u != tail) {
+        if constexpr (!TL) {
             const uint32_t cx = pk_max(pk_sub_sat(xr, s.mx), K.neg127);
             const uint32_t ax = abs_r(cx, K.c510);
             const uint32_t sacc = s.sacc ^ cx;
@@ -272,31 +320,28 @@ struct Slab3 {
             const uint32_t k2 = pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0) & HIBYTES;
             const uint32_t P = (sacc ^ ((D0 & 1) ? SIGNS : 0u)) & SIGNS;
             MA = 0;
+            uint32_t nv[X + 1];
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t vn = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
-                stv(var[J], vn);
-                sm.ring[rs][k][J][q] = vn;
+                nv[J] = pack_v(new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127));
             });
-            stv(var[X], new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127));
+            nv[X] = pack_v(new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127));
             // the o edge: message bits only (the next check rewrites V[o] as its x edge)
             (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
             MB = perm(k2, k1, 0x07030501u);
+#pragma unroll
+            for (int j = 0; j <= X; j++) st[j * 8 + q] = (unsigned short)nv[j];
         } else {
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                stv(var[J], s.c[J]);
-                sm.ring[rs][k][J][q] = s.c[J];
+                st[J * 8 + q] = (unsigned short)pack_v(s.c[J]);
             });
-            stv(var[D0 - 1], s.c[X]);   // the tail's last edge (record entries X, D0-1 swapped)
-            stv(var[X], xr);            // V of the last group-0 check's o edge: only the chain had it
+            st[X * 8 + q] = (unsigned short)pack_v(xr);               // V of the last group-0 check's o edge
+            st[(D0 - 1) * 8 + q] = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
             MA = s.mn1;
             MB = s.mn2;
         }
-        i32x2 m;
-        m.x = (int)MA;
-        m.y = (int)MB;
-        sbuf_store_v2(m, mr, (int)(meta & COOP_CHK_MASK), 8 * q, 0, 0);
+        *(uint2 *)((char *)&sm.mst[w][kl][0] + 8 * q) = make_uint2(MA, MB);
     }
 };
 
@@ -319,18 +364,17 @@ struct Slab3 {
 // sits at position k % 8 of w (w[i] low / high half = positions 2i, 2i+1) and
 // its output goes to position k+1, so after step 8j+6 positions 0..7 hold the
 // inputs of steps 8j .. 8j+7: the x inputs post needs, stored as one uint4.
-template <int WS, int R>
+template <int WS, int R, int B0, int B1>
 LDPC_DEV void chain_window3(Smem3<WS, R> &sm, int buf, int c, uint32_t (&w)[4])
 {
-    constexpr int S = Cfg<WS, R>::S, NB = S / 8;
     const uint4 *cp = &sm.cst[buf][0][c & 1][c >> 1];
     constexpr int KST = 2 * NP;       // uint4 between steps
     uint4 kq[2][8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) kq[0][i] = cp[i * KST];
+    for (int i = 0; i < 8; i++) kq[B0 & 1][i] = cp[(B0 * 8 + i) * KST];
 #pragma unroll
-    for (int b = 0; b < NB; b++) {
-        if (b + 1 < NB) {
+    for (int b = B0; b < B1; b++) {
+        if (b + 1 < B1) {
 #pragma unroll
             for (int i = 0; i < 8; i++) kq[(b + 1) & 1][i] = cp[((b + 1) * 8 + i) * KST];
         }
@@ -356,13 +400,13 @@ LDPC_DEV unsigned long long stamp3()
     return t;
 }
 
-// Waves 0 .. WS-1: slab waves (slots 8w .. 8w+7), wave WS: the chain.
+// Wave CHW: the chain; the others: slab waves (slab index w: slots 8w .. 8w+7).
 template <int WS, int R, bool STAMP>
 __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 {
     using SM = Smem3<WS, R>;
     using CF = Cfg<WS, R>;
-    constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U;
+    constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U, CHW = CF::CHW, NB = CF::NB, NB1 = CF::NB1;
     __shared__ SM sm;
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -383,7 +427,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         }
     };
 
-    if (wave == WS) {
+    if (wave == CHW) {
         // ------------------------------------------------------------ chain wave
         if (a.prio) __builtin_amdgcn_s_setprio(3);
         constexpr int NCH = S * RECW / 4;   // 16-B chunks per window table
@@ -408,7 +452,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         if (STAMP) t0 = stamp3();
         for (int p = 0; p <= G; p++) {
             if (STAMP) tx = stamp3();
-            if (p < G && cl) chain_window3<WS, R>(sm, p & 1, c, w4);
+            if (p < G && cl) chain_window3<WS, R, 0, NB1>(sm, p & 1, c, w4);
+            __syncthreads();   // mid-period barrier (the slab waves' posts -> pres)
+            if (p < G && cl) chain_window3<WS, R, NB1, NB>(sm, p & 1, c, w4);
             if (STAMP) sB += stamp3() - tx;
             stage(un, (p + KAHEAD) & (TQ - 1));
             un = (un + 1 == a.nw) ? 0 : un + 1;
@@ -421,54 +467,116 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     }
 
     // ------------------------------------------------------------ slab waves
+    const int sw = wave - (wave > CHW ? 1 : 0);   // slab index
+    // the second-dispatched half of the slab waves loses VALU arbitration to
+    // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
+    // "Two waves per SIMD", item 4)
+    if (a.slab_prio && wave > CHW) __builtin_amdgcn_s_setprio(1);
+    const int kl = lane >> 3, q = lane & 7;
+    const char *Vb = (const char *)a.V + (size_t)wg * CW;
+    const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
     Slab3<WS, R> sl{sm,
                     a,
-                    buffer_rsrc(a.V + (size_t)wg * CW, (uint32_t)a.pitch, (uint32_t)(a.n + 1)),
-                    buffer_rsrc(a.Mc + (size_t)wg * a.mrows * MREC, (uint32_t)MREC, (uint32_t)a.mrows),
-                    8 * wave + (lane >> 3),
-                    lane & 7,
+                    buffer_rsrc(Vb, (uint32_t)a.pitch, (uint32_t)(a.n + 1)),
+                    buffer_rsrc(Mb, 16u, (uint32_t)a.mrows * 4u),
+                    8 * sw + kl,
+                    kl,
+                    q,
+                    sw,
+                    lane,
                     a.tail,
                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
-                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)}};
+                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
+                    q < 6 ? Vb : Mb + (q - 6) * 16,
+                    Mb + (2 + (lane & 1)) * 16,
+                    q < 6 ? (uint32_t)a.pitch : (uint32_t)MREC,
+                    q < 6 ? 0xFFFFFFFFu : COOP_CHK_MASK,
+                    (uint32_t)(q < X ? q : (q == X ? D0 - 1 : D0)),
+                    (uint32_t)(kl * 128 + 4 * (q >> 1)),
+                    (uint32_t)(q < 4 ? kl * 128 + (6 + (q >> 1)) * 16 + (q & 1) * 8
+                                     : 1024 + kl * 32 + ((q >> 1) - 2) * 16 + (q & 1) * 8)};
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
+    constexpr int NI = CF::NI, NS = CF::NS;
     __syncthreads();   // prologue 1: tables in LDS
-    Pf3 pf[R + 1];
-    St3 st[3];
+    St3 st[NS];
+    {
+        PfIn pi;
 #pragma unroll
-    for (int i = 0; i <= R; i++) sl.prefetch(i, pf[i]);   // nw > R + 3
-    sl.pre(0, 0, pf[0], st[0]);
-    // nothing in flight when the period loop is entered: hipcc's waitcnt
-    // insertion merges the loop-entry state with the back-edge state, and the
-    // prologue's just-issued loads would make every period wait for its own
-    // loads (measured: the period took 2x)
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+        for (int i = 0; i <= R; i++) {   // window i -> in[w][i]   (nw > R + 3)
+            sl.read_pf(i, pi);
+            sl.gathers(pi, i);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PreIn in;
+        sl.read_pre(0, 0, in);
+        if (a.tail == 0)
+            sl.template pre<true>(0, in, st[0]);
+        else
+            sl.template pre<false>(0, in, st[0]);
+    }
     __syncthreads();   // prologue 2
     if (STAMP) t0 = stamp3();
-    int uA = a.nw - 1;   // local index of window p-1
-    int uB = 1 % a.nw;   // local index of window p+1
-    // period p: post of window p-1 (state st[(p-1) % 3]), loads of window
-    // p+1+R into pf[(p+R+1) % (R+1)], pre of window p+1 from pf[(p+1) % (R+1)].
-    // The main loop runs only periods that do all three (1 <= p <= G-2) with
-    // no branch around any memory operation: hipcc's waitcnt insertion counts
-    // the vector memory operations of the path with the fewest, so a
-    // skippable post (its stores) made every pre wait for its own period's
-    // loads.  The edge periods run guarded outside the loop.
+    int uA = a.nw - 1;   // local index of window p-1 (post, stores)
+    int uB = 1 % a.nw;   // local index of window p+1 (pre)
+    // Period p, phase 1: post of window p-1 (state st[(p-1) % NS]) -> staged
+    // outputs.  Mid barrier: the plan only keeps neighbouring windows free of
+    // shared information variables (dist 1), so a value window p+1 reads may
+    // have been written by the post just done; it is forwarded from the stage.
+    // Phase 2: pre of window p+1 (inputs in[w][(p+1) % NI], -> st[(p+1) % NS]),
+    // then the two stores of window p-1 and the two LDS-DMA gathers of window
+    // p+1+R into in[w][(p+1+R) % NI].  The gathers of window p+1 were the
+    // last vector memory operations of period p-R, followed by 4 in each
+    // later period: in the main loop (1 <= p <= G-2, every period does
+    // everything, no tail window) vmcnt(4(R-1)) covers them.
     auto period = [&](auto sc, auto guarded, int p) __attribute__((always_inline)) {
         constexpr int s = decltype(sc)::value;   // p % U
         constexpr bool GU = decltype(guarded)::value;
         if (STAMP) tx = stamp3();
-        if (!GU || p + 1 < G) sl.prefetch((p + 1 + R) & (TQ - 1), pf[(s + R + 1) % (R + 1)]);
-        unsigned long long t1 = 0, t2 = 0;
+        const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
+        const bool fast = !GU && uA != a.tail && uB != a.tail;
+        if (fast) {
+            sl.template post<false>(p - 1, sl.read_x(p - 1), st[(s + NS - 1) % NS]);
+        } else if (dpo) {
+            if (uA == a.tail)
+                sl.template post<true>(p - 1, sl.read_x(p - 1), st[(s + NS - 1) % NS]);
+            else
+                sl.template post<false>(p - 1, sl.read_x(p - 1), st[(s + NS - 1) % NS]);
+        }
+        unsigned long long t1 = 0;
         if (STAMP) t1 = stamp3();
-        if (!GU || p >= 1) sl.post(p - 1, uA, st[(s + 2) % 3]);
-        if (STAMP) t2 = stamp3();
-        if (!GU || p + 1 < G) sl.pre(p + 1, uB, pf[(s + 1) % (R + 1)], st[(s + 1) % 3]);
+        __syncthreads();
+        if (STAMP) sC += stamp3() - t1;
+        if constexpr (GU)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1)) : "memory");
+        PreIn in;
+        StIn si;
+        PfIn pi;
+        if (fast) {
+            sl.read_st(p - 1, si);
+            sl.read_pre(p + 1, (s + 1) % NI, in);
+            sl.read_pf(p + 1 + R, pi);
+            sl.template pre<false>(p + 1, in, st[(s + 1) % NS]);
+            sl.stores(si, false);
+            sl.gathers(pi, (s + R + 1) % NI);
+        } else {
+            if (dpo) sl.read_st(p - 1, si);
+            if (dpr) {
+                sl.read_pre(p + 1, (s + 1) % NI, in);
+                sl.read_pf(p + 1 + R, pi);
+                if (uB == a.tail)
+                    sl.template pre<true>(p + 1, in, st[(s + 1) % NS]);
+                else
+                    sl.template pre<false>(p + 1, in, st[(s + 1) % NS]);
+            }
+            if (dpo) sl.stores(si, uA == a.tail);
+            if (dpr) sl.gathers(pi, (s + R + 1) % NI);
+        }
         if (STAMP) {
             const unsigned long long t3 = stamp3();
             sA += t3 - tx;
             sB += t1 - tx;
-            sC += t2 - t1;
-            sD += t3 - t2;
         }
         __syncthreads();
         next(uA);
@@ -503,37 +611,32 @@ int env_int3(const char *name, int def)
     return (e && *e) ? atoi(e) : def;
 }
 
-// diagnostic build (LDPC_COOP3_STAMP=1): per-period cycles of each wave role
+// diagnostic build (LDPC_COOP3_STAMP=1): per-period cycles of each wave
 template <int WS>
 void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
 {
-    constexpr int nwaves = WS + 1;
+    constexpr int nwaves = WS + 1, CHW = WS >= 3 ? 3 : WS;
     std::vector<unsigned long long> h((size_t)grid * nwaves * 4);
     if (hipStreamSynchronize(s) != hipSuccess ||
         hipMemcpy(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
         return;
-    double slab = 0, slab_max = 0, chain = 0, chain_steps = 0, total = 0, pf = 0, po = 0, pr = 0;
+    // slab: busy (both phases, without the end barrier), phase 1, mid-barrier wait
+    // chain: steps + staging (without the end barrier), steps
+    std::vector<double> busy(nwaves, 0.0), ph1(nwaves, 0.0), mid(nwaves, 0.0);
+    double total = 0;
     for (int b = 0; b < grid; b++)
         for (int w = 0; w < nwaves; w++) {
             const unsigned long long *o = &h[((size_t)b * nwaves + w) * 4];
             const double G = (o[3] & 0xffffffffu) ? (double)(o[3] & 0xffffffffu) : 1.0;
-            if (w < WS) {
-                slab += o[0] / G;
-                slab_max = std::max(slab_max, o[0] / G);
-                pf += (o[1] & 0xffffffffu) / G;
-                po += (o[1] >> 32) / G;
-                pr += (o[2] >> 32) / G;
-            } else {
-                chain += o[0] / G;
-                chain_steps += (o[1] & 0xffffffffu) / G;
-            }
-            total += (o[2] & 0xffffffffu) / G;
+            busy[w] += o[0] / G / grid;
+            ph1[w] += (o[1] & 0xffffffffu) / G / grid;
+            mid[w] += (o[1] >> 32) / G / grid;
+            total += (o[2] & 0xffffffffu) / G / (grid * nwaves);
         }
-    fprintf(stderr,
-            "coop3 stamps [cycles per period]: total %.0f | slab %.0f (max %.0f; prefetch %.0f, post %.0f, pre %.0f) | "
-            "chain %.0f (steps %.0f)\n",
-            total / (grid * nwaves), slab / (grid * WS), slab_max, pf / (grid * WS), po / (grid * WS), pr / (grid * WS),
-            chain / grid, chain_steps / grid);
+    fprintf(stderr, "coop3 stamps [cycles per period]: total %.0f | per wave busy/phase1/midwait:", total);
+    for (int w = 0; w < nwaves; w++)
+        fprintf(stderr, " %s%d:%.0f/%.0f/%.0f", w == CHW ? "chain" : "", w, busy[w], ph1[w], mid[w]);
+    fprintf(stderr, "\n");
 }
 
 template <int WS, int R>
@@ -555,13 +658,16 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
 {
     *cc = CoopCode{};
     if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return LDPC_OK;
-    const int ws = env_int3("LDPC_COOP3_WS", 4);
+    const int ws = env_int3("LDPC_COOP3_WS", 6);
     const int r = env_int3("LDPC_COOP3_R", 2);
-    if ((ws != 3 && ws != 4) || (r != 2 && r != 5))
-        return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 3 | 4 and LDPC_COOP3_R 2 | 5");
+    if ((ws != 3 && ws != 4 && ws != 6) || (r != 2 && r != 3))
+        return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 3 | 4 | 6 and LDPC_COOP3_R 2 | 3");
     const int S = 8 * ws;
     CoopPlan pl;
-    if (coop_build_plan(h, S, r, DIST, RECW, pl, true) != 0) return LDPC_OK;
+    // dist 1 (a mid-period barrier orders posts before pres); a value is
+    // stored in the period after its window's chain, so reads 2 .. r+2 windows
+    // later are forwarded from the LDS stage (plan prefetch depth r + 1)
+    if (coop_build_plan(h, S, r + 1, 1, RECW, pl, true) != 0) return LDPC_OK;
     const int nw = (int)pl.first.size();
     for (int u = 0; u < nw; u++)
         for (int k = 0; k < S; k++) {
@@ -627,6 +733,7 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.coff = (uint32_t)(L.param * 256) * 0x00010001u;
     a.offp = (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
     a.prio = env_int3("LDPC_COOP3_PRIO", 1);
+    a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 0);
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0;
     const int ws = cc.S / 8;
@@ -637,12 +744,17 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
     int rc;
-    if (ws == 4)
-        rc = cc.R == 5 ? launch_wsr<4, 5>(a, grid, stamped, s) : launch_wsr<4, 2>(a, grid, stamped, s);
+    if (ws == 6)
+        rc = cc.R == 3 ? launch_wsr<6, 3>(a, grid, stamped, s) : launch_wsr<6, 2>(a, grid, stamped, s);
+    else if (ws == 4)
+        rc = cc.R == 3 ? launch_wsr<4, 3>(a, grid, stamped, s) : launch_wsr<4, 2>(a, grid, stamped, s);
     else
-        rc = cc.R == 5 ? launch_wsr<3, 5>(a, grid, stamped, s) : launch_wsr<3, 2>(a, grid, stamped, s);
+        rc = cc.R == 3 ? launch_wsr<3, 3>(a, grid, stamped, s) : launch_wsr<3, 2>(a, grid, stamped, s);
     if (stamped) {
-        if (rc == 0) (ws == 4 ? report_stamps3<4>(a.stamps, grid, s) : report_stamps3<3>(a.stamps, grid, s));
+        if (rc == 0)
+            (ws == 6   ? report_stamps3<6>(a.stamps, grid, s)
+             : ws == 4 ? report_stamps3<4>(a.stamps, grid, s)
+                       : report_stamps3<3>(a.stamps, grid, s));
         (void)hipFree(a.stamps);
     }
     return rc;
