@@ -18,15 +18,24 @@
 //   ds_read_b128 per step; step outputs are written alternately into the low
 //   / high halves of four VGPRs (op_sel dst), so 8 steps' x inputs leave in
 //   one ds_write_b128;
-// * WS = 4 slab waves (S = 32 checks per window) use all four SIMDs; the
-//   chain wave shares one with the highest priority (WS = 3: S = 24, the
-//   chain has a SIMD of its own).
+// * WS = 6 slab waves (S = 48 checks per window, the plan fills ~45: DVB-S2
+//   r1/2 has q = 90) two per SIMD on SIMDs 0-2, the chain wave alone on SIMD
+//   3 with the highest priority;
+// * a window's checks are permuted over its slots (coop3_upload): the chain
+//   still runs them in check order (each record carries its chain step), and
+//   every distance-2 forwarding source and reader sits in slab wave 0, so no
+//   wave ever waits for another inside a period (one s_barrier per period);
+// * vector memory -- the bound on MI355X: each check moves 6 scattered 16-B
+//   V row pieces each way per 16 codewords, and the CU's texture path stalls
+//   on the scattered stores -- is issued at the start and middle of a
+//   period, never at its end: stores one barrier after their post, LDS-DMA
+//   gathers R = 2 windows ahead.
 //
 // Period p (one s_barrier): chain = steps of window p; slab waves = post of
-// window p-1, pre of window p+1, V / message loads of window p+1+R.  The plan
-// (dist 2) keeps windows closer than 3 free of shared information variables;
-// values written 3 .. R+2 windows before a pre are forwarded through the LDS
-// ring as in coop2.
+// window p-1, pre of window p+1, stores of window p-2, gathers of window
+// p+1+R.  The plan (dist 1) keeps neighbouring windows free of shared
+// information variables; values written 2 .. R+3 windows before a pre are
+// forwarded through a 4-window LDS stage ring.
 //
 // The chain recurrence (check i, x edge input Y = V[p_{i-1}]):
 //   V[p_i] = clamp(c_o + eps * sign(c_x) * min(max(|c_x| - off, 0), T), +-127)
@@ -47,6 +56,12 @@
 __device__ void sbuf_store_v4(i32x4 v, i32x4 rsrc, int index, int offset, int soffset, int aux)
     __asm("llvm.amdgcn.struct.buffer.store.v4i32");
 
+#ifdef C3_MARKERS   // instruction census of the fast period (asm comments; scheduling boundaries)
+#define C3_MARK(s) asm volatile(";C3MARK " s)
+#else
+#define C3_MARK(s)
+#endif
+
 namespace {
 
 constexpr int D0 = 7, X = D0 - 2;   // first-group check degree, information edges per check
@@ -54,6 +69,7 @@ constexpr int NFW = (X + 1) / 2;    // forwarding-code dwords per record
 constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;
 constexpr int DPER = 3;             // a window table's LDS-DMA is waited for DPER periods after its issue
 constexpr int TQ = 16;              // window-table slots in LDS
+constexpr int STG_RING = 8192;      // bytes per forwarding-ring slot (power of two: see fwd_code3)
 
 template <int WS, int R>
 struct Cfg {
@@ -62,11 +78,14 @@ struct Cfg {
     static constexpr int NI = R + 1;                   // LDS-DMA input windows in flight per slab wave
     static constexpr int NS = R + 1 < 3 ? 3 : R + 1;   // window states in VGPRs (pre at p-1, post at p+1)
     static constexpr int U = NS;                       // periods unrolled (multiple of NI and NS)
-    static constexpr int NR = (R + 1 <= 4) ? 4 : 8;    // staged-output windows (forwarding reads up to R + 2 later)
+    static constexpr int NR = 4;                       // staged-output windows: window g's entries are read in
+                                                       // periods g+1 .. g+R+2 (stores, forwards)
     static constexpr int CHW = WS >= 3 ? 3 : WS;       // the chain wave (waves go to SIMDs 0,2,1,3,0,2,1: wave 3
                                                        // has a SIMD of its own for WS = 3 and WS = 6)
-    static constexpr int NB = S / 8, NB1 = (NB + 1) / 2;   // chain blocks of 8 steps, before the mid barrier
+    static constexpr int NB = S / 8;                   // chain blocks of 8 steps
     static_assert(TQ >= KAHEAD + 2, "table ring: a window's records are read until its stores");
+    static_assert(NR == 4 && R + 2 <= NR && 8 * (S + 1) * 16 <= STG_RING,
+                  "forwarding ring: codes carry (g - dW) mod 4 for dW = 2 .. R+3");
     static_assert(U % NI == 0 && U % NS == 0, "unroll");
 };
 
@@ -78,12 +97,17 @@ struct alignas(16) Smem3 {
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
     uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post)
-    struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA:
-        uint4 a[8][8];                //   [slot][0..5] V rows (info edges, record entry D0-1), [6..7] message 0..31 B
-        uint4 b[8][2];                //   [slot][0..1] message 32..63 B
-    } in[WS][NI];
-    uint4 stg[NR][S][8];              // new V of a window, [slot][record entry] x 16 codewords (int8): the V
-                                      // stores' staging and the forwarding ring
+    struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
+        uint4 a[8][8];                //   [0..5][slot] V rows (info edges, record entry D0-1), [6..7][slot] message
+                                      //   0..31 B
+        uint4 pad[4];                 //   (rows 6, 7 and b[0], b[1] in different banks)
+        uint4 b[2][8];                //   [0..1][slot] message 32..63 B
+    } in[WS][NI];                     // (entry-major: the 8 slots of one read are in different banks)
+    static constexpr uint32_t IN_B = sizeof(uint4) * (8 * 8 + 4);   // byte offset of In::b
+    uint4 stg[NR][STG_RING / 16];     // new V of a window, [record entry * (S + 1) + slot] x 16 codewords (int8,
+                                      // entries padded: the stores' reads of 8 entries are conflict-free): the
+                                      // V stores' staging and the forwarding ring (ring slot g % NR, 8 KB apart
+                                      // so that a forwarding code + (g << 13) addresses its entry)
     uint4 mst[WS][8][4];              // new messages of a window per slab wave, [slot] x 64 B
 };
 
@@ -102,7 +126,14 @@ struct St3 {                          // one window's state from pre to post (R 
     uint32_t a[D0 - 1];               // |c| (not clipped: min1 / min2 are, where the constants are made)
     uint32_t mn1, mn2, sacc, mx;      // min1 / min2 / sign parity over info + o; x-edge old message
                                       // tail: mn1 = MA, mn2 = MB
+    uint32_t xs;                      // the slot's chain step: u16 index of its x input in xo[buf]
 };
+
+// record meta (word D0): check | COOP_M_ACT | chain step << STEP_SHIFT.  The
+// host permutes a window's checks over its slots (coop3_upload: every
+// distance-2 forwarding source and reader in slab wave 0); the chain runs the
+// steps in check order, so a slot's constants / x input sit at its step
+constexpr int STEP_SHIFT = 22;
 
 LDPC_DEV uint32_t pk_ashr8(uint32_t a) { return us(sv(a) >> (short)8); }
 LDPC_DEV uint32_t pk_add(uint32_t a, uint32_t b) { return us(sv(a) + sv(b)); }
@@ -113,7 +144,8 @@ constexpr uint32_t V127 = 0x007F007Fu, VNEG127 = 0xFF81FF81u;   // +-127 per hal
 struct PreIn {
     uint32_t v[D0 - 1];               // raw V dwords (info edges, entry D0-1)
     uint32_t ma, mb;                  // old message record of this pair
-    uint4 mf;                         // record words D0 .. D0+3: meta, forwarding codes
+    uint4 mf;                         // record words D0 .. D0+3: meta, forwarding codes (read a period early)
+    uint32_t fv[X];                   // forwarded V pairs (raw u16) of the info edges with a forwarding code
 };
 struct StIn {                         // the stores of window p-2
     uint4 vd, md;                     // staged V row piece (16 codewords), message piece
@@ -139,32 +171,50 @@ struct Slab3 {
     uint32_t vrd, mrd;                // byte offsets of this lane's V dword / message pair in an In record
 
     // ---- reads
-    LDPC_DEV void read_pre(int g, int ib, PreIn &in) const
+    // in.mf = mfc (window g's codes, read in the previous period); mfn <- window g+1's
+    LDPC_DEV void read_pre(int g, int ib, PreIn &in, const uint4 &mfc, uint4 &mfn) const
     {
         const char *inb = (const char *)&sm.in[w][ib];
 #pragma unroll
-        for (int j = 0; j < D0 - 1; j++) in.v[j] = *(const uint32_t *)(inb + vrd + 16 * j);
+        for (int j = 0; j < D0 - 1; j++) in.v[j] = *(const uint32_t *)(inb + vrd + 128 * j);
         const uint2 mm = *(const uint2 *)(inb + mrd);
         in.ma = mm.x;
         in.mb = mm.y;
-        in.mf = *(const uint4 *)&sm.tab[g & (TQ - 1)][k][D0];
+        in.mf = mfc;
+        mfn = read_mf(g + 1);
+    }
+    LDPC_DEV uint4 read_mf(int g) const { return *(const uint4 *)&sm.tab[g & (TQ - 1)][k][D0]; }
+    // forwarded values of window g's info edges: code j (16 bits, fwd_code3)
+    // = ((-dW) mod 4) << 13 | stage offset | near << 1 | use; code + (g << 13)
+    // carries ring slot (g - dW) mod 4 in bits 13-14.  Unused codes read
+    // ring offset 0 (ignored).  Branch-free: 2 VALU + 1 ds_read_u16 per edge.
+    LDPC_DEV void fwd_read(int g, PreIn &in) const
+    {
+        const char *sbase = (const char *)&sm.stg[0][0];
+        const uint32_t gs = (uint32_t)g << 13, q2 = 2u * (uint32_t)q;
+        const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
+#pragma unroll
+        for (int j = 0; j < X; j++) {
+            const uint32_t code = (j & 1) ? fw[j >> 1] >> 16 : fw[j >> 1] & 0xFFFFu;
+            in.fv[j] = *(const unsigned short *)(sbase + (((code + gs) & 0x7FF0u) | q2));
+        }
     }
     LDPC_DEV void read_st(int g, StIn &in) const
     {
-        in.vd = sm.stg[g % NR][k][q];
+        in.vd = sm.stg[g % NR][q * (S + 1) + k];
         in.md = sm.mst[w][kl][q & 3];
         in.row = sm.tab[g & (TQ - 1)][k][q];
         in.chk = sm.tab[g & (TQ - 1)][k][D0] & COOP_CHK_MASK;
     }
     LDPC_DEV void read_pf(int g, PfIn &in) const
     {
-        in.rv = sm.tab[g & (TQ - 1)][k][recsel] & g1mask;
-        in.chk2 = sm.tab[g & (TQ - 1)][8 * w + ((lane >> 1) & 7)][D0] & COOP_CHK_MASK;
+        in.rv = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][recsel] & g1mask;
+        in.chk2 = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][D0] & COOP_CHK_MASK;
     }
-    LDPC_DEV uint32_t read_x(int g) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
+    LDPC_DEV uint32_t read_x(int g, const St3 &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
-        const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][k >> 3][0];
-        const uint32_t x0 = xs[(2 * q) * 8 + (k & 7)], x1 = xs[(2 * q + 1) * 8 + (k & 7)];
+        const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 16 * q;
+        const uint32_t x0 = xs[0], x1 = xs[8];
         return perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127]
     }
 
@@ -173,38 +223,32 @@ struct Slab3 {
     // message piece c (c < 4) of its wave's slot kl
     LDPC_DEV void stores(const StIn &in, bool tl) const
     {
+#ifndef C3X_NOVSTORE   // timing experiment only: results are wrong
         if (q < (tl ? D0 : D0 - 1)) sbuf_store_v4(__builtin_bit_cast(i32x4, in.vd), vr, (int)in.row, 0, 0, 0);
+#endif
         if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
     }
     LDPC_DEV void gathers(const PfIn &in, int ib) const
     {
+        static_assert(offsetof(typename SM::In, b) == SM::IN_B, "In layout");
         const uint32_t base = (uint32_t)(uintptr_t)&sm.in[w][ib];
         dma16(g1base + (size_t)in.rv * g1mul, base);
-        if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + (uint32_t)sizeof(sm.in[0][0].a));
+        if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + SM::IN_B);
     }
 
-    // V pairs written 2 .. R+2 windows ago replace the loaded ones (per
-    // lane): all five reads issued together, unused ones from the lane's own
-    // stage slot, then selected
-    LDPC_DEV void forward(int g, const uint4 &mf, uint32_t *v) const
+    // the first windows of the decode: a code whose source window precedes
+    // window 0 (g < dW) is not used
+    LDPC_DEV static void mask_early(int g, uint4 &mf)
     {
-        const uint32_t fw[3] = {mf.y, mf.z, mf.w};
-        static_assert(NFW == 3 && (NR & (NR - 1)) == 0, "record layout, ring size");
-        const char *sbase = (const char *)&sm.stg[0][0][0];
-        uint32_t val[X];
-        bool use[X];
+        uint32_t *fw = &mf.y;
 #pragma unroll
-        for (int j = 0; j < X; j++) {
-            const uint32_t code = (fw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
-            const int dw = (int)(code >> 9);
-            use[j] = code != COOP_FWD_NONE && g >= dw;
-            const uint32_t off = ((uint32_t)(g - dw) & (NR - 1)) * (uint32_t)sizeof(sm.stg[0]) +
-                                 ((code >> 3) & 63) * (uint32_t)sizeof(sm.stg[0][0]) + (code & 7) * 16u;
-            val[j] = *(const unsigned short *)(sbase + (use[j] ? off : 0u) + 2 * q);
-        }
+        for (int i = 0; i < 3; i++)
 #pragma unroll
-        for (int j = 0; j < X; j++)
-            if (use[j]) v[j] = perm(val[j], val[j], 0x010d000du);
+            for (int h = 0; h < 2; h++) {
+                const uint32_t code = (fw[i] >> (16 * h)) & 0xFFFFu;
+                const int dw = (int)(((0u - (code >> 13) - 2u) & 3u) + 2u);
+                if ((code & 1u) && g < dw) fw[i] &= ~(1u << (16 * h));
+            }
     }
 
     // pre of window g: chain constants -> cst[g & 1], state -> s
@@ -213,9 +257,15 @@ struct Slab3 {
     {
         const uint32_t meta = in.mf.x;
         uint32_t v[D0 - 1];
+        // V pair of edge j: this pair's two bytes of the loaded V dword, or the
+        // forwarded u16 (selector 0x050d040d: bytes 0, 1 of in.fv[j] -> R pair)
+        const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
 #pragma unroll
-        for (int j = 0; j < D0 - 1; j++) v[j] = unpack_v(in.v[j], usel);
-        if (__any((meta & COOP_M_FWD) != 0)) forward(g, in.mf, v);
+        for (int j = 0; j < X; j++) {
+            const uint32_t m = 0u - ((fw[j >> 1] >> (16 * (j & 1))) & 1u);
+            v[j] = perm(in.fv[j], in.v[j], (usel & ~m) | (0x050d040du & m));
+        }
+        v[X] = unpack_v(in.v[X], usel);
         const MsgTab t = msg_tab(in.mb);
         const uint32_t MA = in.ma, neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
@@ -300,8 +350,11 @@ struct Slab3 {
         r1.z = perm(H, L, 0x07060302u);
         r0.w = r1.w = 0;
         const int cb = g & 1;
-        sm.cst[cb][k][0][q] = r0;
-        sm.cst[cb][k][1][q] = r1;
+        const uint32_t step = (meta >> STEP_SHIFT) & 63u;
+        s.xs = (step >> 3) * (CW * 8) + (step & 7);
+        uint4 *cp = &sm.cst[cb][0][0][q] + step * (2 * NP);
+        cp[0] = r0;
+        cp[NP] = r1;
     }
 
     // post of window g (x inputs xr): new V pairs -> stg[g % NR], messages ->
@@ -309,7 +362,8 @@ struct Slab3 {
     template <bool TL>
     LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
     {
-        unsigned short *st = (unsigned short *)&sm.stg[g % NR][k][0];   // [entry][8 pairs] u16
+        unsigned short *st = (unsigned short *)&sm.stg[g % NR][k];      // [entry][..S slots..][8 pairs] u16
+        constexpr int ES = (S + 1) * 8;                                 // u16 between entries
         uint32_t MA, MB;
         if constexpr (!TL) {
             const uint32_t cx = pk_max(pk_sub_sat(xr, s.mx), K.neg127);
@@ -330,14 +384,14 @@ struct Slab3 {
             (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
             MB = perm(k2, k1, 0x07030501u);
 #pragma unroll
-            for (int j = 0; j <= X; j++) st[j * 8 + q] = (unsigned short)nv[j];
+            for (int j = 0; j <= X; j++) st[j * ES + q] = (unsigned short)nv[j];
         } else {
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                st[J * 8 + q] = (unsigned short)pack_v(s.c[J]);
+                st[J * ES + q] = (unsigned short)pack_v(s.c[J]);
             });
-            st[X * 8 + q] = (unsigned short)pack_v(xr);               // V of the last group-0 check's o edge
-            st[(D0 - 1) * 8 + q] = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
+            st[X * ES + q] = (unsigned short)pack_v(xr);               // V of the last group-0 check's o edge
+            st[(D0 - 1) * ES + q] = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
             MA = s.mn1;
             MB = s.mn2;
         }
@@ -391,6 +445,16 @@ LDPC_DEV void chain_window3(Smem3<WS, R> &sm, int buf, int c, uint32_t (&w)[4])
     }
 }
 
+// diagnostic stamps that do not wait: the compiler waits for s_memtime only
+// where the value is used (the end of a period)
+LDPC_DEV unsigned long long stampL()
+{
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
 LDPC_DEV unsigned long long stamp3()
 {
     unsigned long long t;
@@ -406,7 +470,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 {
     using SM = Smem3<WS, R>;
     using CF = Cfg<WS, R>;
-    constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U, CHW = CF::CHW, NB = CF::NB, NB1 = CF::NB1;
+    constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U, CHW = CF::CHW, NB = CF::NB;
     __shared__ SM sm;
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -416,14 +480,17 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     const int G = a.G;
     if (G == 0) return;
     if (a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
-    unsigned long long sA = 0, sB = 0, sC = 0, sD = 0, t0 = 0, tx = 0;
+    // stamps (diagnostic build): per wave 8 words: busy, phases 1..3 (slab:
+    // vmcnt, first and second half), -, elapsed, -, G
+    unsigned long long sA = 0, sP[4] = {0, 0, 0, 0}, sD = 0, t0 = 0, tx = 0;
     auto write_stamps = [&]() {
         if (STAMP && lane == 0) {
-            unsigned long long *o = a.stamps + ((size_t)id * (WS + 1) + wave) * 4;
+            unsigned long long *o = a.stamps + ((size_t)id * (WS + 1) + wave) * 8;
             o[0] = sA;
-            o[1] = sB | (sC << 32);
-            o[2] = (stamp3() - t0) | (sD << 32);
-            o[3] = (unsigned long long)G | (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) << 32;
+            for (int i = 0; i < 4; i++) o[1 + i] = sP[i];
+            o[5] = stamp3() - t0;
+            o[6] = sD;
+            o[7] = (unsigned long long)G;
         }
     };
 
@@ -452,10 +519,10 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         if (STAMP) t0 = stamp3();
         for (int p = 0; p <= G; p++) {
             if (STAMP) tx = stamp3();
-            if (p < G && cl) chain_window3<WS, R, 0, NB1>(sm, p & 1, c, w4);
-            __syncthreads();   // mid-period barrier (the slab waves' posts -> pres)
-            if (p < G && cl) chain_window3<WS, R, NB1, NB>(sm, p & 1, c, w4);
-            if (STAMP) sB += stamp3() - tx;
+#ifndef C3X_NOCHAIN   // timing experiment only: results are wrong
+            if (p < G && cl) chain_window3<WS, R, 0, NB>(sm, p & 1, c, w4);
+#endif
+            if (STAMP) sP[0] += stamp3() - tx;
             stage(un, (p + KAHEAD) & (TQ - 1));
             un = (un + 1 == a.nw) ? 0 : un + 1;
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPL * DPER) : "memory");
@@ -487,18 +554,22 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     a.tail,
                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
                     PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
-                    q < 6 ? Vb : Mb + (q - 6) * 16,
-                    Mb + (2 + (lane & 1)) * 16,
-                    q < 6 ? (uint32_t)a.pitch : (uint32_t)MREC,
-                    q < 6 ? 0xFFFFFFFFu : COOP_CHK_MASK,
-                    (uint32_t)(q < X ? q : (q == X ? D0 - 1 : D0)),
-                    (uint32_t)(kl * 128 + 4 * (q >> 1)),
-                    (uint32_t)(q < 4 ? kl * 128 + (6 + (q >> 1)) * 16 + (q & 1) * 8
-                                     : 1024 + kl * 32 + ((q >> 1) - 2) * 16 + (q & 1) * 8)};
+                    // DMA lane 8e + slot: entry e < 6 a V row (record entry e, the
+                    // o edge's D0-1 for e = X), e >= 6 message piece e - 6
+                    kl < 6 ? Vb : Mb + (kl - 6) * 16,
+                    Mb + (2 + (kl & 1)) * 16,
+                    kl < 6 ? (uint32_t)a.pitch : (uint32_t)MREC,
+                    kl < 6 ? 0xFFFFFFFFu : COOP_CHK_MASK,
+                    (uint32_t)(kl < X ? kl : (kl == X ? D0 - 1 : D0)),
+                    (uint32_t)(kl * 16 + 4 * (q >> 1)),
+                    (uint32_t)(q < 4 ? (6 + (q >> 1)) * 128 + kl * 16 + (q & 1) * 8
+                                     : SM::IN_B + ((q >> 1) - 2) * 128 + kl * 16 +
+                                           (q & 1) * 8)};
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     constexpr int NI = CF::NI, NS = CF::NS;
     __syncthreads();   // prologue 1: tables in LDS
     St3 st[NS];
+    uint4 mfc;   // records D0 .. D0+3 of the next pre's window
     {
         PfIn pi;
 #pragma unroll
@@ -508,7 +579,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         PreIn in;
-        sl.read_pre(0, 0, in);
+        sl.read_pre(0, 0, in, sl.read_mf(0), mfc);
+        sl.mask_early(0, in.mf);
+        sl.fwd_read(0, in);
         if (a.tail == 0)
             sl.template pre<true>(0, in, st[0]);
         else
@@ -516,67 +589,104 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     }
     __syncthreads();   // prologue 2
     if (STAMP) t0 = stamp3();
-    int uA = a.nw - 1;   // local index of window p-1 (post, stores)
+    int uA = a.nw - 1;   // local index of window p-1 (post)
     int uB = 1 % a.nw;   // local index of window p+1 (pre)
-    // Period p, phase 1: post of window p-1 (state st[(p-1) % NS]) -> staged
-    // outputs.  Mid barrier: the plan only keeps neighbouring windows free of
-    // shared information variables (dist 1), so a value window p+1 reads may
-    // have been written by the post just done; it is forwarded from the stage.
-    // Phase 2: pre of window p+1 (inputs in[w][(p+1) % NI], -> st[(p+1) % NS]),
-    // then the two stores of window p-1 and the two LDS-DMA gathers of window
-    // p+1+R into in[w][(p+1+R) % NI].  The gathers of window p+1 were the
-    // last vector memory operations of period p-R, followed by 4 in each
-    // later period: in the main loop (1 <= p <= G-2, every period does
-    // everything, no tail window) vmcnt(4(R-1)) covers them.
-    auto period = [&](auto sc, auto guarded, int p) __attribute__((always_inline)) {
-        constexpr int s = decltype(sc)::value;   // p % U
+    StIn sc;             // the stores of window p-2 (read from the stage at the end of period p-1)
+    bool sc_tl = false;  // ... window p-2 is the tail
+    // Period p: post of window p-1 (state st[(p-1) % NS], x inputs from the
+    // chain's window p-1) -> staged outputs; pre of window p+1 (inputs
+    // in[w][(p+1) % NI], -> st[(p+1) % NS]).  Vector memory: the two stores of
+    // window p-2 go first, the two LDS-DMA gathers of window p+1+R into
+    // in[w][(p+1+R) % NI] follow the first half, so no wave ends a period
+    // queueing behind the workgroup's stores (the CU's vector-memory issue is
+    // what bounds this kernel at the end of a period).
+    // The plan only keeps neighbouring windows free of shared information
+    // variables (dist 1): a value window p+1 reads may have been written by
+    // the post of window p-1 in this same period.  The host puts every such
+    // source and reader in slab wave 0, which posts before its pre and reads
+    // those values back from its own stage (LDS keeps a wave's order); the
+    // other waves run their pre first, so their x inputs arrive behind it.
+    // A value is stored at the start of the second period after its window's
+    // chain, so reads 2 .. R+3 windows later are forwarded (plan depth R + 2).
+    // The gathers of window p+1 were the last vector memory operations of
+    // period p-R, followed by 4 in each later period: in the main loop (every
+    // period does everything, no tail window) vmcnt(4(R-1)) covers them.
+    auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc_)::value;   // p % U
         constexpr bool GU = decltype(guarded)::value;
-        if (STAMP) tx = stamp3();
-        const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
-        const bool fast = !GU && uA != a.tail && uB != a.tail;
-        if (fast) {
-            sl.template post<false>(p - 1, sl.read_x(p - 1), st[(s + NS - 1) % NS]);
-        } else if (dpo) {
-            if (uA == a.tail)
-                sl.template post<true>(p - 1, sl.read_x(p - 1), st[(s + NS - 1) % NS]);
-            else
-                sl.template post<false>(p - 1, sl.read_x(p - 1), st[(s + NS - 1) % NS]);
-        }
-        unsigned long long t1 = 0;
-        if (STAMP) t1 = stamp3();
-        __syncthreads();
-        if (STAMP) sC += stamp3() - t1;
-        if constexpr (GU)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1)) : "memory");
+        if (STAMP) tx = stampL();
+        const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G, dst = p >= 2 && p <= G + 1;
+        const bool fast = !GU && uA != a.tail && uB != a.tail && !sc_tl;
         PreIn in;
-        StIn si;
         PfIn pi;
+        St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
+        unsigned long long t1 = 0, t2 = 0, t3 = 0;
         if (fast) {
-            sl.read_st(p - 1, si);
-            sl.read_pre(p + 1, (s + 1) % NI, in);
+            // every read of the period that does not depend on this period's
+            // own writes goes first (one exposed LDS latency): the gathers of
+            // window p+1 have landed (the vmcnt count of the main loop),
+            // chain inputs of window p-1, records of window p+1+R
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1)) : "memory");
+            if (STAMP) t1 = stampL();
+            sl.stores(sc, false);
+            const uint32_t xr = sl.read_x(p - 1, sp);
+            sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
             sl.read_pf(p + 1 + R, pi);
-            sl.template pre<false>(p + 1, in, st[(s + 1) % NS]);
-            sl.stores(si, false);
-            sl.gathers(pi, (s + R + 1) % NI);
+            if (sw == 0) {
+                C3_MARK("post0");
+                sl.template post<false>(p - 1, xr, sp);
+                sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values
+                sl.gathers(pi, (s + R + 1) % NI);
+                sl.read_st(p - 1, sc);
+                if (STAMP) t2 = stampL();
+                C3_MARK("pre0");
+                sl.template pre<false>(p + 1, in, sn);
+            } else {
+                sl.fwd_read(p + 1, in);   // windows <= p-2, staged before the barrier
+                C3_MARK("pre");
+                sl.template pre<false>(p + 1, in, sn);
+                sl.gathers(pi, (s + R + 1) % NI);
+                if (STAMP) t2 = stampL();
+                C3_MARK("post");
+                sl.template post<false>(p - 1, xr, sp);
+                sl.read_st(p - 1, sc);
+            }
+            if (STAMP) t3 = stampL();
+            C3_MARK("end");
         } else {
-            if (dpo) sl.read_st(p - 1, si);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (dst) sl.stores(sc, sc_tl);
+            if (dpo) {
+                if (uA == a.tail)
+                    sl.template post<true>(p - 1, sl.read_x(p - 1, sp), sp);
+                else
+                    sl.template post<false>(p - 1, sl.read_x(p - 1, sp), sp);
+            }
+            if (STAMP) t1 = t2 = t3 = stampL();
+            if (dpo) {
+                sl.read_st(p - 1, sc);
+                sc_tl = uA == a.tail;
+            }
             if (dpr) {
-                sl.read_pre(p + 1, (s + 1) % NI, in);
+                sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
+                if (p + 1 < R + 3) sl.mask_early(p + 1, in.mf);
+                sl.fwd_read(p + 1, in);
                 sl.read_pf(p + 1 + R, pi);
                 if (uB == a.tail)
-                    sl.template pre<true>(p + 1, in, st[(s + 1) % NS]);
+                    sl.template pre<true>(p + 1, in, sn);
                 else
-                    sl.template pre<false>(p + 1, in, st[(s + 1) % NS]);
+                    sl.template pre<false>(p + 1, in, sn);
+                sl.gathers(pi, (s + R + 1) % NI);
             }
-            if (dpo) sl.stores(si, uA == a.tail);
-            if (dpr) sl.gathers(pi, (s + R + 1) % NI);
         }
         if (STAMP) {
-            const unsigned long long t3 = stamp3();
-            sA += t3 - tx;
-            sB += t1 - tx;
+            const unsigned long long t5 = stampL();
+            sA += t5 - tx;
+            if (fast) {
+                sP[0] += t1 - tx;
+                sP[1] += t2 - t1;
+                sP[2] += t3 - t2;
+            }
         }
         __syncthreads();
         next(uA);
@@ -584,8 +694,12 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     };
     using T = std::true_type;
     using F = std::false_type;
-    period(std::integral_constant<int, 0>{}, T{}, 0);
-    int p = 1;
+    // periods 0 .. U guarded (their pres drop codes whose source window
+    // precedes window 0: U + 2 >= R + 3, the largest forwarding distance)
+    static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
+        if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, T{}, decltype(jc)::value);
+    });
+    int p = U + 1;
     // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U
     for (; p + U - 1 <= G - 2; p += U)
         static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
@@ -593,9 +707,10 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         });
     // the rest (at most U + 1 periods: p .. G), guarded
     static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
-        if (p + decltype(jc)::value <= G)
+        if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)
             period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
     });
+    sl.stores(sc, sc_tl);   // window G-1
     write_stamps();
 }
 
@@ -616,27 +731,28 @@ template <int WS>
 void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
 {
     constexpr int nwaves = WS + 1, CHW = WS >= 3 ? 3 : WS;
-    std::vector<unsigned long long> h((size_t)grid * nwaves * 4);
+    std::vector<unsigned long long> h((size_t)grid * nwaves * 8);
     if (hipStreamSynchronize(s) != hipSuccess ||
         hipMemcpy(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
         return;
-    // slab: busy (both phases, without the end barrier), phase 1, mid-barrier wait
-    // chain: steps + staging (without the end barrier), steps
-    std::vector<double> busy(nwaves, 0.0), ph1(nwaves, 0.0), mid(nwaves, 0.0);
-    double total = 0;
+    std::vector<double> v((size_t)nwaves * 8, 0.0);
     for (int b = 0; b < grid; b++)
         for (int w = 0; w < nwaves; w++) {
-            const unsigned long long *o = &h[((size_t)b * nwaves + w) * 4];
-            const double G = (o[3] & 0xffffffffu) ? (double)(o[3] & 0xffffffffu) : 1.0;
-            busy[w] += o[0] / G / grid;
-            ph1[w] += (o[1] & 0xffffffffu) / G / grid;
-            mid[w] += (o[1] >> 32) / G / grid;
-            total += (o[2] & 0xffffffffu) / G / (grid * nwaves);
+            const unsigned long long *o = &h[((size_t)b * nwaves + w) * 8];
+            const double G = o[7] ? (double)o[7] : 1.0;
+            for (int i = 0; i < 6; i++) v[w * 8 + i] += o[i] / G / grid;
+            v[w * 8 + 6] += ((o[6] >> 16) & 0xffff) / G / grid;
+            v[w * 8 + 7] += (o[6] & 0xffff) / G / grid;
         }
-    fprintf(stderr, "coop3 stamps [cycles per period]: total %.0f | per wave busy/phase1/midwait:", total);
-    for (int w = 0; w < nwaves; w++)
-        fprintf(stderr, " %s%d:%.0f/%.0f/%.0f", w == CHW ? "chain" : "", w, busy[w], ph1[w], mid[w]);
-    fprintf(stderr, "\n");
+    fprintf(stderr, "coop3 stamps [cycles per period]: elapsed %.0f\n", v[5]);
+    for (int w = 0; w < nwaves; w++) {
+        const double *x = &v[w * 8];
+        if (w == CHW)
+            fprintf(stderr, "  chain %d: busy %.0f steps %.0f\n", w, x[0], x[1]);
+        else
+            fprintf(stderr, "  slab %d: busy %.0f | vmcnt %.0f %s %.0f %s %.0f mem %.0f\n", w, x[0], x[1],
+                    w == 0 ? "post" : "pre", x[2], w == 0 ? "pre" : "post", x[3], x[0] - x[1] - x[2] - x[3]);
+    }
 }
 
 template <int WS, int R>
@@ -652,6 +768,14 @@ int launch_wsr(const Coop3Args &a, int grid, bool stamped, hipStream_t s)
 
 }  // namespace
 
+// forwarding code of a value written dW windows before the reading window,
+// by slot `slot`, record entry e (Slab3::fwd_read): ring slot (g - dW) mod 4 is
+// ((-dW) mod 4 + g) mod 4, entry offset (e * (S + 1) + slot) * 16 < 8192
+static uint32_t fwd_code3(int dW, int slot, int e, int S)
+{
+    return ((uint32_t)(-dW) & 3u) << 13 | (uint32_t)(e * (S + 1) + slot) * 16u | (dW == 2 ? 2u : 0u) | 1u;
+}
+
 bool coop3_params_ok(const ldpc_params *p) { return coop_params_ok(p); }
 
 int coop3_upload(const ldpc_code *h, CoopCode *cc)
@@ -660,25 +784,70 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
     if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return LDPC_OK;
     const int ws = env_int3("LDPC_COOP3_WS", 6);
     const int r = env_int3("LDPC_COOP3_R", 2);
-    if ((ws != 3 && ws != 4 && ws != 6) || (r != 2 && r != 3))
-        return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 3 | 4 | 6 and LDPC_COOP3_R 2 | 3");
+    if ((ws != 3 && ws != 4 && ws != 6) || r != 2)
+        return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 3 | 4 | 6 and LDPC_COOP3_R 2");
     const int S = 8 * ws;
     CoopPlan pl;
-    // dist 1 (a mid-period barrier orders posts before pres); a value is
-    // stored in the period after its window's chain, so reads 2 .. r+2 windows
-    // later are forwarded from the LDS stage (plan prefetch depth r + 1)
-    if (coop_build_plan(h, S, r + 1, 1, RECW, pl, true) != 0) return LDPC_OK;
+    // dist 1 (distance-2 sources and readers share slab wave 0); a value is
+    // stored at the start of the second period after its window's chain, so
+    // reads 2 .. r+3 windows later are forwarded from the LDS stage (plan
+    // prefetch depth r + 2)
+    if (coop_build_plan(h, S, r + 2, 1, RECW, pl, true) != 0) return LDPC_OK;
     const int nw = (int)pl.first.size();
+    auto rec_at = [&](int u, int k) { return &pl.tab[((size_t)u * S + k) * RECW]; };
+    auto code_at = [&](const uint32_t *rec, int j) { return (rec[D0 + 1 + j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
+    // distance-2 forwarding sources and readers -> slab wave 0 (slots 0..7);
+    // the other checks keep their order, the inactive slots come last
+    std::vector<char> special((size_t)nw * S, 0);
     for (int u = 0; u < nw; u++)
-        for (int k = 0; k < S; k++) {
-            uint32_t *rec = &pl.tab[((size_t)u * S + k) * RECW];
+        for (int k = 0; k < pl.count[u]; k++)
+            for (int j = 0; j < X; j++) {
+                const uint32_t f = code_at(rec_at(u, k), j);
+                if (f == COOP_FWD_NONE || (f >> 9) != 2) continue;
+                special[(size_t)u * S + k] = 1;
+                special[(size_t)((u + nw - 2) % nw) * S + ((f >> 3) & 63)] = 1;
+            }
+    std::vector<int> slot_of((size_t)nw * S), check_at((size_t)nw * S);   // plan slot (= chain step) <-> slot
+    for (int u = 0; u < nw; u++) {
+        int n = 0;
+        for (int pass = 0; pass < 3; pass++)
+            for (int k = 0; k < S; k++) {
+                const bool act = k < pl.count[u], sp = special[(size_t)u * S + k] != 0;
+                if ((pass == 0 && sp) || (pass == 1 && act && !sp) || (pass == 2 && !act)) {
+                    if (pass == 0 && n >= 8) return LDPC_OK;   // more than wave 0 holds: no coop3 schedule
+                    slot_of[(size_t)u * S + k] = n;
+                    check_at[(size_t)u * S + n] = k;
+                    n++;
+                }
+            }
+    }
+    std::vector<uint32_t> tab(pl.tab.size());
+    for (int u = 0; u < nw; u++)
+        for (int kn = 0; kn < S; kn++) {
+            const int k = check_at[(size_t)u * S + kn];
+            const uint32_t *src = rec_at(u, k);
+            uint32_t *rec = &tab[((size_t)u * S + kn) * RECW];
+            std::copy(src, src + RECW, rec);
+            for (int j = 0; j < 2 * NFW; j++) {   // plan codes -> fwd_code3 (the unused last half: 0)
+                const uint32_t f = j < X ? code_at(src, j) : COOP_FWD_NONE;
+                uint32_t c = 0;
+                if (f != COOP_FWD_NONE) {
+                    const int dw = (int)(f >> 9), uw = (u + nw - dw) % nw;
+                    c = fwd_code3(dw, slot_of[(size_t)uw * S + ((f >> 3) & 63)], (int)(f & 7), S);
+                }
+                uint32_t &d = rec[D0 + 1 + j / 2];
+                d = (d & ~(0xFFFFu << (16 * (j & 1)))) | (c << (16 * (j & 1)));
+            }
             if (k >= pl.count[u]) {   // inactive slot: sink V row n, sink message row m, no flags
                 for (int j = 0; j < D0; j++) rec[j] = (uint32_t)h->n;
                 rec[D0] = (uint32_t)h->m;
-            } else if (u == pl.tail) {
-                std::swap(rec[X], rec[D0 - 1]);   // prefetch always loads record entry D0-1
+            } else {
+                rec[D0] &= COOP_CHK_MASK | COOP_M_ACT;
+                if (u == pl.tail) std::swap(rec[X], rec[D0 - 1]);   // prefetch always loads record entry D0-1
             }
+            rec[D0] |= (uint32_t)k << STEP_SHIFT;
         }
+    pl.tab.swap(tab);
     if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop3 tables");
     if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         coop_free(cc);
@@ -739,17 +908,17 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     const int ws = cc.S / 8;
     const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0;
     if (stamped) {
-        const size_t bytes = (size_t)grid * (ws + 1) * 4 * sizeof(unsigned long long);
+        const size_t bytes = (size_t)grid * (ws + 1) * 8 * sizeof(unsigned long long);
         if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
     int rc;
     if (ws == 6)
-        rc = cc.R == 3 ? launch_wsr<6, 3>(a, grid, stamped, s) : launch_wsr<6, 2>(a, grid, stamped, s);
+        rc = launch_wsr<6, 2>(a, grid, stamped, s);
     else if (ws == 4)
-        rc = cc.R == 3 ? launch_wsr<4, 3>(a, grid, stamped, s) : launch_wsr<4, 2>(a, grid, stamped, s);
+        rc = launch_wsr<4, 2>(a, grid, stamped, s);
     else
-        rc = cc.R == 3 ? launch_wsr<3, 3>(a, grid, stamped, s) : launch_wsr<3, 2>(a, grid, stamped, s);
+        rc = launch_wsr<3, 2>(a, grid, stamped, s);
     if (stamped) {
         if (rc == 0)
             (ws == 6   ? report_stamps3<6>(a.stamps, grid, s)

@@ -31,6 +31,9 @@ for p in $PASSES; do
     write) run write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/write -o run -- python3 bench.py $ARGS ;;
     sq) run sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-include-regex "$KRE" -f csv -d $OUT/sq -o run -- python3 bench.py $ARGS ;;
     sq2) run sq2 600 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES --kernel-include-regex "$KRE" -f csv -d $OUT/sq2 -o run -- python3 bench.py $ARGS ;;
+    tlb) run tlb 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS TCP_UTCL1_TRANSLATION_HIT TCP_UTCL1_REQUEST TCP_UTCL1_STALL_MULTI_MISS --kernel-include-regex "$KRE" -f csv -d $OUT/tlb -o run -- python3 bench.py $ARGS ;;
+    tcplat) run tcplat 600 rocprofv3 --pmc TCP_TCC_WRITE_REQ_LATENCY TCP_TCC_READ_REQ_LATENCY TCP_TCC_WRITE_REQ TCP_TCC_READ_REQ TA_ADDR_STALLED_BY_TC_CYCLES TA_BUSY --kernel-include-regex "$KRE" -f csv -d $OUT/tcplat -o run -- python3 bench.py $ARGS ;;
+    tcpstall) run tcpstall 600 rocprofv3 --pmc TCP_PENDING_STALL_CYCLES TCP_TCP_TA_DATA_STALL_CYCLES TCP_TCR_TCP_STALL_CYCLES TCP_UTCL1_SERIALIZATION_STALL TA_DATA_STALLED_BY_TC_CYCLES TA_TA_BUSY --kernel-include-regex "$KRE" -f csv -d $OUT/tcpstall -o run -- python3 bench.py $ARGS ;;
     list) timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true ;;
     tcc) run tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KRE" -f csv -d $OUT/tcc -o run -- python3 bench.py $ARGS ;;
     esac
