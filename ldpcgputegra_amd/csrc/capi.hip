@@ -267,7 +267,7 @@ static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, i
     case 6: return co2 ? 6 : -1;
     case 8: return co3 ? 8 : -1;
     default:
-        if (co3 && getenv_int("LDPC_DEFAULT_COOP3", 0)) return 8;
+        if (co3 && getenv_int("LDPC_DEFAULT_COOP3", 1)) return 8;
         if (co2) return 6;
         if (co) return 5;
         if (w2 && c->w16.valid) return 3;
