@@ -319,15 +319,17 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     }
     const bool win = kern >= 2;
     // + a sink row / sink words for the masked stores of the coop kernel
-    const size_t msg_need = (kern == 6 || kern == 8 ? coop2_msg_bytes(h, stride)
+    const size_t msg_zero = (kern == 6 || kern == 8 ? coop2_msg_bytes(h, stride)
                              : win    ? windowed_msg_bytes(h, stride)
                                       : (size_t)h->e * stride * esz) +
                             4096;
+    // coop3: its parity-row layout follows the messages (DecodeLaunch::P)
+    const size_t msg_need = msg_zero + (kern == 8 ? (size_t)(h->m + 1) * stride : 0);
     if ((rc = ensure(&c->d_V, &c->V_bytes, (size_t)(h->n + 1) * stride * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&c->d_msg, &c->msg_bytes, msg_need)) != LDPC_OK) return rc;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
-    HIP_TRY(hipMemsetAsync(c->d_msg, 0, msg_need, s));
+    HIP_TRY(hipMemsetAsync(c->d_msg, 0, msg_zero, s));
     if (is_float) {
         if (launch_interleave_f32((const float *)d_llr, (float *)c->d_V, h->n, batch, stride, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
@@ -338,6 +340,7 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     DecodeLaunch L{};
     L.V = c->d_V;
     L.msg = c->d_msg;
+    if (kern == 8) L.P = (int8_t *)c->d_msg + msg_zero;
     L.stride = stride;
     L.batch = batch;
     L.iters = n_iter;

@@ -10,6 +10,7 @@ struct CoopCode {
     int nw;          // windows per iteration (tail and empty windows included)
     int tail;        // window index of the tail check
     int n_fwd;       // forwarded info-edge reads per iteration (plan statistic)
+    int x0;          // coop3: V row of check 0's x edge (the chain's first input)
     uint32_t *d_tab; // [nw][S][recw]
 };
 

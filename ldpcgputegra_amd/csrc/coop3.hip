@@ -117,7 +117,8 @@ struct Coop3Args {
     const uint32_t *tab;              // [nw][S][RECW] slot records
     unsigned long long *stamps;       // diagnostic build: [grid][waves][4]
     const uint8_t *live;              // early termination: [pitch] 0 = converged (NULL: all live)
-    int pitch, G, nw, tail, mrows, n, remap, prio, slab_prio;
+    int8_t *P;                        // parity rows k + j at P[group][j], j <= m (DecodeLaunch::P)
+    int pitch, G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
 };
 
@@ -161,7 +162,9 @@ struct Slab3 {
     static constexpr int S = SM::S, NR = SM::NR;
     SM &sm;
     const Coop3Args &a;
-    i32x4 vr, mr;                     // V rows of this group (stride pitch), message rows in 16-B units
+    char *vsb;                        // V row store of record entry q: vsb + row * vsm (the parity entries
+    uint32_t vsm;                     //   q >= X go to the parity rows' own layout P, see Coop3Args)
+    i32x4 mr;                         // message rows in 16-B units
     int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
     uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
     PkK K;
@@ -224,7 +227,7 @@ struct Slab3 {
     LDPC_DEV void stores(const StIn &in, bool tl) const
     {
 #ifndef C3X_NOVSTORE   // timing experiment only: results are wrong
-        if (q < (tl ? D0 : D0 - 1)) sbuf_store_v4(__builtin_bit_cast(i32x4, in.vd), vr, (int)in.row, 0, 0, 0);
+        if (q < (tl ? D0 : D0 - 1)) *(uint4 *)(vsb + (size_t)in.row * vsm) = in.vd;
 #endif
         if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
     }
@@ -480,6 +483,27 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     const int G = a.G;
     if (G == 0) return;
     if (a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
+    // the group's parity rows -> P (consecutive checks' parity values
+    // contiguous: a wave's 8 o-edge gathers / x-edge stores touch 1-2 lines,
+    // not 8), back into V at the end
+    {
+        int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * CW;
+        int8_t *ppar = a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
+#pragma unroll 8
+        for (int j = threadIdx.x; j < a.m; j += blockDim.x)
+            *(uint4 *)(ppar + 16 * (size_t)j) = *(const uint4 *)(vpar + (size_t)j * (size_t)a.pitch);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    auto parity_out = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * CW;
+        const int8_t *ppar = a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
+#pragma unroll 8
+        for (int j = threadIdx.x; j < a.m; j += blockDim.x)
+            *(uint4 *)(vpar + (size_t)j * (size_t)a.pitch) = *(const uint4 *)(ppar + 16 * (size_t)j);
+    };
     // stamps (diagnostic build): per wave 8 words: busy, phases 1..3 (slab:
     // vmcnt, first and second half), -, elapsed, -, G
     unsigned long long sA = 0, sP[4] = {0, 0, 0, 0}, sD = 0, t0 = 0, tx = 0;
@@ -511,7 +535,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         for (int w = 0; w < KAHEAD; w++) stage(w % a.nw, w);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t w4[4] = {0, 0, 0, 0};
-        w4[0] = (uint32_t)(int)a.V[(size_t)a.tab[X] * (uint32_t)a.pitch + (uint32_t)(wg * CW + c)] & 0xFFFFu;
+        w4[0] = (uint32_t)(int)a.V[(size_t)a.x0 * (uint32_t)a.pitch + (uint32_t)(wg * CW + c)] & 0xFFFFu;
         int un = KAHEAD % a.nw;
         __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 in LDS
         __syncthreads();   // prologue 2: constants of window 0 in LDS
@@ -530,6 +554,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             __syncthreads();
         }
         write_stamps();
+        parity_out();
         return;
     }
 
@@ -542,9 +567,12 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     const int kl = lane >> 3, q = lane & 7;
     const char *Vb = (const char *)a.V + (size_t)wg * CW;
     const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
+    // parity rows k + j of this group at Pb + 16 j: row r at Pb - 16 k + 16 r
+    char *Pr = (char *)a.P + ((size_t)wg * (size_t)(a.m + 1) - (size_t)a.k) * 16;
     Slab3<WS, R> sl{sm,
                     a,
-                    buffer_rsrc(Vb, (uint32_t)a.pitch, (uint32_t)(a.n + 1)),
+                    q >= X ? Pr : (char *)Vb,
+                    q >= X ? 16u : (uint32_t)a.pitch,
                     buffer_rsrc(Mb, 16u, (uint32_t)a.mrows * 4u),
                     8 * sw + kl,
                     kl,
@@ -556,9 +584,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
                     // DMA lane 8e + slot: entry e < 6 a V row (record entry e, the
                     // o edge's D0-1 for e = X), e >= 6 message piece e - 6
-                    kl < 6 ? Vb : Mb + (kl - 6) * 16,
+                    kl < X ? Vb : kl == X ? Pr : Mb + (kl - 6) * 16,
                     Mb + (2 + (kl & 1)) * 16,
-                    kl < 6 ? (uint32_t)a.pitch : (uint32_t)MREC,
+                    kl < X ? (uint32_t)a.pitch : kl == X ? 16u : (uint32_t)MREC,
                     kl < 6 ? 0xFFFFFFFFu : COOP_CHK_MASK,
                     (uint32_t)(kl < X ? kl : (kl == X ? D0 - 1 : D0)),
                     (uint32_t)(kl * 16 + 4 * (q >> 1)),
@@ -712,6 +740,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     });
     sl.stores(sc, sc_tl);   // window G-1
     write_stamps();
+    parity_out();
 }
 
 __global__ void fill_iters3_k(int batch, int32_t *iters_used, int iters)
@@ -860,6 +889,7 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
     cc->nw = nw;
     cc->tail = pl.tail;
     cc->n_fwd = pl.n_fwd;
+    cc->x0 = (int)h->edge_var[h->check_start[0] + X];
     return LDPC_OK;
 }
 
@@ -898,6 +928,10 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.tail = cc.tail;
     a.mrows = L.m + 1;
     a.n = L.n;
+    a.m = L.m;
+    a.k = L.n - L.m;
+    a.x0 = cc.x0;
+    a.P = L.P;
     a.rmm = (uint32_t)(L.msg_max * 256 + 255) * 0x00010001u;
     a.coff = (uint32_t)(L.param * 256) * 0x00010001u;
     a.offp = (uint32_t)(L.param & 0xFFFF) * 0x00010001u;

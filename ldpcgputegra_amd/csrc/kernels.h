@@ -27,6 +27,10 @@ struct DecodeLaunch {
     // (coop2 keeps iterating converged codewords that share a workgroup with
     // live ones; the snapshot is merged back before the hard decisions)
     int8_t *Vs;
+    // coop3: the parity rows k .. n-1 (+ a sink row) in their own layout,
+    // [stride / 16][m + 1][16 codewords]: consecutive checks' parity values
+    // are contiguous per codeword group (the kernel copies them in and out)
+    int8_t *P;
 };
 
 int launch_generic(const DecodeLaunch &L, hipStream_t s);
