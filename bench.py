@@ -382,6 +382,8 @@ def main():
                                    cpu_baseline(a.code, a.iters, a.cpu_seconds, thr, a.seed))
         else:
             out["cpu_baseline"] = None
+        if dec.last_skipped:   # a faster kernel did not apply at this batch size
+            out["config"]["kernel_skipped"] = dec.last_skipped
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

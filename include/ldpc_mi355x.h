@@ -151,8 +151,12 @@ int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel family the last decode actually ran (1 generic, 2 windowed,
- * 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2, 7 lds; 0 before the first decode). */
+ * 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2, 7 lds, 8 coop3; 0 before the first decode). */
 int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
+/* The faster kernel the last automatic selection had to skip because of the
+ * batch size (6: coop2, whose V descriptor caps the batch at 16320
+ * codewords), 0 when none was. */
+int ldpc_ctx_last_skipped(ldpc_ctx *ctx, int *kernel);
 /* Kernel timing (bench / profiling): when enabled, every decode records HIP
  * events around the decode kernel on the stream it is launched on;
  * ldpc_ctx_kernel_time returns the summed kernel time and launch count since
@@ -212,6 +216,19 @@ int ldpc_awgn_i8_host(int n, int batch, uint64_t first_cw, uint64_t seed, const 
 int ldpc_awgn_i8_async(ldpc_ctx *ctx, void *hip_stream, int8_t *d_llr, int batch,
                        uint64_t first_cw, uint64_t seed, const uint32_t *table,
                        const uint8_t *d_codeword);
+/* float -> int8 LLR conversion, replacing CFastFixConversion::generate
+ * (code/x86/CFixPointConversion/CFastFixConversion.cpp:55-65) and the GPU
+ * converter (code/gpu_fixed/decoder_template/GPU_Scheduled_functions.cu:54-62):
+ *   q[i] = clamp((int)((float)factor * y[i]), sat_neg, sat_pos)
+ * (int) truncates toward zero; NaN and |product| >= 2^31 give sat_neg, as
+ * x86 cvttss2si does.  factor >= 1, -128 <= sat_neg <= sat_pos <= 127
+ * (the reference runs factor 8, saturation -31 / +31).
+ * _async: device buffers on hip_stream; the plain form: host buffers,
+ * synchronous, on the context's stream. */
+int ldpc_quantize_f32_i8_async(ldpc_ctx *ctx, void *hip_stream, const float *d_y, int8_t *d_q, long count,
+                               int factor, int sat_neg, int sat_pos);
+int ldpc_quantize_f32_i8(ldpc_ctx *ctx, const float *y, int8_t *q, long count, int factor, int sat_neg,
+                         int sat_pos);
 /* Count bit errors over the first k positions of each codeword vs d_ref
  * (NULL = all-zero); d_counts[0] += bit errors, d_counts[1] += frame errors. */
 int ldpc_count_errors_async(ldpc_ctx *ctx, void *hip_stream, const uint8_t *d_hard, int batch,

@@ -57,6 +57,7 @@ SIGNATURES = {
     "ldpc_ctx_set_kernel": (I, [P, I]),
     "ldpc_ctx_get_kernel": (I, [P, C.POINTER(I)]),
     "ldpc_ctx_last_kernel": (I, [P, C.POINTER(I)]),
+    "ldpc_ctx_last_skipped": (I, [P, C.POINTER(I)]),
     "ldpc_ctx_profile": (I, [P, I]),
     "ldpc_ctx_kernel_time": (I, [P, C.POINTER(C.c_double), C.POINTER(I), I]),
     "ldpc_decode_i8": (I, [P, P, P, I, I, C.POINTER(ldpc_params)]),
@@ -72,6 +73,8 @@ SIGNATURES = {
     "ldpc_awgn_i8_host": (I, [I, I, U64, U64, P, P, P]),
     "ldpc_awgn_i8_async": (I, [P, P, P, I, U64, U64, P, P]),
     "ldpc_count_errors_async": (I, [P, P, P, I, I, P, P]),
+    "ldpc_quantize_f32_i8_async": (I, [P, P, P, P, C.c_long, I, I, I]),
+    "ldpc_quantize_f32_i8": (I, [P, P, P, C.c_long, I, I, I]),
 }
 
 _lib = None

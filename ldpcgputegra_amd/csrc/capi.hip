@@ -34,6 +34,7 @@ struct ldpc_ctx {
     int max_stride = 0;
     int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop, 6 coop2, 7 lds, 8 coop3
     int last_kernel = 0;
+    int last_skipped = 0;   // the preferred kernel the last decode could not use at its batch size (0: none)
     hipStream_t stream = nullptr;
     // device copy of the code
     uint32_t *d_edge_var = nullptr;
@@ -217,6 +218,13 @@ extern "C" int ldpc_ctx_last_kernel(ldpc_ctx *c, int *k)
     return LDPC_OK;
 }
 
+extern "C" int ldpc_ctx_last_skipped(ldpc_ctx *c, int *k)
+{
+    if (!c || !k) return ldpc_set_error(LDPC_EINVAL, "NULL");
+    *k = c->last_skipped;
+    return LDPC_OK;
+}
+
 extern "C" int ldpc_ctx_get_kernel(ldpc_ctx *c, int *k)
 {
     if (!c || !k) return ldpc_set_error(LDPC_EINVAL, "NULL");
@@ -248,8 +256,9 @@ static int check_params(const ldpc_ctx *c, int batch, int n_iter, const ldpc_par
 // 4 windowed2/S32, 5 coop (workgroup-cooperative), 6 coop2 (packed pairs),
 // 7 lds (LDS-resident short codes, int8 and float), 8 coop3 (slab waves doing
 // pre + post, i16 chain)
-static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, int stride)
+static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int stride)
 {
+    c->last_skipped = 0;
     const bool ld = lds_applicable(c->code, c->lds, is_float);
     if (c->kernel == 7) return ld ? 7 : -1;
     if (is_float) return (c->kernel == 0 && lds_preferred(c->code, c->lds, true)) ? 7 : (c->kernel <= 1 ? 1 : -1);
@@ -257,7 +266,7 @@ static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, i
     const bool w2 = windowed2_params_ok(p);
     const bool co = c->coop.valid && coop_params_ok(p);
     const bool co2 = c->coop2.valid && coop2_params_ok(p) && coop2_stride_ok(stride);
-    const bool co3 = c->coop3.valid && coop3_params_ok(p) && coop2_stride_ok(stride);
+    const bool co3 = c->coop3.valid && coop3_params_ok(p) && coop3_stride_ok(stride);
     switch (c->kernel) {
     case 1: return 1;
     case 2: return w1 ? 2 : -1;
@@ -269,6 +278,8 @@ static int pick_kernel(const ldpc_ctx *c, const ldpc_params *p, bool is_float, i
     default:
         if (co3 && getenv_int("LDPC_DEFAULT_COOP3", 1)) return 8;
         if (co2) return 6;
+        // coop2's V descriptor caps its batch (coop2_stride_ok): say so
+        if (c->coop2.valid && coop2_params_ok(p)) c->last_skipped = 6;
         if (co) return 5;
         if (w2 && c->w16.valid) return 3;
         if (lds_preferred(c->code, c->lds, false)) return 7;
@@ -454,6 +465,43 @@ extern "C" int ldpc_awgn_i8_async(ldpc_ctx *c, void *s, int8_t *d_llr, int batch
     memcpy(t.t, table, sizeof(t.t));
     if (launch_awgn_i8(d_llr, c->code->n, batch, first_cw, seed, t, d_codeword, (hipStream_t)s))
         return ldpc_set_error(LDPC_EDEVICE, "awgn: %s", hipGetErrorString(hipGetLastError()));
+    return LDPC_OK;
+}
+
+static bool quantize_args_ok(long count, int factor, int sat_neg, int sat_pos)
+{
+    return count >= 0 && factor >= 1 && sat_neg >= -128 && sat_pos <= 127 && sat_neg <= sat_pos;
+}
+
+extern "C" int ldpc_quantize_f32_i8_async(ldpc_ctx *c, void *s, const float *d_y, int8_t *d_q, long count, int factor,
+                                          int sat_neg, int sat_pos)
+{
+    if (!c || (count > 0 && (!d_y || !d_q)) || !quantize_args_ok(count, factor, sat_neg, sat_pos))
+        return ldpc_set_error(LDPC_EINVAL, "quantize args");
+    HIP_TRY(hipSetDevice(c->device));
+    if (launch_quantize_f32_i8(d_y, d_q, count, factor, sat_neg, sat_pos, (hipStream_t)s))
+        return ldpc_set_error(LDPC_EDEVICE, "quantize: %s", hipGetErrorString(hipGetLastError()));
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_quantize_f32_i8(ldpc_ctx *c, const float *y, int8_t *q, long count, int factor, int sat_neg,
+                                    int sat_pos)
+{
+    if (!c || (count > 0 && (!y || !q)) || !quantize_args_ok(count, factor, sat_neg, sat_pos))
+        return ldpc_set_error(LDPC_EINVAL, "quantize args");
+    if (count == 0) return LDPC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t in_bytes = (size_t)count * sizeof(float), al = (in_bytes + 255) & ~(size_t)255;
+    int rc;
+    if ((rc = ensure(&c->d_io, &c->io_bytes, al + (size_t)count)) != LDPC_OK) return rc;
+    float *d_y = (float *)c->d_io;
+    int8_t *d_q = (int8_t *)c->d_io + al;
+    const hipStream_t s = c->stream;
+    HIP_TRY(hipMemcpyAsync(d_y, y, in_bytes, hipMemcpyHostToDevice, s));
+    if (launch_quantize_f32_i8(d_y, d_q, count, factor, sat_neg, sat_pos, s))
+        return ldpc_set_error(LDPC_EDEVICE, "quantize: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipMemcpyAsync(q, d_q, (size_t)count, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
     return LDPC_OK;
 }
 

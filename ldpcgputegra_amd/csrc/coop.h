@@ -57,5 +57,6 @@ int launch_coop2(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
 
 // ---- coop3.hip: slab waves doing pre + post, i16 chain (D0 = 7) ----
 bool coop3_params_ok(const ldpc_params *p);
+bool coop3_stride_ok(int stride);
 int coop3_upload(const ldpc_code *h, CoopCode *cc);
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);

@@ -227,7 +227,15 @@ struct Slab3 {
     LDPC_DEV void stores(const StIn &in, bool tl) const
     {
 #ifndef C3X_NOVSTORE   // timing experiment only: results are wrong
+#ifdef C3X_VSTORE2   // timing experiment: V row pieces as two 8-B stores
+        if (q < (tl ? D0 : D0 - 1)) {
+            uint2 *d = (uint2 *)(vsb + (size_t)in.row * vsm);
+            d[0] = make_uint2(in.vd.x, in.vd.y);
+            d[1] = make_uint2(in.vd.z, in.vd.w);
+        }
+#else
         if (q < (tl ? D0 : D0 - 1)) *(uint4 *)(vsb + (size_t)in.row * vsm) = in.vd;
+#endif
 #endif
         if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
     }
@@ -235,6 +243,9 @@ struct Slab3 {
     {
         static_assert(offsetof(typename SM::In, b) == SM::IN_B, "In layout");
         const uint32_t base = (uint32_t)(uintptr_t)&sm.in[w][ib];
+#ifdef C3X_NOVLOAD   // timing experiment only: results are wrong
+        if (lane >= 8 * X)
+#endif
         dma16(g1base + (size_t)in.rv * g1mul, base);
         if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + SM::IN_B);
     }
@@ -807,6 +818,9 @@ static uint32_t fwd_code3(int dW, int slot, int e, int S)
 
 bool coop3_params_ok(const ldpc_params *p) { return coop_params_ok(p); }
 
+// V and P are addressed with 64-bit flat addresses: no batch cap (coop2 has one)
+bool coop3_stride_ok(int stride) { return stride > 0 && stride % 64 == 0; }
+
 int coop3_upload(const ldpc_code *h, CoopCode *cc)
 {
     *cc = CoopCode{};
@@ -898,7 +912,7 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
 
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
 {
-    if (!cc.valid || !coop2_stride_ok(L.stride)) return -1;
+    if (!cc.valid || !coop3_stride_ok(L.stride)) return -1;
     if (L.early) {
         // one launch per iteration; converged codewords keep iterating inside
         // live workgroups, so their V is snapshot when they converge and

@@ -36,6 +36,8 @@ struct DecodeLaunch {
 int launch_generic(const DecodeLaunch &L, hipStream_t s);
 
 // frame-major [batch][N] <-> node-major V[N][stride] (+ hard decision x > 0)
+int launch_quantize_f32_i8(const float *y, int8_t *q, long count, int factor, int sat_neg, int sat_pos,
+                           hipStream_t s);
 int launch_interleave_i8(const int8_t *llr, int8_t *V, int n, int batch, int stride, hipStream_t s);
 int launch_interleave_f32(const float *llr, float *V, int n, int batch, int stride, hipStream_t s);
 int launch_deinterleave_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, int stride,

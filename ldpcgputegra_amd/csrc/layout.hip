@@ -9,6 +9,8 @@
 //
 // Transposes move 64x64 tiles through LDS: global reads are 64 contiguous
 // elements per row of the source, writes 64 contiguous codewords per node row.
+#include <climits>
+#include <algorithm>
 #include "kernels.h"
 
 namespace {
@@ -121,6 +123,32 @@ __global__ void __launch_bounds__(256) copy_rows_k(const uint8_t *__restrict__ s
 inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -1; }
 
 }  // namespace
+
+// float -> int8 LLR, CFastFixConversion::generate
+// (code/x86/CFixPointConversion/CFastFixConversion.cpp:55-65): the float
+// product truncated toward zero, then clamped.  x86 cvttss2si gives INT_MIN
+// for NaN and for |product| >= 2^31: those clamp to sat_neg there, and here.
+__global__ void __launch_bounds__(256) quantize_k(const float *__restrict__ y, int8_t *__restrict__ q, long count,
+                                                  float factor, int sat_neg, int sat_pos)
+{
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+        const float v = factor * y[i];
+        int value = (fabsf(v) < 2147483648.0f) ? (int)v : INT_MIN;
+        value = value > sat_neg ? value : sat_neg;
+        value = value < sat_pos ? value : sat_pos;
+        q[i] = (int8_t)value;
+    }
+}
+
+int launch_quantize_f32_i8(const float *y, int8_t *q, long count, int factor, int sat_neg, int sat_pos,
+                           hipStream_t s)
+{
+    if (count <= 0) return 0;
+    const long blocks = std::min<long>((count + 255) / 256, 256L * 64);
+    hipLaunchKernelGGL(quantize_k, dim3((unsigned)blocks), dim3(256), 0, s, y, q, count, (float)factor, sat_neg,
+                       sat_pos);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_interleave_i8(const int8_t *llr, int8_t *V, int n, int batch, int stride, hipStream_t s)
 {

@@ -72,6 +72,14 @@ class Decoder:
         return self.KERNEL_NAMES.get(k.value, str(k.value))
 
     @property
+    def last_skipped(self):
+        """Name of the faster kernel the last decode skipped because of its
+        batch size (coop2's batch cap), None when none was."""
+        k = C.c_int()
+        _lib.check(_lib.lib().ldpc_ctx_last_skipped(self._ctx, C.byref(k)))
+        return self.KERNEL_NAMES.get(k.value, str(k.value)) if k.value else None
+
+    @property
     def stream(self):
         s = C.c_void_p()
         _lib.check(_lib.lib().ldpc_ctx_stream(self._ctx, C.byref(s)))
@@ -131,6 +139,21 @@ class Decoder:
         t = np.ascontiguousarray(table, dtype=np.uint32)
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_awgn_i8_async(
             self._ctx, s, self._ptr(llr), llr.shape[0], first_cw, seed, t.ctypes.data, self._ptr(codeword))), self.device)
+
+    def quantize_device(self, y, q, factor=8, sat_neg=-31, sat_pos=31, stream=None):
+        """float -> int8 LLR on the device (CFastFixConversion::generate's rule:
+        clamp(trunc(factor * y), sat_neg, sat_pos)); y float32, q int8, same numel."""
+        assert y.is_contiguous() and q.is_contiguous() and y.numel() == q.numel()
+        self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_quantize_f32_i8_async(
+            self._ctx, s, self._ptr(y), self._ptr(q), y.numel(), factor, sat_neg, sat_pos)), self.device)
+
+    def quantize(self, y, factor=8, sat_neg=-31, sat_pos=31):
+        """Host arrays: float32 -> int8 through the device (synchronous)."""
+        y = np.ascontiguousarray(y, dtype=np.float32)
+        q = np.empty(y.shape, dtype=np.int8)
+        _lib.check(_lib.lib().ldpc_quantize_f32_i8(self._ctx, y.ctypes.data, q.ctypes.data, y.size, factor, sat_neg,
+                                                   sat_pos))
+        return q
 
     def count_errors_device(self, hard, k, counts, ref=None, stream=None):
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_count_errors_async(

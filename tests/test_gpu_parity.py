@@ -7,6 +7,8 @@ exact IEEE ops (sub/add/min/max/abs, no FMA) as the oracle, so the test
 tolerance is FLOAT_TOL = 1e-6 absolute and in practice the results are
 bit-identical.
 """
+import os
+
 import numpy as np
 import pytest
 from conftest import golden_cases, golden_inputs
@@ -386,3 +388,60 @@ def test_device_calls_ordered_with_torch_default_stream():
         assert np.array_equal(i2.cpu().numpy(), got_i[sel])
         dec.close()
     mx.close()
+
+
+@pytest.mark.gpu
+def test_quantize_f32_i8_vs_oracle():
+    """ldpc_quantize_f32_i8[_async] vs CFastFixConversion::generate's rule
+    (code/x86/CFixPointConversion/CFastFixConversion.cpp:55-65, restated as
+    oracle_quantize): truncation toward zero at +-0.124 / 0.126 (x 8), the
+    saturation limits, other factors / limits, and a large random vector."""
+    torch = _torch()
+    dec = Decoder(Code("576x288"), max_batch=8)
+    edge = np.array([-5.0, -3.9, -0.124, -0.126, 0.0, -0.0, 0.124, 0.126, 0.9999, 3.874, 3.876, 100.0,
+                     1e30, -1e30], np.float32)
+    assert dec.quantize(edge).tolist() == O.quantize(edge).tolist()
+    rng = np.random.default_rng(5)
+    y = (rng.standard_normal(1 << 20) * 6).astype(np.float32)
+    for factor, lo, hi in ((8, -31, 31), (4, -127, 127), (16, -128, 127), (1, -7, 9)):
+        ref = O.quantize(y, factor, lo, hi)
+        assert np.array_equal(dec.quantize(y, factor, lo, hi), ref), (factor, lo, hi)
+        yd = torch.from_numpy(y).cuda()
+        qd = torch.empty(y.shape, dtype=torch.int8, device="cuda")
+        dec.quantize_device(yd, qd, factor, lo, hi)
+        assert np.array_equal(qd.cpu().numpy(), ref), (factor, lo, hi)
+
+
+def test_dvbs2_batch_above_coop2_cap_vs_reference():
+    """A batch above coop2's 16320-codeword cap (coop2_stride_ok): coop3 has
+    no cap and runs it -- every hard decision equals the reference SSE
+    decoder's (10 iterations); with coop3 disabled the automatic selection
+    falls back and reports the skipped coop2 (ldpc_ctx_last_skipped)."""
+    torch = _torch()
+    t = load_table("dvbs2_r1_2")
+    B = 16384 + 80
+    dec = decoder("dvbs2_r1_2", 0, B)
+    table = channel.i8_table(channel.sigma_from_ebn0(1.2, 0.5))
+    llr = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
+    dec.awgn_i8_device(llr, 5, 91, table)
+    hard = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+    dec.decode_i8_device(llr, hard, 10)
+    assert dec.last_kernel == "coop3" and dec.last_skipped is None
+    got = hard.cpu().numpy()
+    host_llr = llr.cpu().numpy()
+    thr = O.host_threads()
+    if O.ref_available("dvbs2_r1_2"):
+        exp = O.ref_decode_mt("dvbs2_r1_2", host_llr, 10, 1, thr)
+    else:
+        exp = O.decode_i8(t, host_llr, 10, threads=thr)
+    diff = np.nonzero((got != exp).any(axis=1))[0]
+    assert diff.size == 0, "codewords differing from the reference: %s" % diff[:16]
+    os.environ["LDPC_DEFAULT_COOP3"] = "0"
+    try:
+        dec.decode_i8_device(llr[:B // 2 + 64], hard[:B // 2 + 64], 2)
+        assert dec.last_skipped is None                        # 8256 codewords: coop2 applies
+        assert dec.last_kernel == "coop2"
+        dec.decode_i8_device(llr, hard, 2)
+        assert dec.last_kernel != "coop2" and dec.last_skipped == "coop2"
+    finally:
+        del os.environ["LDPC_DEFAULT_COOP3"]
