@@ -51,6 +51,7 @@
 #ifndef LDPC_MI355X_H
 #define LDPC_MI355X_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -164,11 +165,21 @@ int ldpc_ctx_last_skipped(ldpc_ctx *ctx, int *kernel);
 int ldpc_ctx_profile(ldpc_ctx *ctx, int enable);
 int ldpc_ctx_kernel_time(ldpc_ctx *ctx, double *total_ms, int *launches, int reset);
 
-/* Host buffers, synchronous, frame-major [batch][N]; hard = (V > 0). */
+/* Host buffers, synchronous, frame-major [batch][N]; hard = (V > 0).
+ * A large batch (>= 64 MB of LLRs) is decoded in chunks (LDPC_HOST_CHUNKS,
+ * default 2, >= 256 codewords each) on the context's copy/decode lanes, so
+ * the PCIe copies of one chunk overlap the decode of the other (decode_stream's streams,
+ * code/gpu_fixed/decoder_ms/CGPU_Decoder_MS_SIMD.cu:219-275).  With buffers
+ * from ldpc_host_alloc the copies are asynchronous DMA. */
 int ldpc_decode_i8(ldpc_ctx *ctx, const int8_t *llr, uint8_t *hard, int batch, int n_iter,
                    const ldpc_params *p);
 int ldpc_decode_f32(ldpc_ctx *ctx, const float *llr, uint8_t *hard, int batch, int n_iter,
                     const ldpc_params *p);
+
+/* Page-locked host memory for the host-buffer API, replacing the
+ * reference's CUDA_MALLOC_HOST (code/gpu_fixed/custom_api/custom_cuda.cu:33). */
+int ldpc_host_alloc(void **ptr, size_t bytes);
+void ldpc_host_free(void *ptr);
 
 /* Device buffers, asynchronous on `hip_stream`.  NULL means HIP's null
  * stream, i.e. the legacy default stream, ordered with all blocking streams

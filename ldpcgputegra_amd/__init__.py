@@ -9,10 +9,10 @@ from . import _lib
 from ._lib import ALGO_MS, ALGO_NMS, ALGO_OMS, LdpcError, default_params
 from .codes import Code, Table, available, load_table
 from .decoder import (CDecoder, CDecoder_NMS_fixed_MI355X, CDecoder_OMS_fixed_MI355X, CreateDecoder, Decoder,
-                      param_decoder)
+                      param_decoder, pinned_empty)
 
 __all__ = [
     "ALGO_MS", "ALGO_NMS", "ALGO_OMS", "LdpcError", "default_params", "Code", "Table", "available",
     "load_table", "CDecoder", "CDecoder_OMS_fixed_MI355X", "CDecoder_NMS_fixed_MI355X", "CreateDecoder",
-    "Decoder", "param_decoder",
+    "Decoder", "param_decoder", "pinned_empty",
 ]

@@ -75,6 +75,8 @@ SIGNATURES = {
     "ldpc_count_errors_async": (I, [P, P, P, I, I, P, P]),
     "ldpc_quantize_f32_i8_async": (I, [P, P, P, P, C.c_long, I, I, I]),
     "ldpc_quantize_f32_i8": (I, [P, P, P, C.c_long, I, I, I]),
+    "ldpc_host_alloc": (I, [C.POINTER(P), C.c_size_t]),
+    "ldpc_host_free": (None, [P]),
 }
 
 _lib = None

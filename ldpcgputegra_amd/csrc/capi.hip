@@ -27,6 +27,33 @@
             return ldpc_set_error(LDPC_EDEVICE, "%s: %s", #expr, hipGetErrorString(_e));       \
     } while (0)
 
+// per-decode device scratch (lazily sized)
+struct Scratch {
+    void *d_V = nullptr;
+    size_t V_bytes = 0;
+    void *d_msg = nullptr;
+    size_t msg_bytes = 0;
+    void *d_early = nullptr;        // coop early termination: live[stride] u8, bad[stride] u32, iters[stride]
+    size_t early_bytes = 0;
+    void *d_Vs = nullptr;           // coop2/coop3 early termination: V snapshot [N+1][stride]
+    size_t Vs_bytes = 0;
+    void release()
+    {
+        (void)hipFree(d_V);
+        (void)hipFree(d_msg);
+        (void)hipFree(d_early);
+        (void)hipFree(d_Vs);
+        *this = Scratch{};
+    }
+};
+
+struct Lane {
+    hipStream_t stream = nullptr;
+    Scratch sc;
+    void *d_io = nullptr;           // chunk input (LLRs) | output (hard decisions)
+    size_t io_bytes = 0;
+};
+
 struct ldpc_ctx {
     const ldpc_code *code = nullptr;
     int device = 0;
@@ -35,6 +62,7 @@ struct ldpc_ctx {
     int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop, 6 coop2, 7 lds, 8 coop3
     int last_kernel = 0;
     int last_skipped = 0;   // the preferred kernel the last decode could not use at its batch size (0: none)
+    int lds_pad = 0;        // extra dynamic LDS per windowed2 workgroup (ldpc_ctx_set_lds_pad)
     hipStream_t stream = nullptr;
     // device copy of the code
     uint32_t *d_edge_var = nullptr;
@@ -45,17 +73,12 @@ struct ldpc_ctx {
     CoopCode coop2{};               // coop2.hip tables (packed-pair variant, D0 = 7)
     CoopCode coop3{};               // coop3.hip tables (pre + post slab waves, i16 chain, D0 = 7)
     LdsCode lds{};                  // lds.hip tables (LDS-resident short-code decoder)
-    // scratch (lazily sized)
-    void *d_V = nullptr;
-    size_t V_bytes = 0;
-    void *d_msg = nullptr;
-    size_t msg_bytes = 0;
-    void *d_io = nullptr;           // staging for the host-buffer API
+    Scratch sc;                     // device-API decodes and the unchunked host path
+    void *d_io = nullptr;           // staging for the quantiser's host-buffer API
     size_t io_bytes = 0;
-    void *d_early = nullptr;        // coop early termination: live[stride] u8, bad[stride] u32, iters[stride]
-    size_t early_bytes = 0;
-    void *d_Vs = nullptr;           // coop2 early termination: V snapshot [N+1][stride]
-    size_t Vs_bytes = 0;
+    // host-buffer API pipeline (decode_host): chunk i of a batch runs on lane
+    // i % lanes.size(): its own stream, scratch and input / output staging
+    std::vector<Lane> lanes;
     // kernel timing (ldpc_ctx_profile)
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -154,11 +177,14 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     (void)hipFree(c->d_edge_var);
     (void)hipFree(c->d_group_deg);
     (void)hipFree(c->d_group_cnt);
-    (void)hipFree(c->d_V);
-    (void)hipFree(c->d_msg);
+    c->sc.release();
     (void)hipFree(c->d_io);
-    (void)hipFree(c->d_early);
-    (void)hipFree(c->d_Vs);
+    for (Lane &l : c->lanes) {
+        if (l.stream) (void)hipStreamSynchronize(l.stream);
+        l.sc.release();
+        (void)hipFree(l.d_io);
+        if (l.stream) (void)hipStreamDestroy(l.stream);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -208,6 +234,18 @@ extern "C" int ldpc_ctx_kernel_time(ldpc_ctx *c, double *total_ms, int *launches
         }
         c->events.clear();
     }
+    return LDPC_OK;
+}
+
+// library-internal (mixed.hip): windowed2 workgroups of this context request
+// `bytes` of dynamic LDS they do not use, so that none fits beside a coop3
+// workgroup (124.5 KB of the CU's 160 KB): a mixed batch's windowed2 waves
+// then stay off the CUs running the coop3 decode, whose slab waves are
+// VALU-bound and would lose issue slots to them
+int ldpc_ctx_set_lds_pad(ldpc_ctx *c, int bytes)
+{
+    if (!c || bytes < 0 || bytes > 65536) return ldpc_set_error(LDPC_EINVAL, "lds pad");
+    c->lds_pad = bytes;
     return LDPC_OK;
 }
 
@@ -288,7 +326,7 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
     }
 }
 
-static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t *d_hard, void *d_soft,
+static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_llr, uint8_t *d_hard, void *d_soft,
                          int32_t *d_iters, int batch, int n_iter, const ldpc_params *p, bool is_float)
 {
     int rc = check_params(c, batch, n_iter, p, is_float);
@@ -336,22 +374,22 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
                             4096;
     // coop3: its parity-row layout follows the messages (DecodeLaunch::P)
     const size_t msg_need = msg_zero + (kern == 8 ? (size_t)(h->m + 1) * stride : 0);
-    if ((rc = ensure(&c->d_V, &c->V_bytes, (size_t)(h->n + 1) * stride * esz)) != LDPC_OK) return rc;
-    if ((rc = ensure(&c->d_msg, &c->msg_bytes, msg_need)) != LDPC_OK) return rc;
+    if ((rc = ensure(&sc.d_V, &sc.V_bytes, (size_t)(h->n + 1) * stride * esz)) != LDPC_OK) return rc;
+    if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_need)) != LDPC_OK) return rc;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
-    HIP_TRY(hipMemsetAsync(c->d_msg, 0, msg_zero, s));
+    HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));
     if (is_float) {
-        if (launch_interleave_f32((const float *)d_llr, (float *)c->d_V, h->n, batch, stride, s))
+        if (launch_interleave_f32((const float *)d_llr, (float *)sc.d_V, h->n, batch, stride, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
     } else {
-        if (launch_interleave_i8((const int8_t *)d_llr, (int8_t *)c->d_V, h->n, batch, stride, s))
+        if (launch_interleave_i8((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, stride, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
     }
     DecodeLaunch L{};
-    L.V = c->d_V;
-    L.msg = c->d_msg;
-    if (kern == 8) L.P = (int8_t *)c->d_msg + msg_zero;
+    L.V = sc.d_V;
+    L.msg = sc.d_msg;
+    if (kern == 8) L.P = (int8_t *)sc.d_msg + msg_zero;
     L.stride = stride;
     L.batch = batch;
     L.iters = n_iter;
@@ -370,15 +408,16 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     L.early = p->early_term;
     L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
     L.iters_used = d_iters;
+    L.lds_pad = c->lds_pad;
     if ((kern == 5 || kern == 6 || kern == 8) && p->early_term) {
         // live u8 | bad u32 | iterations used i32 (when the caller passed none)
-        if ((rc = ensure(&c->d_early, &c->early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
-        L.bad = (uint32_t *)c->d_early;
-        if (!L.iters_used) L.iters_used = (int32_t *)((char *)c->d_early + (size_t)stride * 4);
-        L.live = (uint8_t *)c->d_early + (size_t)stride * 8;
+        if ((rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
+        L.bad = (uint32_t *)sc.d_early;
+        if (!L.iters_used) L.iters_used = (int32_t *)((char *)sc.d_early + (size_t)stride * 4);
+        L.live = (uint8_t *)sc.d_early + (size_t)stride * 8;
         if (kern == 6 || kern == 8) {
-            if ((rc = ensure(&c->d_Vs, &c->Vs_bytes, (size_t)(h->n + 1) * stride)) != LDPC_OK) return rc;
-            L.Vs = (int8_t *)c->d_Vs;
+            if ((rc = ensure(&sc.d_Vs, &sc.Vs_bytes, (size_t)(h->n + 1) * stride)) != LDPC_OK) return rc;
+            L.Vs = (int8_t *)sc.d_Vs;
         }
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -400,9 +439,9 @@ static int decode_device(ldpc_ctx *c, hipStream_t s, const void *d_llr, uint8_t 
     }
     if (lr) return ldpc_set_error(LDPC_EDEVICE, "decode launch: %s", hipGetErrorString(hipGetLastError()));
     if (d_hard || d_soft) {
-        int r2 = is_float ? launch_deinterleave_f32((const float *)c->d_V, d_hard, (float *)d_soft, h->n, batch,
+        int r2 = is_float ? launch_deinterleave_f32((const float *)sc.d_V, d_hard, (float *)d_soft, h->n, batch,
                                                     stride, s)
-                          : launch_deinterleave_i8((const int8_t *)c->d_V, d_hard, (int8_t *)d_soft, h->n,
+                          : launch_deinterleave_i8((const int8_t *)sc.d_V, d_hard, (int8_t *)d_soft, h->n,
                                                    batch, stride, s);
         if (r2) return ldpc_set_error(LDPC_EDEVICE, "deinterleave: %s", hipGetErrorString(hipGetLastError()));
     }
@@ -413,16 +452,45 @@ extern "C" int ldpc_decode_i8_async(ldpc_ctx *c, void *s, const int8_t *d_llr, u
                                     int32_t *d_iters, int batch, int n_iter, const ldpc_params *p)
 {
     if (!c || (!d_llr && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr");
-    return decode_device(c, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, false);
+    return decode_device(c, c->sc, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, false);
 }
 
 extern "C" int ldpc_decode_f32_async(ldpc_ctx *c, void *s, const float *d_llr, uint8_t *d_hard, float *d_soft,
                                      int32_t *d_iters, int batch, int n_iter, const ldpc_params *p)
 {
     if (!c || (!d_llr && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr");
-    return decode_device(c, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, true);
+    return decode_device(c, c->sc, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, true);
 }
 
+// Chunks of the host-buffer path: whole 64-codeword rows, at least 256
+// codewords each (16 coop workgroups), LDPC_HOST_CHUNKS of them (at most 16;
+// default 2 when the input is large enough for its copy time to matter,
+// >= 64 MB, else 1).  Concurrent chunk decodes need hardware queues of their
+// own: HIP maps streams onto GPU_MAX_HW_QUEUES (4) queues per process, and
+// the null stream and the context's stream hold two of them, so a third
+// lane would share a queue -- and wait for -- the first one's decode
+// (measured: 4 lanes on 2 queues, 114 ms per DVB-S2 4096-codeword call vs
+// 68 ms unchunked).
+static int host_chunks(int batch, size_t in_bytes)
+{
+    const int def = in_bytes >= ((size_t)64 << 20) ? 2 : 1;
+    const int want = std::min(16, std::max(1, getenv_int("LDPC_HOST_CHUNKS", def)));
+    return std::max(1, std::min(want, batch / 256));
+}
+
+// The host-buffer path (CDecoder::decode(char*, char*, int), synchronous).
+// The batch is cut into chunks; chunk i runs on lane i (own stream, scratch
+// and staging): H2D(i) -> decode(i) are queued chunk by chunk, then the D2H
+// copies, so the copies of one chunk overlap the decodes of the others -- the
+// reference's W streams x F frames scheme (paper/ldpcGpuTegra.tex:279-289;
+// its decode_stream, code/gpu_fixed/decoder_ms/CGPU_Decoder_MS_SIMD.cu:219-275,
+// runs one stream with blocking copies).  A staircase-code decode takes about
+// as long for one 16-codeword workgroup as for a whole chip of them (its
+// serial chain is per workgroup), so the concurrent chunk decodes cost
+// nothing: a call takes ~ H2D(batch) + one decode + D2H(one chunk).  Pinned
+// host buffers (ldpc_host_alloc) make the copies asynchronous DMA; pageable
+// ones are staged by the HIP runtime (the host thread blocks in the copy, the
+// GPU keeps decoding).
 static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, int n_iter, const ldpc_params *p,
                        bool is_float)
 {
@@ -430,17 +498,63 @@ static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, i
     int rc = check_params(c, batch, n_iter, p, is_float);
     if (rc != LDPC_OK || batch == 0) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    const size_t in_bytes = (size_t)batch * c->code->n * (is_float ? 4 : 1);
-    const size_t out_bytes = (size_t)batch * c->code->n;
-    const size_t in_al = (in_bytes + 255) / 256 * 256;
-    if ((rc = ensure(&c->d_io, &c->io_bytes, in_al + out_bytes)) != LDPC_OK) return rc;
-    char *d_in = (char *)c->d_io, *d_out = d_in + in_al;
-    HIP_TRY(hipMemcpyAsync(d_in, llr, in_bytes, hipMemcpyHostToDevice, c->stream));
-    rc = decode_device(c, c->stream, d_in, (uint8_t *)d_out, nullptr, nullptr, batch, n_iter, p, is_float);
-    if (rc != LDPC_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(hard, d_out, out_bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    const size_t esz = is_float ? 4 : 1;
+    const int n = c->code->n, nc = host_chunks(batch, (size_t)batch * n * esz);
+    const int cs = ((batch + nc - 1) / nc + 63) / 64 * 64;   // codewords per chunk
+    if ((int)c->lanes.size() < nc) c->lanes.resize(nc);
+    int used = 0;
+    // every queued lane is joined before returning, on success and on error
+    auto finish = [&](int r) {
+        for (int i = 0; i < used; i++) {
+            const hipError_t e = hipStreamSynchronize(c->lanes[i].stream);
+            if (e != hipSuccess && r == LDPC_OK) r = ldpc_set_error(LDPC_EDEVICE, "host path: %s", hipGetErrorString(e));
+        }
+        return r;
+    };
+    for (int i = 0, b0 = 0; b0 < batch; i++, b0 += cs) {
+        Lane &l = c->lanes[i];
+        const int nb = std::min(cs, batch - b0);
+        const size_t in_bytes = (size_t)nb * n * esz, in_al = (in_bytes + 255) / 256 * 256;
+        if (!l.stream && hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess) {
+            l.stream = nullptr;
+            return finish(ldpc_set_error(LDPC_EDEVICE, "host path: hipStreamCreate"));
+        }
+        used = i + 1;
+        if ((rc = ensure(&l.d_io, &l.io_bytes, in_al + (size_t)cs * n)) != LDPC_OK) return finish(rc);
+        char *d_in = (char *)l.d_io, *d_out = d_in + in_al;
+        if (hipMemcpyAsync(d_in, (const char *)llr + (size_t)b0 * n * esz, in_bytes, hipMemcpyHostToDevice,
+                           l.stream) != hipSuccess)
+            return finish(ldpc_set_error(LDPC_EDEVICE, "host path H2D: %s", hipGetErrorString(hipGetLastError())));
+        rc = decode_device(c, l.sc, l.stream, d_in, (uint8_t *)d_out, nullptr, nullptr, nb, n_iter, p, is_float);
+        if (rc != LDPC_OK) return finish(rc);
+    }
+    for (int i = 0, b0 = 0; b0 < batch; i++, b0 += cs) {
+        Lane &l = c->lanes[i];
+        const int nb = std::min(cs, batch - b0);
+        const size_t in_al = ((size_t)nb * n * esz + 255) / 256 * 256;
+        if (hipMemcpyAsync(hard + (size_t)b0 * n, (char *)l.d_io + in_al, (size_t)nb * n, hipMemcpyDeviceToHost,
+                           l.stream) != hipSuccess)
+            return finish(ldpc_set_error(LDPC_EDEVICE, "host path D2H: %s", hipGetErrorString(hipGetLastError())));
+    }
+    return finish(LDPC_OK);
+}
+
+extern "C" int ldpc_host_alloc(void **p, size_t bytes)
+{
+    if (!p) return ldpc_set_error(LDPC_EINVAL, "NULL pointer");
+    *p = nullptr;
+    if (bytes == 0) return LDPC_OK;
+    const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return ldpc_set_error(LDPC_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    }
     return LDPC_OK;
+}
+
+extern "C" void ldpc_host_free(void *p)
+{
+    if (p) (void)hipHostFree(p);
 }
 
 extern "C" int ldpc_decode_i8(ldpc_ctx *c, const int8_t *llr, uint8_t *hard, int batch, int n_iter,

@@ -11,6 +11,7 @@ struct CoopCode {
     int tail;        // window index of the tail check
     int n_fwd;       // forwarded info-edge reads per iteration (plan statistic)
     int x0;          // coop3: V row of check 0's x edge (the chain's first input)
+    int m0, d1;      // coop3: checks of degree d0 (group 0), degree of the later group
     uint32_t *d_tab; // [nw][S][recw]
 };
 

@@ -118,6 +118,13 @@ struct Coop3Args {
     unsigned long long *stamps;       // diagnostic build: [grid][waves][4]
     const uint8_t *live;              // early termination: [pitch] 0 = converged (NULL: all live)
     int8_t *P;                        // parity rows k + j at P[group][j], j <= m (DecodeLaunch::P)
+    // in-kernel early termination (ET kernels): layered edge list (group 0:
+    // checks [0, m0) of degree D0, then degree d1), snapshot V [n][pitch],
+    // iterations used per codeword
+    const uint32_t *ev;
+    int8_t *Vs;
+    int32_t *iters_used;
+    int iters, batch, m0, d1;
     int pitch, G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
 };
@@ -478,8 +485,43 @@ LDPC_DEV unsigned long long stamp3()
     return t;
 }
 
+// ---- in-kernel early termination helpers (16 codewords = the 16 bytes of a
+// V row piece, codeword wg * 16 + j in byte j)
+// high bit of byte j set where byte j > 0 (the hard decision)
+LDPC_DEV uint32_t pos_bits(uint32_t d)
+{
+    const uint32_t nz = ((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d;   // high bit: byte != 0
+    return nz & ~d & 0x80808080u;
+}
+LDPC_DEV uint32_t high_bits16(uint4 x)   // byte high bits -> 16-bit codeword mask
+{
+    auto c4 = [](uint32_t v) { return ((v >> 7) & 1u) | ((v >> 14) & 2u) | ((v >> 21) & 4u) | ((v >> 28) & 8u); };
+    return c4(x.x) | c4(x.y) << 4 | c4(x.z) << 8 | c4(x.w) << 12;
+}
+LDPC_DEV uint32_t byte_mask4(uint32_t b)   // 4 codeword bits -> 4 byte masks
+{
+    return (b & 1u) * 0xFFu | ((b >> 1) & 1u) * 0xFF00u | ((b >> 2) & 1u) * 0xFF0000u | ((b >> 3) & 1u) * 0xFF000000u;
+}
+LDPC_DEV uint4 byte_mask16(uint32_t m)
+{
+    return make_uint4(byte_mask4(m & 15u), byte_mask4((m >> 4) & 15u), byte_mask4((m >> 8) & 15u),
+                      byte_mask4((m >> 12) & 15u));
+}
+LDPC_DEV uint4 blend16(uint4 a, uint4 b, uint4 m)   // (a & ~m) | (b & m)
+{
+    return make_uint4((a.x & ~m.x) | (b.x & m.x), (a.y & ~m.y) | (b.y & m.y), (a.z & ~m.z) | (b.z & m.z),
+                      (a.w & ~m.w) | (b.w & m.w));
+}
+
 // Wave CHW: the chain; the others: slab waves (slab index w: slots 8w .. 8w+7).
-template <int WS, int R, bool STAMP>
+// ET: in-kernel early termination -- the decode runs one iteration per
+// segment (pipeline drained at its end), then the whole workgroup checks the
+// syndrome of its live codewords (stopping once each has a failing check),
+// snapshots the V of the codewords converging now, and leaves when none is
+// live; the snapshots are merged back at the end.  Same result as the
+// reference's per-codeword stop (oracle: syndrome after every iteration), with
+// one launch instead of one per iteration plus syndrome / snapshot kernels.
+template <int WS, int R, bool STAMP, bool ET = false>
 __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 {
     using SM = Smem3<WS, R>;
@@ -491,9 +533,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     const int lane = threadIdx.x & 63;
     const int nb = gridDim.x, id = blockIdx.x;
     const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
-    const int G = a.G;
+    const int G = ET ? a.nw : a.G;   // periods per segment (ET: one iteration)
     if (G == 0) return;
-    if (a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
+    if (!ET && a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
     // the group's parity rows -> P (consecutive checks' parity values
     // contiguous: a wave's 8 o-edge gathers / x-edge stores touch 1-2 lines,
     // not 8), back into V at the end
@@ -514,6 +556,112 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 #pragma unroll 8
         for (int j = threadIdx.x; j < a.m; j += blockDim.x)
             *(uint4 *)(vpar + (size_t)j * (size_t)a.pitch) = *(const uint4 *)(ppar + 16 * (size_t)j);
+    };
+    // ---- ET state: [0] live codewords, [1] failing codewords (syndrome)
+    __shared__ uint32_t et_sh[2];
+    constexpr int NT = 64 * (WS + 1);
+    const char *etV = (const char *)a.V + (size_t)wg * CW;
+    const char *etP = (const char *)a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
+    auto et_row = [&](uint32_t v) -> const uint4 * {   // V row piece of variable v (parity rows: in P)
+        return (int)v < a.k ? (const uint4 *)(etV + (size_t)v * (size_t)a.pitch)
+                            : (const uint4 *)(etP + (size_t)(v - (uint32_t)a.k) * 16);
+    };
+    if constexpr (ET) {
+        if (threadIdx.x == 0) {
+            const int valid = min(CW, max(0, a.batch - wg * CW));
+            et_sh[0] = (1u << valid) - 1u;
+            et_sh[1] = 0;
+        }
+        if (threadIdx.x < CW && wg * CW + (int)threadIdx.x < a.batch) a.iters_used[wg * CW + threadIdx.x] = a.iters;
+        __syncthreads();
+        if (et_sh[0] == 0) return;   // padding columns only
+    }
+    // after iteration `it` (ET): syndrome, snapshot, decision -- every thread,
+    // uniform result (true: decode another iteration)
+    auto et_after = [&](int it) -> bool {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the iteration's stores and table DMAs
+        __syncthreads();
+        const uint32_t live = et_sh[0];
+        // each thread: 2 checks per round, 4 rounds between exit tests
+        for (int c0 = 0; c0 < a.m; c0 += NT * 8) {
+            uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                uint4 x[2];
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const int c = c0 + (2 * r + i) * NT + (int)threadIdx.x;
+                    x[i] = make_uint4(0, 0, 0, 0);
+                    if (c < a.m0) {
+                        const uint32_t *e = a.ev + (size_t)c * D0;
+                        uint4 y[D0];
+#pragma unroll
+                        for (int j = 0; j < D0; j++) y[j] = *et_row(e[j]);
+#pragma unroll
+                        for (int j = 0; j < D0; j++) {
+                            x[i].x ^= pos_bits(y[j].x);
+                            x[i].y ^= pos_bits(y[j].y);
+                            x[i].z ^= pos_bits(y[j].z);
+                            x[i].w ^= pos_bits(y[j].w);
+                        }
+                    } else if (c < a.m) {
+                        const uint32_t *e = a.ev + (size_t)a.m0 * D0 + (size_t)(c - a.m0) * a.d1;
+                        for (int j = 0; j < a.d1; j++) {
+                            const uint4 y = *et_row(e[j]);
+                            x[i].x ^= pos_bits(y.x);
+                            x[i].y ^= pos_bits(y.y);
+                            x[i].z ^= pos_bits(y.z);
+                            x[i].w ^= pos_bits(y.w);
+                        }
+                    }
+                }
+                acc.x |= x[0].x | x[1].x;
+                acc.y |= x[0].y | x[1].y;
+                acc.z |= x[0].z | x[1].z;
+                acc.w |= x[0].w | x[1].w;
+            }
+            const uint32_t f = high_bits16(acc) & live;
+            if (f) atomicOr(&et_sh[1], f);
+            __syncthreads();
+            const uint32_t fail = et_sh[1];
+            __syncthreads();
+            if ((fail & live) == live) break;   // every live codeword has a failing check
+        }
+        const uint32_t fresh = live & ~et_sh[1];   // converged after this iteration
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            et_sh[0] = live & ~fresh;
+            et_sh[1] = 0;
+        }
+        if (fresh) {
+            if (threadIdx.x < CW && ((fresh >> threadIdx.x) & 1u)) a.iters_used[wg * CW + threadIdx.x] = it + 1;
+            // snapshot of the fresh codewords' bytes of every row (Vs: V layout)
+            const uint4 M = byte_mask16(fresh);
+            char *vs = (char *)a.Vs + (size_t)wg * CW;
+#pragma unroll 8
+            for (int r = threadIdx.x; r < a.n; r += NT) {
+                uint4 *d = (uint4 *)(vs + (size_t)r * (size_t)a.pitch);
+                *d = blend16(*d, *et_row((uint32_t)r), M);
+            }
+        }
+        __syncthreads();
+        return (live & ~fresh) != 0 && it + 1 < a.iters;
+    };
+    // the end (ET): converged codewords take their snapshot back
+    auto et_merge = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int valid = min(CW, max(0, a.batch - wg * CW));
+        const uint32_t conv = ((1u << valid) - 1u) & ~et_sh[0];
+        if (conv) {
+            const uint4 M = byte_mask16(conv);
+            const char *vs = (const char *)a.Vs + (size_t)wg * CW;
+#pragma unroll 8
+            for (int r = threadIdx.x; r < a.n; r += NT) {
+                uint4 *d = (uint4 *)et_row((uint32_t)r);
+                *d = blend16(*d, *(const uint4 *)(vs + (size_t)r * (size_t)a.pitch), M);
+            }
+        }
     };
     // stamps (diagnostic build): per wave 8 words: busy, phases 1..3 (slab:
     // vmcnt, first and second half), -, elapsed, -, G
@@ -543,28 +691,33 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             for (int i = 0; i < CPL; i++)
                 if (lane + 64 * i < NCH) dma16(src + 64 * i + lane, dst + 1024 * i);
         };
-        for (int w = 0; w < KAHEAD; w++) stage(w % a.nw, w);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint32_t w4[4] = {0, 0, 0, 0};
-        w4[0] = (uint32_t)(int)a.V[(size_t)a.x0 * (uint32_t)a.pitch + (uint32_t)(wg * CW + c)] & 0xFFFFu;
-        int un = KAHEAD % a.nw;
-        __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 in LDS
-        __syncthreads();   // prologue 2: constants of window 0 in LDS
         const bool cl = lane < CW;
-        if (STAMP) t0 = stamp3();
-        for (int p = 0; p <= G; p++) {
-            if (STAMP) tx = stamp3();
+        for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
+            for (int w = 0; w < KAHEAD; w++) stage(w % a.nw, w);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t w4[4] = {0, 0, 0, 0};
+            // the chain's first input V[x0] (a parity row: in P during the decode)
+            w4[0] = (uint32_t)(int)((const int8_t *)et_row((uint32_t)a.x0))[c] & 0xFFFFu;
+            int un = KAHEAD % a.nw;
+            __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 in LDS
+            __syncthreads();   // prologue 2: constants of window 0 in LDS
+            if (STAMP) t0 = stamp3();
+            for (int p = 0; p <= G; p++) {
+                if (STAMP) tx = stamp3();
 #ifndef C3X_NOCHAIN   // timing experiment only: results are wrong
-            if (p < G && cl) chain_window3<WS, R, 0, NB>(sm, p & 1, c, w4);
+                if (p < G && cl) chain_window3<WS, R, 0, NB>(sm, p & 1, c, w4);
 #endif
-            if (STAMP) sP[0] += stamp3() - tx;
-            stage(un, (p + KAHEAD) & (TQ - 1));
-            un = (un + 1 == a.nw) ? 0 : un + 1;
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPL * DPER) : "memory");
-            if (STAMP) sA += stamp3() - tx;
-            __syncthreads();
+                if (STAMP) sP[0] += stamp3() - tx;
+                stage(un, (p + KAHEAD) & (TQ - 1));
+                un = (un + 1 == a.nw) ? 0 : un + 1;
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPL * DPER) : "memory");
+                if (STAMP) sA += stamp3() - tx;
+                __syncthreads();
+            }
+            if (!ET || !et_after(it)) break;
         }
         write_stamps();
+        if (ET) et_merge();
         parity_out();
         return;
     }
@@ -606,151 +759,155 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                                            (q & 1) * 8)};
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     constexpr int NI = CF::NI, NS = CF::NS;
-    __syncthreads();   // prologue 1: tables in LDS
-    St3 st[NS];
-    uint4 mfc;   // records D0 .. D0+3 of the next pre's window
-    {
-        PfIn pi;
+    for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
+        __syncthreads();   // prologue 1: tables in LDS
+        St3 st[NS];
+        uint4 mfc;   // records D0 .. D0+3 of the next pre's window
+        {
+            PfIn pi;
 #pragma unroll
-        for (int i = 0; i <= R; i++) {   // window i -> in[w][i]   (nw > R + 3)
-            sl.read_pf(i, pi);
-            sl.gathers(pi, i);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        PreIn in;
-        sl.read_pre(0, 0, in, sl.read_mf(0), mfc);
-        sl.mask_early(0, in.mf);
-        sl.fwd_read(0, in);
-        if (a.tail == 0)
-            sl.template pre<true>(0, in, st[0]);
-        else
-            sl.template pre<false>(0, in, st[0]);
-    }
-    __syncthreads();   // prologue 2
-    if (STAMP) t0 = stamp3();
-    int uA = a.nw - 1;   // local index of window p-1 (post)
-    int uB = 1 % a.nw;   // local index of window p+1 (pre)
-    StIn sc;             // the stores of window p-2 (read from the stage at the end of period p-1)
-    bool sc_tl = false;  // ... window p-2 is the tail
-    // Period p: post of window p-1 (state st[(p-1) % NS], x inputs from the
-    // chain's window p-1) -> staged outputs; pre of window p+1 (inputs
-    // in[w][(p+1) % NI], -> st[(p+1) % NS]).  Vector memory: the two stores of
-    // window p-2 go first, the two LDS-DMA gathers of window p+1+R into
-    // in[w][(p+1+R) % NI] follow the first half, so no wave ends a period
-    // queueing behind the workgroup's stores (the CU's vector-memory issue is
-    // what bounds this kernel at the end of a period).
-    // The plan only keeps neighbouring windows free of shared information
-    // variables (dist 1): a value window p+1 reads may have been written by
-    // the post of window p-1 in this same period.  The host puts every such
-    // source and reader in slab wave 0, which posts before its pre and reads
-    // those values back from its own stage (LDS keeps a wave's order); the
-    // other waves run their pre first, so their x inputs arrive behind it.
-    // A value is stored at the start of the second period after its window's
-    // chain, so reads 2 .. R+3 windows later are forwarded (plan depth R + 2).
-    // The gathers of window p+1 were the last vector memory operations of
-    // period p-R, followed by 4 in each later period: in the main loop (every
-    // period does everything, no tail window) vmcnt(4(R-1)) covers them.
-    auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
-        constexpr int s = decltype(sc_)::value;   // p % U
-        constexpr bool GU = decltype(guarded)::value;
-        if (STAMP) tx = stampL();
-        const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G, dst = p >= 2 && p <= G + 1;
-        const bool fast = !GU && uA != a.tail && uB != a.tail && !sc_tl;
-        PreIn in;
-        PfIn pi;
-        St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
-        unsigned long long t1 = 0, t2 = 0, t3 = 0;
-        if (fast) {
-            // every read of the period that does not depend on this period's
-            // own writes goes first (one exposed LDS latency): the gathers of
-            // window p+1 have landed (the vmcnt count of the main loop),
-            // chain inputs of window p-1, records of window p+1+R
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1)) : "memory");
-            if (STAMP) t1 = stampL();
-            sl.stores(sc, false);
-            const uint32_t xr = sl.read_x(p - 1, sp);
-            sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
-            sl.read_pf(p + 1 + R, pi);
-            if (sw == 0) {
-                C3_MARK("post0");
-                sl.template post<false>(p - 1, xr, sp);
-                sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values
-                sl.gathers(pi, (s + R + 1) % NI);
-                sl.read_st(p - 1, sc);
-                if (STAMP) t2 = stampL();
-                C3_MARK("pre0");
-                sl.template pre<false>(p + 1, in, sn);
-            } else {
-                sl.fwd_read(p + 1, in);   // windows <= p-2, staged before the barrier
-                C3_MARK("pre");
-                sl.template pre<false>(p + 1, in, sn);
-                sl.gathers(pi, (s + R + 1) % NI);
-                if (STAMP) t2 = stampL();
-                C3_MARK("post");
-                sl.template post<false>(p - 1, xr, sp);
-                sl.read_st(p - 1, sc);
+            for (int i = 0; i <= R; i++) {   // window i -> in[w][i]   (nw > R + 3)
+                sl.read_pf(i, pi);
+                sl.gathers(pi, i);
             }
-            if (STAMP) t3 = stampL();
-            C3_MARK("end");
-        } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (dst) sl.stores(sc, sc_tl);
-            if (dpo) {
-                if (uA == a.tail)
-                    sl.template post<true>(p - 1, sl.read_x(p - 1, sp), sp);
-                else
-                    sl.template post<false>(p - 1, sl.read_x(p - 1, sp), sp);
-            }
-            if (STAMP) t1 = t2 = t3 = stampL();
-            if (dpo) {
-                sl.read_st(p - 1, sc);
-                sc_tl = uA == a.tail;
-            }
-            if (dpr) {
-                sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
-                if (p + 1 < R + 3) sl.mask_early(p + 1, in.mf);
-                sl.fwd_read(p + 1, in);
-                sl.read_pf(p + 1 + R, pi);
-                if (uB == a.tail)
-                    sl.template pre<true>(p + 1, in, sn);
-                else
-                    sl.template pre<false>(p + 1, in, sn);
-                sl.gathers(pi, (s + R + 1) % NI);
-            }
+            PreIn in;
+            sl.read_pre(0, 0, in, sl.read_mf(0), mfc);
+            sl.mask_early(0, in.mf);
+            sl.fwd_read(0, in);
+            if (a.tail == 0)
+                sl.template pre<true>(0, in, st[0]);
+            else
+                sl.template pre<false>(0, in, st[0]);
         }
-        if (STAMP) {
-            const unsigned long long t5 = stampL();
-            sA += t5 - tx;
+        __syncthreads();   // prologue 2
+        if (STAMP) t0 = stamp3();
+        int uA = a.nw - 1;   // local index of window p-1 (post)
+        int uB = 1 % a.nw;   // local index of window p+1 (pre)
+        StIn sc;             // the stores of window p-2 (read from the stage at the end of period p-1)
+        bool sc_tl = false;  // ... window p-2 is the tail
+        // Period p: post of window p-1 (state st[(p-1) % NS], x inputs from the
+        // chain's window p-1) -> staged outputs; pre of window p+1 (inputs
+        // in[w][(p+1) % NI], -> st[(p+1) % NS]).  Vector memory: the two stores of
+        // window p-2 go first, the two LDS-DMA gathers of window p+1+R into
+        // in[w][(p+1+R) % NI] follow the first half, so no wave ends a period
+        // queueing behind the workgroup's stores (the CU's vector-memory issue is
+        // what bounds this kernel at the end of a period).
+        // The plan only keeps neighbouring windows free of shared information
+        // variables (dist 1): a value window p+1 reads may have been written by
+        // the post of window p-1 in this same period.  The host puts every such
+        // source and reader in slab wave 0, which posts before its pre and reads
+        // those values back from its own stage (LDS keeps a wave's order); the
+        // other waves run their pre first, so their x inputs arrive behind it.
+        // A value is stored at the start of the second period after its window's
+        // chain, so reads 2 .. R+3 windows later are forwarded (plan depth R + 2).
+        // The gathers of window p+1 were the last vector memory operations of
+        // period p-R, followed by 4 in each later period: in the main loop (every
+        // period does everything, no tail window) vmcnt(4(R-1)) covers them.
+        auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
+            constexpr int s = decltype(sc_)::value;   // p % U
+            constexpr bool GU = decltype(guarded)::value;
+            if (STAMP) tx = stampL();
+            const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G, dst = p >= 2 && p <= G + 1;
+            const bool fast = !GU && uA != a.tail && uB != a.tail && !sc_tl;
+            PreIn in;
+            PfIn pi;
+            St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
+            unsigned long long t1 = 0, t2 = 0, t3 = 0;
             if (fast) {
-                sP[0] += t1 - tx;
-                sP[1] += t2 - t1;
-                sP[2] += t3 - t2;
+                // every read of the period that does not depend on this period's
+                // own writes goes first (one exposed LDS latency): the gathers of
+                // window p+1 have landed (the vmcnt count of the main loop),
+                // chain inputs of window p-1, records of window p+1+R
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1)) : "memory");
+                if (STAMP) t1 = stampL();
+                sl.stores(sc, false);
+                const uint32_t xr = sl.read_x(p - 1, sp);
+                sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
+                sl.read_pf(p + 1 + R, pi);
+                if (sw == 0) {
+                    C3_MARK("post0");
+                    sl.template post<false>(p - 1, xr, sp);
+                    sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values
+                    sl.gathers(pi, (s + R + 1) % NI);
+                    sl.read_st(p - 1, sc);
+                    if (STAMP) t2 = stampL();
+                    C3_MARK("pre0");
+                    sl.template pre<false>(p + 1, in, sn);
+                } else {
+                    sl.fwd_read(p + 1, in);   // windows <= p-2, staged before the barrier
+                    C3_MARK("pre");
+                    sl.template pre<false>(p + 1, in, sn);
+                    sl.gathers(pi, (s + R + 1) % NI);
+                    if (STAMP) t2 = stampL();
+                    C3_MARK("post");
+                    sl.template post<false>(p - 1, xr, sp);
+                    sl.read_st(p - 1, sc);
+                }
+                if (STAMP) t3 = stampL();
+                C3_MARK("end");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (dst) sl.stores(sc, sc_tl);
+                if (dpo) {
+                    if (uA == a.tail)
+                        sl.template post<true>(p - 1, sl.read_x(p - 1, sp), sp);
+                    else
+                        sl.template post<false>(p - 1, sl.read_x(p - 1, sp), sp);
+                }
+                if (STAMP) t1 = t2 = t3 = stampL();
+                if (dpo) {
+                    sl.read_st(p - 1, sc);
+                    sc_tl = uA == a.tail;
+                }
+                if (dpr) {
+                    sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
+                    if (p + 1 < R + 3) sl.mask_early(p + 1, in.mf);
+                    sl.fwd_read(p + 1, in);
+                    sl.read_pf(p + 1 + R, pi);
+                    if (uB == a.tail)
+                        sl.template pre<true>(p + 1, in, sn);
+                    else
+                        sl.template pre<false>(p + 1, in, sn);
+                    sl.gathers(pi, (s + R + 1) % NI);
+                }
             }
-        }
-        __syncthreads();
-        next(uA);
-        next(uB);
-    };
-    using T = std::true_type;
-    using F = std::false_type;
-    // periods 0 .. U guarded (their pres drop codes whose source window
-    // precedes window 0: U + 2 >= R + 3, the largest forwarding distance)
-    static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
-        if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, T{}, decltype(jc)::value);
-    });
-    int p = U + 1;
-    // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U
-    for (; p + U - 1 <= G - 2; p += U)
-        static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
-            period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, F{}, p + decltype(jc)::value);
+            if (STAMP) {
+                const unsigned long long t5 = stampL();
+                sA += t5 - tx;
+                if (fast) {
+                    sP[0] += t1 - tx;
+                    sP[1] += t2 - t1;
+                    sP[2] += t3 - t2;
+                }
+            }
+            __syncthreads();
+            next(uA);
+            next(uB);
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        // periods 0 .. U guarded (their pres drop codes whose source window
+        // precedes window 0: U + 2 >= R + 3, the largest forwarding distance)
+        static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
+            if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, T{}, decltype(jc)::value);
         });
-    // the rest (at most U + 1 periods: p .. G), guarded
-    static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
-        if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)
-            period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
-    });
-    sl.stores(sc, sc_tl);   // window G-1
+        int p = U + 1;
+        // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U
+        for (; p + U - 1 <= G - 2; p += U)
+            static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
+                period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, F{}, p + decltype(jc)::value);
+            });
+        // the rest (at most U + 1 periods: p .. G), guarded
+        static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
+            if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)
+                period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
+        });
+        sl.stores(sc, sc_tl);   // window G-1
+        if (!ET || !et_after(it)) break;
+    }
     write_stamps();
+    if (ET) et_merge();
     parity_out();
 }
 
@@ -904,6 +1061,8 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
     cc->tail = pl.tail;
     cc->n_fwd = pl.n_fwd;
     cc->x0 = (int)h->edge_var[h->check_start[0] + X];
+    cc->m0 = h->group_cnt[0];
+    cc->d1 = h->group_deg[1];
     return LDPC_OK;
 }
 
@@ -913,6 +1072,15 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
 {
     if (!cc.valid || !coop3_stride_ok(L.stride)) return -1;
+    if (L.early && cc.S == 48) {
+        // in-kernel early termination (one launch, coop3_decode<.., ET>)
+        if (!L.Vs || !L.iters_used) return -1;
+        if (L.iters == 0) {
+            hipLaunchKernelGGL(fill_iters3_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used, 0);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        }
+        return launch_coop3_iters(L, cc, L.iters, nullptr, s);
+    }
     if (L.early) {
         // one launch per iteration; converged codewords keep iterating inside
         // live workgroups, so their V is snapshot when they converge and
@@ -946,6 +1114,14 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.k = L.n - L.m;
     a.x0 = cc.x0;
     a.P = L.P;
+    const bool et = L.early && live == nullptr;   // in-kernel early termination
+    a.ev = L.d_edge_var;
+    a.Vs = L.Vs;
+    a.iters_used = L.iters_used;
+    a.iters = iters;
+    a.batch = L.batch;
+    a.m0 = cc.m0;
+    a.d1 = cc.d1;
     a.rmm = (uint32_t)(L.msg_max * 256 + 255) * 0x00010001u;
     a.coff = (uint32_t)(L.param * 256) * 0x00010001u;
     a.offp = (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
@@ -961,6 +1137,11 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
     int rc;
+    if (et) {
+        if (stamped) (void)hipFree(a.stamps);
+        hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (ws == 6)
         rc = launch_wsr<6, 2>(a, grid, stamped, s);
     else if (ws == 4)

@@ -31,6 +31,9 @@ struct DecodeLaunch {
     // [stride / 16][m + 1][16 codewords]: consecutive checks' parity values
     // are contiguous per codeword group (the kernel copies them in and out)
     int8_t *P;
+    // dynamic LDS bytes added to the windowed2 launch (mixed batches: keeps its
+    // waves off the CUs of a concurrent coop3 decode, see ldpc_ctx_set_lds_pad)
+    int lds_pad;
 };
 
 int launch_generic(const DecodeLaunch &L, hipStream_t s);

@@ -34,6 +34,9 @@ struct ldpc_code {
     std::vector<int8_t> chain_in, chain_out;
 };
 
+// windowed2 dynamic-LDS pad of a context (capi.hip; mixed batches)
+int ldpc_ctx_set_lds_pad(ldpc_ctx *c, int bytes);
+
 // error reporting (capi.cpp)
 int ldpc_set_error(int status, const char *fmt, ...);
 

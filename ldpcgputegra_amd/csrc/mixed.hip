@@ -110,6 +110,22 @@ extern "C" int ldpc_mixed_create(const ldpc_code *const *codes, int n_codes, int
             return ldpc_set_error(LDPC_ENOMEM, "mixed: staging buffers");
         }
     }
+    // a coop3 decode (one 124.5-KB workgroup per CU, VALU-bound slab waves)
+    // runs slower with other rates' windowed2 waves on its CUs: those get an
+    // LDS pad that keeps them off (LDPC_MIXED_LDS_PAD bytes, default 40 KB > the
+    // 35.5 KB a coop3 workgroup leaves; 0 = off)
+    std::vector<bool> c3(nc, false);
+    bool any_c3 = false;
+    for (int c = 0; c < n_codes; c++) {
+        c3[c] = ldpc_ctx_set_kernel(mx->ctx[c], 8) == LDPC_OK;
+        (void)ldpc_ctx_set_kernel(mx->ctx[c], 0);
+        any_c3 = any_c3 || c3[c];
+    }
+    const char *pp = getenv("LDPC_MIXED_LDS_PAD");
+    const int pad = (pp && *pp) ? atoi(pp) : 40 * 1024;
+    if (any_c3 && pad > 0)
+        for (int c = 0; c < n_codes; c++)
+            if (!c3[c]) (void)ldpc_ctx_set_lds_pad(mx->ctx[c], pad);
     if (hipEventCreateWithFlags(&mx->fork, hipEventDisableTiming) != hipSuccess) {
         ldpc_mixed_destroy(mx);
         return ldpc_set_error(LDPC_EDEVICE, "mixed: event");

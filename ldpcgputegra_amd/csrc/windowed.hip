@@ -393,7 +393,7 @@ void windowed_code_free(WindowedCode *w)
 size_t windowed_msg_bytes(const ldpc_code *h, int stride)
 {
     // one compressed word per check: 19 header bits + one sign bit per edge
-    return (size_t)h->m * stride * (h->max_deg + 19 <= 32 ? 4 : 8);
+    return (size_t)h->m * stride * (h->max_deg + 19 < 32 ? 4 : 8);   // windowed2 MsgT
 }
 
 int launch_windowed(const DecodeLaunch &L, const WindowedCode &w, hipStream_t s)

@@ -131,9 +131,13 @@ struct Tab {
     uint32_t meta;
 };
 
-// compressed message word: 19 header bits + one sign bit per edge
+// compressed message word: 19 header bits + one sign bit per edge.  Both
+// degree groups of a code must use the same word (the tail check's word sits
+// in the same Mc array): D0 = 14 needs 33 bits, so its tail (D = 13) takes 64
+// bits as well -- hence u32 only up to D = 12 (the kernel's degrees: 7 / 6,
+// 10 / 9 in u32; 14 / 13, 22 / 21, 27 / 26, 30 / 29 in u64)
 template <int D>
-using MsgT = typename std::conditional<(D + 19 <= 32), uint32_t, uint64_t>::type;
+using MsgT = typename std::conditional<(D + 19 < 32), uint32_t, uint64_t>::type;
 
 template <int D>
 struct Buf {
@@ -447,7 +451,8 @@ int windowed2_upload(const ldpc_code *h, int S, int P, Windowed2Code *w)
     *w = Windowed2Code{};
     std::vector<ldpc_window> wins;
     if (!(h->staircase && h->n_groups == 2 && h->group_deg[1] == h->group_deg[0] - 1 &&
-          (h->group_deg[0] == 7 || h->group_deg[0] == 10 || h->group_deg[0] == 27 || h->group_deg[0] == 30)))
+          (h->group_deg[0] == 7 || h->group_deg[0] == 10 || h->group_deg[0] == 14 || h->group_deg[0] == 22 ||
+           h->group_deg[0] == 27 || h->group_deg[0] == 30)))
         return LDPC_OK;
     extern int ldpc_plan_windows(const ldpc_code *h, int S, int P, std::vector<ldpc_window> &out);
     if (ldpc_plan_windows(h, S, P, wins) != LDPC_OK || wins.empty()) return LDPC_OK;
@@ -502,9 +507,9 @@ void windowed2_free(Windowed2Code *w)
 }
 
 template <int D0, int S, int P>
-static int launch3(const W2Args &a, int grid, hipStream_t s)
+static int launch3(const W2Args &a, int grid, hipStream_t s, int lds_pad)
 {
-    hipLaunchKernelGGL((windowed2_decode<D0, S, P>), dim3(grid), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((windowed2_decode<D0, S, P>), dim3(grid), dim3(64), (size_t)lds_pad, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -526,15 +531,19 @@ int launch_windowed2(const DecodeLaunch &L, const Windowed2Code &w, hipStream_t 
     const int G = 64 / w.S;
     const int grid = L.stride / G;   // stride % 64 == 0 -> grid % 8 == 0
     if (w.S == 32) {
-        if (w.d0 == 7) return launch3<7, 32, 1>(a, grid, s);
-        if (w.d0 == 10) return launch3<10, 32, 1>(a, grid, s);
-        if (w.d0 == 27) return launch3<27, 32, 1>(a, grid, s);
-        if (w.d0 == 30) return launch3<30, 32, 1>(a, grid, s);
+        if (w.d0 == 7) return launch3<7, 32, 1>(a, grid, s, L.lds_pad);
+        if (w.d0 == 10) return launch3<10, 32, 1>(a, grid, s, L.lds_pad);
+        if (w.d0 == 14) return launch3<14, 32, 1>(a, grid, s, L.lds_pad);
+        if (w.d0 == 22) return launch3<22, 32, 1>(a, grid, s, L.lds_pad);
+        if (w.d0 == 27) return launch3<27, 32, 1>(a, grid, s, L.lds_pad);
+        if (w.d0 == 30) return launch3<30, 32, 1>(a, grid, s, L.lds_pad);
     } else {
-        if (w.d0 == 7) return launch3<7, 16, 2>(a, grid, s);
-        if (w.d0 == 10) return launch3<10, 16, 2>(a, grid, s);
-        if (w.d0 == 27) return launch3<27, 16, 2>(a, grid, s);
-        if (w.d0 == 30) return launch3<30, 16, 2>(a, grid, s);
+        if (w.d0 == 7) return launch3<7, 16, 2>(a, grid, s, L.lds_pad);
+        if (w.d0 == 10) return launch3<10, 16, 2>(a, grid, s, L.lds_pad);
+        if (w.d0 == 14) return launch3<14, 16, 2>(a, grid, s, L.lds_pad);
+        if (w.d0 == 22) return launch3<22, 16, 2>(a, grid, s, L.lds_pad);
+        if (w.d0 == 27) return launch3<27, 16, 2>(a, grid, s, L.lds_pad);
+        if (w.d0 == 30) return launch3<30, 16, 2>(a, grid, s, L.lds_pad);
     }
     return -1;
 }

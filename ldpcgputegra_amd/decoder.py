@@ -25,6 +25,20 @@ import numpy as np
 from . import _lib
 from .codes import Code
 
+def pinned_empty(shape, dtype):
+    """numpy array in page-locked host memory (ldpc_host_alloc, the
+    reference's CUDA_MALLOC_HOST): the host-buffer decodes copy it by DMA,
+    overlapped with the decodes of the other chunks.  Freed with the array."""
+    import weakref
+    dt = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dt.itemsize
+    ptr = C.c_void_p()
+    _lib.check(_lib.lib().ldpc_host_alloc(C.byref(ptr), max(nbytes, 1)))
+    buf = (C.c_char * max(nbytes, 1)).from_address(ptr.value)
+    weakref.finalize(buf, _lib.lib().ldpc_host_free, ptr)
+    return np.frombuffer(buf, dtype=dt, count=int(np.prod(shape))).reshape(shape)
+
+
 class Decoder:
     """One C-ABI decoder context (device scratch for ``max_batch`` codewords)."""
 

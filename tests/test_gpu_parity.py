@@ -78,7 +78,8 @@ def _torch():
 
 
 @pytest.mark.parametrize("code", ["576x288", "648x324", "1944x972", "2048x384", "1024x518", "1200x600", "200x100",
-                                  "dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r9_10", "16200x7560"])
+                                  "dvbs2_r1_2", "dvbs2_r2_3", "dvbs2_r9_10", "16200x7560", "dvbs2shape_r3_4",
+                                  "dvbs2shape_r5_6"])
 @pytest.mark.parametrize("batch", [1, 37, 64])
 def test_soft_output_bit_exact_vs_oracle(code, batch):
     torch = _torch()
@@ -160,12 +161,15 @@ def test_algorithms_vs_oracle(algo, param):
         assert np.array_equal(got, exp), "kernel %d" % k
 
 
-@pytest.mark.parametrize("code", ["576x288", "648x324", "dvbs2_r1_2"])
+ET_EBN0 = {"dvbs2_r1_2": 1.0, "dvbs2shape_r3_4": 2.8, "dvbs2shape_r5_6": 3.5}
+
+
+@pytest.mark.parametrize("code", ["576x288", "648x324", "dvbs2_r1_2", "dvbs2shape_r3_4", "dvbs2shape_r5_6"])
 def test_early_termination_vs_oracle(code):
     torch = _torch()
     t = load_table(code)
     batch = 24
-    sigma = channel.sigma_from_ebn0(1.0 if t.n > 10000 else 2.0, t.k_info / t.n)
+    sigma = channel.sigma_from_ebn0(ET_EBN0.get(code, 2.0), t.k_info / t.n)
     llr = channel.awgn_i8_host(t.n, batch, seed=3, table=channel.i8_table(sigma))
     ref_hard, ref_soft, ref_its = O.decode_i8(t, llr, 30, O.OMS, 1, early_term=True, return_soft=True)
     assert ref_its.min() < 30                                # some codewords stop early
@@ -445,3 +449,40 @@ def test_dvbs2_batch_above_coop2_cap_vs_reference():
         assert dec.last_kernel != "coop2" and dec.last_skipped == "coop2"
     finally:
         del os.environ["LDPC_DEFAULT_COOP3"]
+
+
+def test_host_path_chunked_vs_device():
+    """The host-buffer API (ldpc_decode_i8 / _f32) decodes a batch in chunks on
+    copy/decode lanes (decode_host): its output equals the device API's on the
+    same LLRs for pageable and pinned (ldpc_host_alloc) buffers, 1 .. 5 chunks
+    and a ragged last chunk; configs[2]'s full 4096-codeword batch included
+    (the device path is pinned against the reference by
+    test_dvbs2_full_batch_vs_reference)."""
+    torch = _torch()
+    from ldpcgputegra_amd import pinned_empty
+    t = load_table("dvbs2_r1_2")
+    B = 4096
+    dec = decoder("dvbs2_r1_2", 0, B)
+    table = channel.i8_table(channel.sigma_from_ebn0(1.0, 0.5))
+    llr = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
+    dec.awgn_i8_device(llr, 0, 78, table)
+    hd = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+    dec.decode_i8_device(llr, hd, 50)
+    exp = hd.cpu().numpy()
+    host = llr.cpu().numpy()
+    assert np.array_equal(dec.decode_i8(host, 50), exp)                      # pageable, 4 chunks
+    pin_in, pin_out = pinned_empty((B, t.n), np.int8), pinned_empty((B, t.n), np.uint8)
+    pin_in[:] = host
+    try:
+        for chunks, b in (("1", 1000), ("3", 1000), ("5", 1400), ("2", B)):
+            os.environ["LDPC_HOST_CHUNKS"] = chunks
+            dec.decode_i8(pin_in[:b], 50, out=pin_out[:b])
+            assert np.array_equal(pin_out[:b], exp[:b]), (chunks, b)
+    finally:
+        del os.environ["LDPC_HOST_CHUNKS"]
+    f = load_table("648x324")
+    fd = decoder("648x324", 0, 1000)
+    y = (-1.0 + 0.8 * np.random.default_rng(3).standard_normal((1000, f.n))).astype(np.float32)
+    hf = torch.empty((1000, f.n), dtype=torch.uint8, device="cuda")
+    fd.decode_f32_device(torch.from_numpy(y).cuda(), hf, 20)
+    assert np.array_equal(fd.decode_f32(y, 20), hf.cpu().numpy())

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """PCIe-inclusive rate of the host-buffer boundary (ldpc_decode_i8 /
-ldpc_decode_f32: pageable host LLRs in, host hard decisions out, synchronous,
-as the reference's CDecoder::decode(char*, char*, int) is called).  Not the
-bench value (bench.py keeps inputs resident in HBM); recorded in DESIGN.md.
-usage (GPU box): python tools/host_path_rate.py"""
+ldpc_decode_f32: host LLRs in, host hard decisions out, synchronous, as the
+reference's CDecoder::decode(char*, char*, int) is called), with pageable
+and with pinned (ldpc_host_alloc) buffers, against the resident rate (the
+same decode on device buffers).  Not the bench value (bench.py keeps inputs
+resident in HBM); recorded in DESIGN.md.
+usage (GPU box): python tools/host_path_rate.py [chunks ...]"""
 import json
 import os
 import sys
@@ -12,32 +14,51 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from ldpcgputegra_amd import ALGO_MS, Code, Decoder, channel, default_params  # noqa: E402
+from ldpcgputegra_amd import ALGO_MS, Code, Decoder, channel, default_params, pinned_empty  # noqa: E402
 
 
-def rate(code_name, batch, iters, is_float, reps=5):
+def rate(code_name, batch, iters, is_float, pinned, reps=5):
+    import torch
     code = Code(code_name)
     dec = Decoder(code, max_batch=batch)
     sigma = channel.sigma_from_ebn0(1.0, code.k_info / code.n)
+    dt = np.float32 if is_float else np.int8
     if is_float:
-        llr = (-1.0 + sigma * np.random.default_rng(1).standard_normal((batch, code.n))).astype(np.float32)
-        run = lambda: dec.decode_f32(llr, iters, default_params(algo=ALGO_MS))   # noqa: E731
+        src = (-1.0 + sigma * np.random.default_rng(1).standard_normal((batch, code.n))).astype(np.float32)
+        p = default_params(algo=ALGO_MS)
     else:
-        llr = channel.awgn_i8_host(code.n, batch, 1, channel.i8_table(sigma))
-        run = lambda: dec.decode_i8(llr, iters)   # noqa: E731
+        src = channel.awgn_i8_host(code.n, batch, 1, channel.i8_table(sigma))
+        p = default_params()
+    llr = pinned_empty(src.shape, dt) if pinned else np.empty(src.shape, dt)
+    llr[:] = src
+    hard = pinned_empty((batch, code.n), np.uint8) if pinned else np.empty((batch, code.n), np.uint8)
+    run = (lambda: dec.decode_f32(llr, iters, p, out=hard)) if is_float else (lambda: dec.decode_i8(llr, iters, p, out=hard))
     run()
-    dec.profile(True)
-    dec.kernel_time(reset=True)
     t0 = time.perf_counter()
     for _ in range(reps):
         run()
     el = (time.perf_counter() - t0) / reps
-    kms, n = dec.kernel_time(reset=True)
+    # resident: the same decode on device buffers
+    d_llr, d_hard = torch.from_numpy(src).cuda(), torch.empty((batch, code.n), dtype=torch.uint8, device="cuda")
+    dev = (lambda: dec.decode_f32_device(d_llr, d_hard, iters, p)) if is_float else (
+        lambda: dec.decode_i8_device(d_llr, d_hard, iters, p))
+    dev()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dev()
+    torch.cuda.synchronize()
+    el_dev = (time.perf_counter() - t0) / reps
     return dict(code=code_name, batch=batch, iters=iters, dtype="f32" if is_float else "int8",
-                kernel=dec.last_kernel, ms_per_call=round(el * 1e3, 3), kernel_ms=round(kms / max(n, 1), 3),
-                host_path_mbps=round(batch * code.n / el / 1e6, 1))
+                buffers="pinned" if pinned else "pageable", chunks=os.environ.get("LDPC_HOST_CHUNKS", "default"),
+                kernel=dec.last_kernel, ms_per_call=round(el * 1e3, 3), resident_ms=round(el_dev * 1e3, 3),
+                host_path_mbps=round(batch * code.n / el / 1e6, 1),
+                resident_mbps=round(batch * code.n / el_dev / 1e6, 1), host_over_resident=round(el_dev / el, 3))
 
 
 if __name__ == "__main__":
-    for args in (("dvbs2_r1_2", 4096, 50, False), ("648x324", 1024, 20, True)):
-        print(json.dumps(rate(*args)), flush=True)
+    for ch in (sys.argv[1:] or ["2"]):
+        os.environ["LDPC_HOST_CHUNKS"] = ch
+        for args in (("dvbs2_r1_2", 4096, 50, False), ("648x324", 1024, 20, True)):
+            for pinned in (False, True):
+                print(json.dumps(rate(*args, pinned)), flush=True)
