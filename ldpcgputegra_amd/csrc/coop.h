@@ -31,12 +31,17 @@ int coop_plan_windows(const ldpc_code *h, int S, int R, int dist, std::vector<in
 
 // ---- window plan shared by coop.hip and coop2.hip ----
 // Slot record [recw] u32: edge variables [D0], meta, forwarding codes (u16 per
-// information edge: dW << 9 | slot << 3 | edge; 0xFFFF = none).
+// information edge: dW << (6 + EB) | slot << EB | edge, EB = coop_fwd_eb(X);
+// 0xFFFF = none); codes with more than 8 information edges (X > 8) carry the
+// ring-source bits in the record word after the codes (coop_src_word), not in
+// the meta word.
 constexpr uint32_t COOP_M_ACT = 1u << 20;            // slot holds a check
 constexpr uint32_t COOP_M_FWD = 1u << 21;            // an info edge of the slot reads the LDS ring
 constexpr int COOP_SRC_SHIFT = 22;                   // bit 22 + j: info edge j feeds the LDS ring
 constexpr uint32_t COOP_CHK_MASK = (1u << 20) - 1;   // check index
 constexpr uint32_t COOP_FWD_NONE = 0xFFFFu;
+constexpr int coop_fwd_eb(int X) { return X > 8 ? 5 : 3; }          // edge bits of a forwarding code
+constexpr int coop_src_word(int D0) { return D0 + 1 + (D0 - 1) / 2; }   // X > 8: the source-bits word
 
 struct CoopPlan {
     std::vector<int> first, count;   // per window: first check, checks (0: empty window)

@@ -36,6 +36,7 @@
 //   gfx950 workgroup-scope memory model needs no vmcnt wait for that).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "coop.h"
@@ -53,12 +54,21 @@ template <int D0>
 struct Geo {
     static constexpr int X = D0 - 2;                          // info edges of a group-0 check
     static constexpr int NFW = (X + 1) / 2;                   // dwords of u16 forwarding codes
-    static constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;   // record: vars, meta, fwd (16-B multiple)
+    static constexpr bool WIDE = X > 8;                       // ring-source bits in a record word of their own
+    static constexpr int EB = coop_fwd_eb(X);                 // edge bits of a forwarding code
+    static constexpr int RECW = (D0 + 1 + NFW + (WIDE ? 1 : 0) + 3) / 4 * 4;   // vars, meta, fwd (, src)
+    static_assert(!WIDE || coop_src_word(D0) == D0 + 1 + NFW, "source-bits word");
 };
+
+// compressed message word: cst1 | cst2 << 7 | jmin << 14 | sign_j << (19 + j),
+// 64 bits when the degree needs them (one width per code: the tail check's
+// word sits in the same array)
+template <int D0>
+using CMsg = typename std::conditional<(D0 + 19 <= 32), uint32_t, uint64_t>::type;
 
 struct CoopArgs {
     int8_t *V;             // V[n + 1][stride]; row n receives masked stores
-    uint32_t *Mc;          // Mc[stride / 16][m][16], then a 1024-word sink
+    void *Mc;              // CMsg<D0> Mc[stride / 16][m][16], then a 512-word sink
     const uint32_t *tab;   // [nw][S][RECW] slot records
     const uint8_t *live;   // [stride] early termination: 0 = codeword frozen (NULL: all live)
     int stride, G, nw, tail, m, n, off, mm, remap;
@@ -87,6 +97,13 @@ LDPC_DEV int dec_msg(uint32_t w, int j, int c1, int c2, int jm)
     const int sm = ((int)(w << (12 - j))) >> 31;   // bit 19 + j
     return (mag ^ sm) - sm;
 }
+LDPC_DEV int dec_msg(uint64_t w, int j, int c1, int c2, int jm)
+{
+    const int mag = (jm == j) ? c1 : c2;
+    const int sm = j < 13 ? ((int)((uint32_t)w << (12 - j))) >> 31
+                          : ((int)((uint32_t)(w >> 32) << (44 - j))) >> 31;   // bit 19 + j
+    return (mag ^ sm) - sm;
+}
 
 template <int D0, int WS, int R>
 struct alignas(16) Smem {
@@ -101,20 +118,23 @@ struct alignas(16) Smem {
 template <int D0>
 struct Pf {                       // prefetched inputs of one window (raw bytes: the
     uint32_t v[D0 - 1];           // sign extension happens at the use, so no wait
-    uint32_t m;                   // is forced right after the load); info, o; message
+    CMsg<D0> m;                   // is forced right after the load); info, o; message
 };
 
 template <int D0>
 struct St {                       // one window's state between pre and post
     int c[D0 - 1];                // contributions c_j (info, o); tail: new V values
     int a[D0 - 1];                // |c_j| clipped
-    int mx, min1, min2, sacc;     // tail: sacc = new message word
+    int mx, min1, min2, sacc;     // tail, 32-bit words: sacc = the new message word
+    uint32_t twh;                 // tail, 64-bit words: its high half
 };
 
 template <int D0, int WS, int R>
 struct Slab {
     using SM = Smem<D0, WS, R>;
     static constexpr int S = SM::S, X = SM::X, RECW = SM::RECW, TQ = SM::TQ, NFW = Geo<D0>::NFW;
+    static constexpr int EB = Geo<D0>::EB;
+    using W = CMsg<D0>;
     SM &sm;
     const CoopArgs &a;
     int k, c;
@@ -138,7 +158,7 @@ struct Slab {
         for (int j = 0; j < X; j++) pf.v[j] = V4[(var[j] * st + b) >> 2];
         const uint32_t vo = (u == a.tail) ? var[X] : var[D0 - 1];
         pf.v[X] = V4[(vo * st + b) >> 2];
-        pf.m = a.Mc[mcbase + (meta & CHK_MASK) * CW];
+        pf.m = ((const W *)a.Mc)[mcbase + (meta & CHK_MASK) * CW];
     }
 
     // pre of window g: forwarding, contributions, chain constants
@@ -156,14 +176,14 @@ struct Slab {
 #pragma unroll
             for (int j = 0; j < X; j++) {
                 const uint32_t code = (fw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu;
-                const int dw = (int)(code >> 9);
+                const int dw = (int)(code >> (6 + EB));
                 if (code != FWD_NONE && g >= dw) {
                     const int q = (g - dw) % R;
-                    v[j] = (int8_t)sm.ring[q][(code >> 3) & 63][code & 7][c];
+                    v[j] = (int8_t)sm.ring[q][(code >> EB) & 63][code & ((1u << EB) - 1)][c];
                 }
             }
         }
-        const uint32_t w = pf.m;
+        const W w = pf.m;
         const int c1 = (int)(w & 127), c2 = (int)((w >> 7) & 127), jm = (int)((w >> 14) & 31);
         const int off = a.off, mm = a.mm;
         int eps, A, B, co, L, H;
@@ -223,7 +243,7 @@ struct Slab {
             }
             const int cst1 = min(max(min2 - off, 0), mm), cst2 = min(max(min1 - off, 0), mm);
             const int P = sacc ^ (((D0 - 1) & 1) ? (int)0x80000000 : 0);
-            uint32_t nw = (uint32_t)cst1 | ((uint32_t)cst2 << 7);
+            W nw = (W)cst1 | ((W)cst2 << 7);
             int jmin = 0;
 #pragma unroll
             for (int j = 0; j <= X; j++) {
@@ -233,10 +253,12 @@ struct Slab {
                 const int t = s.c[j] ^ P;
                 const int sm = t >> 31;
                 const int lsb = (int)((uint32_t)t >> 31);
-                nw |= (uint32_t)lsb << (19 + j);
+                nw |= (W)lsb << (19 + j);
                 s.c[j] = clamp127(s.c[j] + (rr ^ sm) + lsb);
             }
-            s.sacc = (int)(nw | ((uint32_t)jmin << 14));
+            nw |= (W)jmin << 14;
+            s.sacc = (int)(uint32_t)nw;
+            if constexpr (sizeof(W) == 8) s.twh = (uint32_t)(nw >> 32);
             const int y = s.c[X];
             eps = 0;
             A = B = co = L = H = y;
@@ -263,7 +285,7 @@ struct Slab {
         const bool tl = (u == a.tail);
         const int xin = sm.xin[g & 1][c][k];
         int vn[D0];
-        uint32_t nw;
+        W nw;
         if (!tl) {
             const int off = a.off, mm = a.mm;
             const int cx = clamp127(clamp127(xin) - s.mx);
@@ -273,7 +295,7 @@ struct Slab {
             const int min1 = min(ax, s.min1);
             const int cst1 = max(min2 - off, 0), cst2 = max(min1 - off, 0);   // <= msg_max already
             const int P = sacc ^ ((D0 & 1) ? (int)0x80000000 : 0);
-            nw = (uint32_t)cst1 | ((uint32_t)cst2 << 7);
+            nw = (W)cst1 | ((W)cst2 << 7);
             int jmin = 0;
 #pragma unroll
             for (int j = 0; j < D0; j++) {
@@ -285,15 +307,16 @@ struct Slab {
                 const int t = cj ^ P;
                 const int sm = t >> 31;
                 const int lsb = (int)((uint32_t)t >> 31);
-                nw |= (uint32_t)lsb << (19 + j);
+                nw |= (W)lsb << (19 + j);
                 vn[j] = clamp127(cj + (rr ^ sm) + lsb);
             }
-            nw |= (uint32_t)jmin << 14;
+            nw |= (W)jmin << 14;
         } else {
 #pragma unroll
             for (int j = 0; j <= X; j++) vn[j] = s.c[j];
             vn[D0 - 1] = clamp127(xin);   // V of the last group-0 check's o edge (only the chain had it)
-            nw = (uint32_t)s.sacc;
+            nw = (W)(uint32_t)s.sacc;
+            if constexpr (sizeof(W) == 8) nw |= (W)s.twh << 32;
         }
         // Stores: edges 0..D0-2 (info + x; the tail: info + o).  A group-0 o
         // store is dead (the next check rewrites the variable through its x
@@ -303,10 +326,15 @@ struct Slab {
 #pragma unroll
         for (int j = 0; j < D0 - 1; j++) a.V[act ? var[j] * st + b : vsink] = (int8_t)vn[j];
         if (tl) a.V[act ? var[D0 - 1] * st + b : vsink] = (int8_t)vn[D0 - 1];
-        a.Mc[act ? mcbase + (meta & CHK_MASK) * CW : mcsink] = nw;
+        ((W *)a.Mc)[act ? mcbase + (meta & CHK_MASK) * CW : mcsink] = nw;
+        uint32_t srcb;
+        if constexpr (Geo<D0>::WIDE)
+            srcb = r[coop_src_word(D0)];
+        else
+            srcb = meta >> SRC_SHIFT;
 #pragma unroll
         for (int j = 0; j < X; j++)
-            if ((meta >> (SRC_SHIFT + j)) & 1) sm.ring[g % R][k][j][c] = (uint8_t)vn[j];
+            if ((srcb >> j) & 1) sm.ring[g % R][k][j][c] = (uint8_t)vn[j];
     }
 };
 
@@ -357,34 +385,43 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
     if (wave == WS) {
         // ------------------------------------------------------------ chain wave
         constexpr int NCH = S * RECW / 4;   // 16-B chunks per window table
-        static_assert(NCH <= 128, "window table too large for two chunks per lane");
+        constexpr int CPL = (NCH + 63) / 64;   // chunks per lane
         const int c = lane & 15;
-        const int i0 = min(lane, NCH - 1), i1 = min(lane + 64, NCH - 1);
-        auto load = [&](int u, uint4 &t0, uint4 &t1) {
+        static_assert(CPL <= 4, "window table: at most 4 chunks per lane");
+        // one window table in flight, CPL 16-B chunks per lane (named
+        // registers: an indexed array here ends up in scratch)
+        uint4 t0, t1, t2, t3;
+        auto load = [&](int u) {
             const uint4 *src = (const uint4 *)(a.tab + (size_t)u * S * RECW);
-            t0 = src[i0];
-            t1 = src[i1];
+            t0 = src[min(lane, NCH - 1)];
+            if constexpr (CPL > 1) t1 = src[min(lane + 64, NCH - 1)];
+            if constexpr (CPL > 2) t2 = src[min(lane + 128, NCH - 1)];
+            if constexpr (CPL > 3) t3 = src[min(lane + 192, NCH - 1)];
         };
-        auto store = [&](int slot, const uint4 &t0, const uint4 &t1) {
+        auto store = [&](int slot) {
             uint4 *dst = (uint4 *)&sm.tab[slot][0][0];
             if (lane < NCH) dst[lane] = t0;
-            if (lane + 64 < NCH) dst[lane + 64] = t1;
+            if constexpr (CPL > 1)
+                if (lane + 64 < NCH) dst[lane + 64] = t1;
+            if constexpr (CPL > 2)
+                if (lane + 128 < NCH) dst[lane + 128] = t2;
+            if constexpr (CPL > 3)
+                if (lane + 192 < NCH) dst[lane + 192] = t3;
         };
-        uint4 t0, t1;
         for (int q = 0; q <= R + 1; q++) {
-            load(q % a.nw, t0, t1);
-            store(q, t0, t1);
+            load(q % a.nw);
+            store(q);
         }
         int Y = a.V[a.tab[X] * (uint32_t)a.stride + (uint32_t)(wg * CW + c)];   // x input of the first check
-        load((R + 2) % a.nw, t0, t1);
+        load((R + 2) % a.nw);
         int un = (R + 3) % a.nw;
         __syncthreads();   // prologue: tables in LDS
         __syncthreads();   // pre(0) done: constants of window 0 in LDS
         const bool cl = lane < CW;   // the chain runs on 16 lanes
         for (int p = 0; p <= G; p++) {
             if (p < G && cl) chain_steps<D0, WS, R, 0, SPLIT>(sm, p, c, Y);
-            store((p + R + 2) % TQ, t0, t1);
-            load(un, t0, t1);
+            store((p + R + 2) % TQ);
+            load(un);
             un = (un + 1 == a.nw) ? 0 : un + 1;
             __syncthreads();   // A
             if (p < G && cl) chain_steps<D0, WS, R, SPLIT, S>(sm, p, c, Y);
@@ -614,7 +651,9 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPl
     if (S < 1 || S > 64 || R < 1 || R > 6 || dist < 1 || dist > 2) return -1;   // forwarding code: 6-bit slot
     if (!h->staircase || h->n_groups != 2 || h->group_cnt[1] != 1) return -1;
     const int D0 = h->group_deg[0], X = D0 - 2, M = h->m, T = M - 1;
-    if (h->group_deg[1] != D0 - 1 || X < 1 || X > 8 || M < 4 || M >= (1 << 20)) return -1;
+    if (h->group_deg[1] != D0 - 1 || X < 1 || X > 28 || M < 4 || M >= (1 << 20)) return -1;
+    const int EB = coop_fwd_eb(X);
+    if (want_tab && X > 8 && recw <= coop_src_word(D0)) return -1;
     auto ev = [&](int c, int j) { return h->edge_var[h->check_start[c] + j]; };
     // staircase: x edge (D0-2) of check c is the o edge (D0-1) of check c-1;
     // the x edge of check 0 is the tail's last edge
@@ -697,7 +736,7 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPl
                         if (dW <= dist) return -1;   // violates the window rule
                         if (dW > dist && dW <= R + dist) {
                             const int w = gw % nw;
-                            fwd[((size_t)u * S + k) * X + j] = (uint16_t)(dW << 9 | lk[v] << 3 | lj[v]);
+                            fwd[((size_t)u * S + k) * X + j] = (uint16_t)(dW << (6 + EB) | lk[v] << EB | lj[v]);
                             src[(size_t)w * S + lk[v]] |= 1u << lj[v];
                             o.n_fwd++;
                         }
@@ -728,7 +767,11 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPl
                 uint32_t &d = rec[D0 + 1 + j / 2];
                 d = (j & 1) ? ((d & 0xFFFFu) | ((uint32_t)f << 16)) : ((d & 0xFFFF0000u) | f);
             }
-            rec[D0] = (uint32_t)cc | M_ACT | (any ? M_FWD : 0u) | (src[(size_t)u * S + k] << SRC_SHIFT);
+            rec[D0] = (uint32_t)cc | M_ACT | (any ? M_FWD : 0u);
+            if (X > 8)
+                rec[coop_src_word(D0)] = src[(size_t)u * S + k];
+            else
+                rec[D0] |= src[(size_t)u * S + k] << SRC_SHIFT;
         }
     return 0;
 }
@@ -736,12 +779,15 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPl
 namespace {
 
 constexpr int kWS = 7;   // slab waves: S = 28 checks per window
-constexpr int kR = 3;    // prefetch depth (windows)
+// prefetch depth (windows): 3, or 2 for degree 22 (R + 1 prefetched windows of
+// 21 V dwords per lane would not fit the 256 VGPRs of two waves per SIMD)
+constexpr int coop_r(int d0) { return d0 > 16 ? 2 : 3; }
 
 template <int D0>
 int launch_d0(const CoopArgs &a, int grid, hipStream_t s)
 {
-    hipLaunchKernelGGL((coop_decode<D0, kWS, kR>), dim3(grid), dim3(64 * (kWS + 1)), 0, s, a);
+    constexpr int R = coop_r(D0);
+    hipLaunchKernelGGL((coop_decode<D0, kWS, R>), dim3(grid), dim3(64 * (kWS + 1)), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -780,10 +826,14 @@ int coop_upload(const ldpc_code *h, CoopCode *cc)
         recw = Geo<7>::RECW;
     else if (d0 == 10)
         recw = Geo<10>::RECW;
+    else if (d0 == 14)
+        recw = Geo<14>::RECW;
+    else if (d0 == 22)
+        recw = Geo<22>::RECW;
     else
         return LDPC_OK;
     CoopPlan pl;
-    if (coop_build_plan(h, 4 * kWS, kR, 1, recw, pl, true) != 0) return LDPC_OK;
+    if (coop_build_plan(h, 4 * kWS, coop_r(d0), 1, recw, pl, true) != 0) return LDPC_OK;
     if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop tables");
     if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         coop_free(cc);
@@ -792,7 +842,7 @@ int coop_upload(const ldpc_code *h, CoopCode *cc)
     cc->valid = 1;
     cc->d0 = d0;
     cc->S = 4 * kWS;
-    cc->R = kR;
+    cc->R = coop_r(d0);
     cc->nw = (int)pl.first.size();
     cc->tail = pl.tail;
     cc->n_fwd = pl.n_fwd;
@@ -810,7 +860,7 @@ static int launch_coop_iters(const DecodeLaunch &L, const CoopCode &cc, int iter
 {
     CoopArgs a;
     a.V = (int8_t *)L.V;
-    a.Mc = (uint32_t *)L.msg;
+    a.Mc = L.msg;
     a.tab = cc.d_tab;
     a.stride = L.stride;
     a.G = cc.nw * iters;
@@ -825,6 +875,8 @@ static int launch_coop_iters(const DecodeLaunch &L, const CoopCode &cc, int iter
     a.remap = (grid % 8) == 0;
     if (cc.d0 == 7) return launch_d0<7>(a, grid, s);
     if (cc.d0 == 10) return launch_d0<10>(a, grid, s);
+    if (cc.d0 == 14) return launch_d0<14>(a, grid, s);
+    if (cc.d0 == 22) return launch_d0<22>(a, grid, s);
     return -1;
 }
 

@@ -40,7 +40,7 @@ def kernels_for(code):
         ks.append(2)
     if c.window_plan(16, 2):
         ks += [3, 4]
-    if c.coop_plan() is not None and c.max_deg in (7, 10):
+    if c.coop_plan() is not None and c.max_deg in (7, 10, 14, 22):
         ks.append(5)
     if c.coop_plan(24, 3) is not None and c.max_deg == 7:
         ks.append(6)
