@@ -177,6 +177,56 @@ MIXED_EBN0 = {"dvbs2_r1_2": 1.0, "dvbs2_r2_3": 2.2, "dvbs2_r8_9": 4.6, "dvbs2_r9
               "dvbs2shape_r3_4": 2.8, "dvbs2shape_r5_6": 3.5}
 
 
+def cpu_baseline_mixed(names, frames, iters, budget_s, threads, seed):
+    """configs[4] on the host: the reference SSE decoder (oracle/_ref) of each
+    rate it can be built for, at FIXED `iters` iterations (code/x86's decoder
+    has no early termination: its arret test is commented out,
+    CDecoder_OMS_fixed_SSE.cpp:551-553), 16-frame decode() calls on `threads`
+    threads, budget_s / len(names) seconds each.  Rates without a reference
+    build (r2/3, the DVB-S2-shaped r3/4 and r5/6) are priced at the measured
+    per-edge cost of the rates that have one (edge counts: 226,799 for r1/2
+    and shaped r3/4, 237,599 for shaped r5/6) -- a stated estimate."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from ldpcgputegra_amd import channel, load_table
+    per_rate, ns_per_edge = [], []
+    for name in names:
+        if not O.ref_available(name):
+            continue
+        t = load_table(name)
+        blk = 16 * threads
+        llr = channel.awgn_i8_host(t.n, blk, seed, channel.i8_table(channel.sigma_from_ebn0(3.0, t.k_info / t.n)))
+        O.ref_decode_mt(name, llr, iters, 1, threads)   # untimed: library load, first touch, thread start
+        done, t0 = 0, time.perf_counter()
+        while True:
+            O.ref_decode_mt(name, llr, iters, 1, threads)
+            done += blk
+            el = time.perf_counter() - t0
+            if el >= budget_s / len(names):
+                break
+        cw_s = done / el
+        ns_per_edge.append(el / (done * t.e * iters) * 1e9)
+        per_rate.append(dict(code=name, codewords_per_s=round(cw_s, 1), mbps=round(cw_s * t.n / 1e6, 3)))
+    if not per_rate:
+        return None
+    npe = sum(ns_per_edge) / len(ns_per_edge)
+    tot = 0.0
+    for name, f in zip(names, frames):
+        t = load_table(name)
+        hit = [r for r in per_rate if r["code"] == name]
+        tot += f / hit[0]["codewords_per_s"] if hit else f * t.e * iters * npe * 1e-9
+    host = host_cpu_info()
+    n = load_table(names[0]).n
+    return dict(value=round(sum(frames) * n / tot / 1e6, 3), unit="Mbit/s", cores=threads, kind="reference",
+                threads=threads, cpu_model=host["model"], host_physical_cores=host["physical_cores"],
+                cpu_quota=host["cpu_quota"], per_rate=per_rate,
+                sample="reference SSE decoder at fixed %d iterations (no early termination in code/x86), 16-frame "
+                       "decode() calls on %d threads, ~%.0f s per rate with a build (%s); rates without one (%s) "
+                       "priced at the measured %.3f ns per edge-iteration (estimate)" % (
+                           iters, threads, budget_s / len(names), ", ".join(r["code"] for r in per_rate),
+                           ", ".join(x for x in names if x not in [r["code"] for r in per_rate]) or "none", npe))
+
+
 def bench_mixed(a, rank, world, local, torch, dist):
     """configs[4]: one batch of B codewords per GPU mixing DVB-S2 normal-frame
     rates (MIXED_SETS[a.mixed_codes]), codeword c using rate c % len(codes),
@@ -256,12 +306,24 @@ def bench_mixed(a, rank, world, local, torch, dist):
                        "parallelism": "codeword shards x%d (no collective)" % world},
             "per_rate": per_rate,
             "ber": be / max(world * bits, 1), "fer": fe / max(frames / a.steps, 1),
-            # whole-step rate (several kernels on concurrent streams): no single dominant launch
+            # whole-step rate (several kernels on concurrent streams): no single dominant launch;
+            # traffic = HBM bytes per step over all its kernels (PMC, profiles/traffic.json)
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": hbm_peak_gbs(), "unit": "GB/s",
                          "frac": round(achieved / hbm_peak_gbs(), 4), "traffic": None, "kernel_ms": None,
                          "algorithmic_bytes_per_step": alg_bytes},
             "cpu_baseline": None,
         }
+        try:
+            tr = json.load(open(a.traffic_file))
+            out["roofline"]["traffic"] = tr.get("mixed_%s_b%d_it%d" % (a.mixed_codes, B, a.iters),
+                                                {}).get("hbm_bytes_per_step")
+        except (OSError, ValueError):
+            pass
+        if world == 1 and a.cpu_seconds > 0:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            out["cpu_baseline"] = cpu_baseline_mixed(list(names), [r["frames"] for r in per_rate], a.iters,
+                                                     a.cpu_seconds, a.cpu_threads or O.host_threads(), a.seed)
         print(json.dumps(out), flush=True)
     mx.close()
 

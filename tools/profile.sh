@@ -34,6 +34,8 @@ for p in $PASSES; do
     tlb) run tlb 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS TCP_UTCL1_TRANSLATION_HIT TCP_UTCL1_REQUEST TCP_UTCL1_STALL_MULTI_MISS --kernel-include-regex "$KRE" -f csv -d $OUT/tlb -o run -- python3 bench.py $ARGS ;;
     tcplat) run tcplat 600 rocprofv3 --pmc TCP_TCC_WRITE_REQ_LATENCY TCP_TCC_READ_REQ_LATENCY TCP_TCC_WRITE_REQ TCP_TCC_READ_REQ TA_ADDR_STALLED_BY_TC_CYCLES TA_BUSY --kernel-include-regex "$KRE" -f csv -d $OUT/tcplat -o run -- python3 bench.py $ARGS ;;
     tcpstall) run tcpstall 600 rocprofv3 --pmc TCP_PENDING_STALL_CYCLES TCP_TCP_TA_DATA_STALL_CYCLES TCP_TCR_TCP_STALL_CYCLES TCP_UTCL1_SERIALIZATION_STALL TA_DATA_STALLED_BY_TC_CYCLES TA_TA_BUSY --kernel-include-regex "$KRE" -f csv -d $OUT/tcpstall -o run -- python3 bench.py $ARGS ;;
+    mixfetch) run mixfetch 600 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/mixfetch -o run -- python3 bench.py --mixed $ARGS ;;
+    mixwrite) run mixwrite 600 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/mixwrite -o run -- python3 bench.py --mixed $ARGS ;;
     list) timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true ;;
     tcc) run tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KRE" -f csv -d $OUT/tcc -o run -- python3 bench.py $ARGS ;;
     esac
