@@ -222,9 +222,10 @@ def cpu_baseline_mixed(names, frames, iters, budget_s, threads, seed):
                 cpu_quota=host["cpu_quota"], per_rate=per_rate,
                 sample="reference SSE decoder at fixed %d iterations (no early termination in code/x86), 16-frame "
                        "decode() calls on %d threads, ~%.0f s per rate with a build (%s); rates without one (%s) "
-                       "priced at the measured %.3f ns per edge-iteration (estimate)" % (
+                       "priced at the measured %.4f ns of %d-thread wall time per edge-iteration (estimate)" % (
                            iters, threads, budget_s / len(names), ", ".join(r["code"] for r in per_rate),
-                           ", ".join(x for x in names if x not in [r["code"] for r in per_rate]) or "none", npe))
+                           ", ".join(x for x in names if x not in [r["code"] for r in per_rate]) or "none", npe,
+                           threads))
 
 
 def bench_mixed(a, rank, world, local, torch, dist):

@@ -76,3 +76,33 @@ def test_two_rank_gloo_shards_match_single_process(tmp_path):
     el, be, fe, fr = red[0]
     assert el == pytest.approx(0.2)                         # max over ranks
     assert fr == total and be == ref[:, :t.k_info].sum()
+
+
+@pytest.mark.gpu
+def test_two_rank_bench_on_gpu_matches_single_process():
+    """bench.py's N > 1 path on hardware: torch.distributed.run with 2 ranks
+    (gloo, both on the box's one MI355X, LDPC_BENCH_BACKEND=gloo as the
+    driver's 8-GPU runs use RCCL), 256 DVB-S2 r1/2 codewords per rank, each
+    rank decoding its own contiguous shard on its own decoder context.  The
+    JSON line reports n_gpus 2 and whole-job BER / FER equal to one process
+    decoding the same 512 codewords (the shards cover exactly those)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    args = ["--batch", "256", "--iters", "10", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"]
+    env = dict(os.environ, LDPC_BENCH_BACKEND="gloo")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                          os.path.join(root, "bench.py"), "--gpus", "2"] + args,
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    two = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    args[1] = "512"
+    out1 = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=300, cwd=root)
+    assert out1.returncode == 0, out1.stderr[-2000:]
+    one = json.loads([l for l in out1.stdout.splitlines() if l.startswith("{")][-1])
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 512 and one["config"]["global_batch"] == 512
+    assert two["ber"] == one["ber"] and two["fer"] == one["fer"] and one["fer"] > 0
+    assert two["value"] > 0

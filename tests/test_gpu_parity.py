@@ -486,3 +486,25 @@ def test_host_path_chunked_vs_device():
     hf = torch.empty((1000, f.n), dtype=torch.uint8, device="cuda")
     fd.decode_f32_device(torch.from_numpy(y).cuda(), hf, 20)
     assert np.array_equal(fd.decode_f32(y, 20), hf.cpu().numpy())
+
+
+def test_context_per_device_and_bad_device():
+    """One context per device id (the multi-GPU layout): every
+    visible device decodes the same codewords bit-identically; a device id
+    beyond the visible ones is rejected with LDPC_EINVAL, not a crash."""
+    torch = _torch()
+    from ldpcgputegra_amd import LdpcError
+    from ldpcgputegra_amd import _lib
+    import ctypes as C
+    cnt = C.c_int()
+    _lib.check(_lib.lib().ldpc_device_count(C.byref(cnt)))
+    assert cnt.value >= 1
+    t = load_table("576x288")
+    llr = channel.awgn_i8_host(t.n, 40, seed=12, table=channel.i8_table(0.8))
+    exp = O.decode_i8(t, llr, 12)
+    for dev in range(cnt.value):
+        d = Decoder(Code("576x288"), device=dev, max_batch=64)
+        assert np.array_equal(d.decode_i8(llr, 12), exp), dev
+        d.close()
+    with pytest.raises(LdpcError):
+        Decoder(Code("576x288"), device=cnt.value, max_batch=64)
