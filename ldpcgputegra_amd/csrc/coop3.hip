@@ -234,7 +234,10 @@ struct Slab3 {
     LDPC_DEV void stores(const StIn &in, bool tl) const
     {
 #ifndef C3X_NOVSTORE   // timing experiment only: results are wrong
-#ifdef C3X_VSTORE2   // timing experiment: V row pieces as two 8-B stores
+#if defined(C3X_VSTORE_NT)   // experiment: V row pieces as non-temporal (streaming) stores
+        if (q < (tl ? D0 : D0 - 1))
+            __builtin_nontemporal_store(__builtin_bit_cast(i32x4, in.vd), (i32x4 *)(vsb + (size_t)in.row * vsm));
+#elif defined(C3X_VSTORE2)   // timing experiment: V row pieces as two 8-B stores
         if (q < (tl ? D0 : D0 - 1)) {
             uint2 *d = (uint2 *)(vsb + (size_t)in.row * vsm);
             d[0] = make_uint2(in.vd.x, in.vd.y);
@@ -253,7 +256,17 @@ struct Slab3 {
 #ifdef C3X_NOVLOAD   // timing experiment only: results are wrong
         if (lane >= 8 * X)
 #endif
+#ifdef C3X_DMA_NT   // experiment: V row gathers with the non-temporal policy
+        {
+            unsigned keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(g1base + (size_t)in.rv * g1mul), "s"(base)
+                         : "memory");
+        }
+#else
         dma16(g1base + (size_t)in.rv * g1mul, base);
+#endif
         if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + SM::IN_B);
     }
 
