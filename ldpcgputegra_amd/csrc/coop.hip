@@ -71,6 +71,11 @@ struct CoopArgs {
     void *Mc;              // CMsg<D0> Mc[stride / 16][m][16], then a 512-word sink
     const uint32_t *tab;   // [nw][S][RECW] slot records
     const uint8_t *live;   // [stride] early termination: 0 = codeword frozen (NULL: all live)
+    // in-kernel early termination (ET kernels): layered edge list (group 0:
+    // checks [0, m0) of degree D0, then degree d1), iterations used
+    const uint32_t *ev;
+    int32_t *iters_used;
+    int iters, batch, m0, d1;
     int stride, G, nw, tail, m, n, off, mm, remap;
 };
 
@@ -364,7 +369,26 @@ LDPC_DEV void chain_steps(Smem<D0, WS, R> &sm, int g, int c, int &Y)
     }
 }
 
-template <int D0, int WS, int R>
+// high bit of byte j set where byte j > 0 (hard decision), SWAR; 16 bytes ->
+// 16-bit codeword mask
+LDPC_DEV uint32_t pos_bits(uint32_t d)
+{
+    const uint32_t nz = ((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d;
+    return nz & ~d & 0x80808080u;
+}
+LDPC_DEV uint32_t high_bits16(uint4 x)
+{
+    auto c4 = [](uint32_t v) { return ((v >> 7) & 1u) | ((v >> 14) & 2u) | ((v >> 21) & 4u) | ((v >> 28) & 8u); };
+    return c4(x.x) | c4(x.y) << 4 | c4(x.z) << 8 | c4(x.w) << 12;
+}
+
+// ET = true: in-kernel early termination (as coop3_decode<.., ET>): one
+// iteration per segment, then the workgroup's syndrome of its live codewords
+// (stopping once each has a failing check); converged codewords' stores are
+// masked from the next segment on, which freezes their V and messages at the
+// iteration they converged (no snapshot needed); the workgroup leaves when
+// all 16 have converged
+template <int D0, int WS, int R, bool ET = false>
 __global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
 {
     using SM = Smem<D0, WS, R>;
@@ -377,10 +401,84 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
     const int lane = threadIdx.x & 63;
     const int nb = gridDim.x, id = blockIdx.x;
     const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
-    const int G = a.G;
+    const int G = ET ? a.nw : a.G;   // periods per segment (ET: one iteration)
     if (G == 0) return;
-    const bool live = a.live ? a.live[wg * CW + (lane & 15)] != 0 : true;
-    if (a.live && !__syncthreads_or(live)) return;   // all 16 codewords converged
+    bool live = (!ET && a.live) ? a.live[wg * CW + (lane & 15)] != 0 : true;
+    if (!ET && a.live && !__syncthreads_or(live)) return;   // all 16 codewords converged
+    // ---- ET state: [0] live codewords, [1] failing codewords (syndrome)
+    __shared__ uint32_t et_sh[2];
+    constexpr int NT = 64 * (WS + 1);
+    const char *etV = (const char *)a.V + (size_t)wg * CW;
+    if constexpr (ET) {
+        if (threadIdx.x == 0) {
+            const int valid = min(CW, max(0, a.batch - wg * CW));
+            et_sh[0] = (1u << valid) - 1u;
+            et_sh[1] = 0;
+        }
+        if (threadIdx.x < CW && wg * CW + (int)threadIdx.x < a.batch) a.iters_used[wg * CW + threadIdx.x] = a.iters;
+        __syncthreads();
+        if (et_sh[0] == 0) return;   // padding columns only
+        live = (et_sh[0] >> (lane & 15)) & 1u;
+    }
+    // after iteration `it` (ET): syndrome and decision, every thread, uniform
+    // result (true: decode another iteration)
+    auto et_after = [&](int it) -> bool {
+        __syncthreads();   // the iteration's stores were issued before the last barrier of the segment
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t lv = et_sh[0];
+        constexpr int CPT = D0 > 10 ? 1 : 2;   // checks per thread and round (VGPRs: D0 x 16 B each)
+        for (int c0 = 0; c0 < a.m; c0 += NT * CPT * 4) {
+            uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4 * CPT; r++) {
+                const int c = c0 + r * NT + (int)threadIdx.x;
+                uint4 x = make_uint4(0, 0, 0, 0);
+                if (c < a.m0) {
+                    const uint32_t *e = a.ev + (size_t)c * D0;
+                    uint4 y[D0];
+#pragma unroll
+                    for (int j = 0; j < D0; j++) y[j] = *(const uint4 *)(etV + (size_t)e[j] * (size_t)a.stride);
+#pragma unroll
+                    for (int j = 0; j < D0; j++) {
+                        x.x ^= pos_bits(y[j].x);
+                        x.y ^= pos_bits(y[j].y);
+                        x.z ^= pos_bits(y[j].z);
+                        x.w ^= pos_bits(y[j].w);
+                    }
+                } else if (c < a.m) {
+                    const uint32_t *e = a.ev + (size_t)a.m0 * D0 + (size_t)(c - a.m0) * a.d1;
+                    for (int j = 0; j < a.d1; j++) {
+                        const uint4 y = *(const uint4 *)(etV + (size_t)e[j] * (size_t)a.stride);
+                        x.x ^= pos_bits(y.x);
+                        x.y ^= pos_bits(y.y);
+                        x.z ^= pos_bits(y.z);
+                        x.w ^= pos_bits(y.w);
+                    }
+                }
+                acc.x |= x.x;
+                acc.y |= x.y;
+                acc.z |= x.z;
+                acc.w |= x.w;
+            }
+            const uint32_t f = high_bits16(acc) & lv;
+            if (f) atomicOr(&et_sh[1], f);
+            __syncthreads();
+            const uint32_t fail = et_sh[1];
+            __syncthreads();
+            if ((fail & lv) == lv) break;   // every live codeword has a failing check
+        }
+        const uint32_t fresh = lv & ~et_sh[1];   // converged after this iteration
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            et_sh[0] = lv & ~fresh;
+            et_sh[1] = 0;
+        }
+        if (threadIdx.x < CW && ((fresh >> threadIdx.x) & 1u)) a.iters_used[wg * CW + threadIdx.x] = it + 1;
+        __syncthreads();
+        live = (et_sh[0] >> (lane & 15)) & 1u;
+        return (lv & ~fresh) != 0 && it + 1 < a.iters;
+    };
 
     if (wave == WS) {
         // ------------------------------------------------------------ chain wave
@@ -408,24 +506,27 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
             if constexpr (CPL > 3)
                 if (lane + 192 < NCH) dst[lane + 192] = t3;
         };
-        for (int q = 0; q <= R + 1; q++) {
-            load(q % a.nw);
-            store(q);
-        }
-        int Y = a.V[a.tab[X] * (uint32_t)a.stride + (uint32_t)(wg * CW + c)];   // x input of the first check
-        load((R + 2) % a.nw);
-        int un = (R + 3) % a.nw;
-        __syncthreads();   // prologue: tables in LDS
-        __syncthreads();   // pre(0) done: constants of window 0 in LDS
         const bool cl = lane < CW;   // the chain runs on 16 lanes
-        for (int p = 0; p <= G; p++) {
-            if (p < G && cl) chain_steps<D0, WS, R, 0, SPLIT>(sm, p, c, Y);
-            store((p + R + 2) % TQ);
-            load(un);
-            un = (un + 1 == a.nw) ? 0 : un + 1;
-            __syncthreads();   // A
-            if (p < G && cl) chain_steps<D0, WS, R, SPLIT, S>(sm, p, c, Y);
-            __syncthreads();   // B
+        for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
+            for (int q = 0; q <= R + 1; q++) {
+                load(q % a.nw);
+                store(q);
+            }
+            int Y = a.V[a.tab[X] * (uint32_t)a.stride + (uint32_t)(wg * CW + c)];   // x input of the first check
+            load((R + 2) % a.nw);
+            int un = (R + 3) % a.nw;
+            __syncthreads();   // prologue: tables in LDS
+            __syncthreads();   // pre(0) done: constants of window 0 in LDS
+            for (int p = 0; p <= G; p++) {
+                if (p < G && cl) chain_steps<D0, WS, R, 0, SPLIT>(sm, p, c, Y);
+                store((p + R + 2) % TQ);
+                load(un);
+                un = (un + 1 == a.nw) ? 0 : un + 1;
+                __syncthreads();   // A
+                if (p < G && cl) chain_steps<D0, WS, R, SPLIT, S>(sm, p, c, Y);
+                __syncthreads();   // B
+            }
+            if (!ET || !et_after(it)) break;
         }
         return;
     }
@@ -435,75 +536,79 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
     Slab<D0, WS, R> sl{sm, a, k, c, (uint32_t)(wg * CW + c), (uint32_t)(wg * a.m * CW + c),
                        (uint32_t)a.n * (uint32_t)a.stride + (uint32_t)lane,
                        (uint32_t)nb * (uint32_t)a.m * CW + threadIdx.x, (c & 3) * 8, live};
-    Pf<D0> pf[R + 1];
-    St<D0> st[2];
-    __syncthreads();   // prologue: tables of windows 0 .. R+1 are in LDS
+    for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
+        sl.live = live;
+        Pf<D0> pf[R + 1];
+        St<D0> st[2];
+        __syncthreads();   // prologue: tables of windows 0 .. R+1 are in LDS
 #pragma unroll
-    for (int i = 0; i <= R; i++) sl.prefetch(i, i, pf[i]);   // nw > R + 3
-    sl.pre(0, 0, pf[0], st[0]);
-    // period 0: chain(0) | nothing to post | loads of R+1, pre(1)
-    __syncthreads();   // B of the prologue
-    __syncthreads();   // A(0)
-    sl.prefetch(R + 1, (R + 1) % a.nw, pf[0]);
-    sl.pre(1, 1, pf[1], st[1]);
-    __syncthreads();   // B(0)
-    int uA = 0, uB = 2 % a.nw, uP = (R + 2) % a.nw;   // windows p-1, p+1, p+1+R (local index)
-    auto next = [&](int &u) { u = (u + 1 == a.nw) ? 0 : u + 1; };
-    // steady state p = 1 .. G: every memory operation unconditional (loads past
-    // the end read valid table rows; their pre only writes unused constants)
-    auto step = [&](auto sc, int p) {
-        constexpr int s = decltype(sc)::value;
-        sl.post(p - 1, uA, st[s % 2]);
-        __syncthreads();   // A(p)
-        sl.prefetch(p + 1 + R, uP, pf[(s + 1) % (R + 1)]);
-        sl.pre(p + 1, uB, pf[(s + 2) % (R + 1)], st[s % 2]);
-        __syncthreads();   // B(p)
-        next(uA);
-        next(uB);
-        next(uP);
-    };
-    // single-exit loop over whole unroll groups (multi-exit loops get
-    // restructured and lose the precise wait counts), then the remainder
-    const int nfull = G / U;
-    int p = 1;
-    for (int i = 0; i < nfull; i++, p += U) {
-        step(std::integral_constant<int, 0>{}, p);
-        step(std::integral_constant<int, 1>{}, p + 1);
+        for (int i = 0; i <= R; i++) sl.prefetch(i, i, pf[i]);   // nw > R + 3
+        sl.pre(0, 0, pf[0], st[0]);
+        // period 0: chain(0) | nothing to post | loads of R+1, pre(1)
+        __syncthreads();   // B of the prologue
+        __syncthreads();   // A(0)
+        sl.prefetch(R + 1, (R + 1) % a.nw, pf[0]);
+        sl.pre(1, 1, pf[1], st[1]);
+        __syncthreads();   // B(0)
+        int uA = 0, uB = 2 % a.nw, uP = (R + 2) % a.nw;   // windows p-1, p+1, p+1+R (local index)
+        auto next = [&](int &u) { u = (u + 1 == a.nw) ? 0 : u + 1; };
+        // steady state p = 1 .. G: every memory operation unconditional (loads past
+        // the end read valid table rows; their pre only writes unused constants)
+        auto step = [&](auto sc, int p) {
+            constexpr int s = decltype(sc)::value;
+            sl.post(p - 1, uA, st[s % 2]);
+            __syncthreads();   // A(p)
+            sl.prefetch(p + 1 + R, uP, pf[(s + 1) % (R + 1)]);
+            sl.pre(p + 1, uB, pf[(s + 2) % (R + 1)], st[s % 2]);
+            __syncthreads();   // B(p)
+            next(uA);
+            next(uB);
+            next(uP);
+        };
+        // single-exit loop over whole unroll groups (multi-exit loops get
+        // restructured and lose the precise wait counts), then the remainder
+        const int nfull = G / U;
+        int p = 1;
+        for (int i = 0; i < nfull; i++, p += U) {
+            step(std::integral_constant<int, 0>{}, p);
+            step(std::integral_constant<int, 1>{}, p + 1);
+            if constexpr (U > 2) {
+                step(std::integral_constant<int, 2>{}, p + 2);
+                step(std::integral_constant<int, 3>{}, p + 3);
+            }
+            if constexpr (U > 4) {
+                step(std::integral_constant<int, 4>{}, p + 4);
+                step(std::integral_constant<int, 5>{}, p + 5);
+            }
+            if constexpr (U > 6) {
+                step(std::integral_constant<int, 6>{}, p + 6);
+                step(std::integral_constant<int, 7>{}, p + 7);
+            }
+            if constexpr (U > 8) {
+                step(std::integral_constant<int, 8>{}, p + 8);
+                step(std::integral_constant<int, 9>{}, p + 9);
+            }
+            static_assert(U <= 10, "unroll");
+        }
+        const int rem = G - nfull * U;
+        if (rem > 0) step(std::integral_constant<int, 0>{}, p);
+        if (rem > 1) step(std::integral_constant<int, 1>{}, p + 1);
         if constexpr (U > 2) {
-            step(std::integral_constant<int, 2>{}, p + 2);
-            step(std::integral_constant<int, 3>{}, p + 3);
+            if (rem > 2) step(std::integral_constant<int, 2>{}, p + 2);
+            if (rem > 3) step(std::integral_constant<int, 3>{}, p + 3);
         }
         if constexpr (U > 4) {
-            step(std::integral_constant<int, 4>{}, p + 4);
-            step(std::integral_constant<int, 5>{}, p + 5);
+            if (rem > 4) step(std::integral_constant<int, 4>{}, p + 4);
+            if (rem > 5) step(std::integral_constant<int, 5>{}, p + 5);
         }
         if constexpr (U > 6) {
-            step(std::integral_constant<int, 6>{}, p + 6);
-            step(std::integral_constant<int, 7>{}, p + 7);
+            if (rem > 6) step(std::integral_constant<int, 6>{}, p + 6);
+            if (rem > 7) step(std::integral_constant<int, 7>{}, p + 7);
         }
         if constexpr (U > 8) {
-            step(std::integral_constant<int, 8>{}, p + 8);
-            step(std::integral_constant<int, 9>{}, p + 9);
+            if (rem > 8) step(std::integral_constant<int, 8>{}, p + 8);
         }
-        static_assert(U <= 10, "unroll");
-    }
-    const int rem = G - nfull * U;
-    if (rem > 0) step(std::integral_constant<int, 0>{}, p);
-    if (rem > 1) step(std::integral_constant<int, 1>{}, p + 1);
-    if constexpr (U > 2) {
-        if (rem > 2) step(std::integral_constant<int, 2>{}, p + 2);
-        if (rem > 3) step(std::integral_constant<int, 3>{}, p + 3);
-    }
-    if constexpr (U > 4) {
-        if (rem > 4) step(std::integral_constant<int, 4>{}, p + 4);
-        if (rem > 5) step(std::integral_constant<int, 5>{}, p + 5);
-    }
-    if constexpr (U > 6) {
-        if (rem > 6) step(std::integral_constant<int, 6>{}, p + 6);
-        if (rem > 7) step(std::integral_constant<int, 7>{}, p + 7);
-    }
-    if constexpr (U > 8) {
-        if (rem > 8) step(std::integral_constant<int, 8>{}, p + 8);
+        if (!ET || !et_after(it)) break;
     }
 }
 
@@ -784,10 +889,13 @@ constexpr int kWS = 7;   // slab waves: S = 28 checks per window
 constexpr int coop_r(int d0) { return d0 > 16 ? 2 : 3; }
 
 template <int D0>
-int launch_d0(const CoopArgs &a, int grid, hipStream_t s)
+int launch_d0(const CoopArgs &a, int grid, hipStream_t s, bool et)
 {
     constexpr int R = coop_r(D0);
-    hipLaunchKernelGGL((coop_decode<D0, kWS, R>), dim3(grid), dim3(64 * (kWS + 1)), 0, s, a);
+    if (et)
+        hipLaunchKernelGGL((coop_decode<D0, kWS, R, true>), dim3(grid), dim3(64 * (kWS + 1)), 0, s, a);
+    else
+        hipLaunchKernelGGL((coop_decode<D0, kWS, R>), dim3(grid), dim3(64 * (kWS + 1)), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -843,6 +951,8 @@ int coop_upload(const ldpc_code *h, CoopCode *cc)
     cc->d0 = d0;
     cc->S = 4 * kWS;
     cc->R = coop_r(d0);
+    cc->m0 = h->group_cnt[0];
+    cc->d1 = h->group_deg[1];
     cc->nw = (int)pl.first.size();
     cc->tail = pl.tail;
     cc->n_fwd = pl.n_fwd;
@@ -856,9 +966,15 @@ void coop_free(CoopCode *cc)
 }
 
 static int launch_coop_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
-                             hipStream_t s)
+                             hipStream_t s, bool et = false)
 {
     CoopArgs a;
+    a.ev = L.d_edge_var;
+    a.iters_used = L.iters_used;
+    a.iters = iters;
+    a.batch = L.batch;
+    a.m0 = cc.m0;
+    a.d1 = cc.d1;
     a.V = (int8_t *)L.V;
     a.Mc = L.msg;
     a.tab = cc.d_tab;
@@ -873,10 +989,10 @@ static int launch_coop_iters(const DecodeLaunch &L, const CoopCode &cc, int iter
     a.mm = L.msg_max;
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0;
-    if (cc.d0 == 7) return launch_d0<7>(a, grid, s);
-    if (cc.d0 == 10) return launch_d0<10>(a, grid, s);
-    if (cc.d0 == 14) return launch_d0<14>(a, grid, s);
-    if (cc.d0 == 22) return launch_d0<22>(a, grid, s);
+    if (cc.d0 == 7) return launch_d0<7>(a, grid, s, et);
+    if (cc.d0 == 10) return launch_d0<10>(a, grid, s, et);
+    if (cc.d0 == 14) return launch_d0<14>(a, grid, s, et);
+    if (cc.d0 == 22) return launch_d0<22>(a, grid, s, et);
     return -1;
 }
 
@@ -888,6 +1004,19 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
             hipLaunchKernelGGL(fill_iters_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used,
                                L.iters);
         return launch_coop_iters(L, cc, L.iters, nullptr, s);
+    }
+    // early termination in the kernel (coop_decode<.., ET>): one launch
+    // (LDPC_COOP_ET_KERNEL=0: the per-iteration launches below)
+    static const bool in_kernel = [] {
+        const char *e = getenv("LDPC_COOP_ET_KERNEL");
+        return !(e && *e && atoi(e) == 0);
+    }();
+    if (in_kernel && L.iters_used) {
+        if (L.iters == 0) {
+            hipLaunchKernelGGL(fill_iters_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used, 0);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        }
+        return launch_coop_iters(L, cc, L.iters, nullptr, s, true);
     }
     // early termination: one launch per iteration (V, messages and the chain
     // input V[p_0] carry the state), then the syndrome of the live codewords

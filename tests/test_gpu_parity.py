@@ -288,13 +288,14 @@ def test_dvbs2_full_batch_vs_reference():
     assert np.array_equal(s1.cpu().numpy()[sel], ref_soft)
 
 
-@pytest.mark.parametrize("kernel", [6, 8])
+@pytest.mark.parametrize("kernel", [5, 6, 8])
 @pytest.mark.parametrize("batch,ebn0", [(40, 1.1), (64, 1.1), (1024, 1.0)])
 def test_coop2_early_termination_vs_oracle(batch, ebn0, kernel):
-    """coop2 (kernel 6) with early termination on whole and partial
-    workgroups and, at batch 1024 (grid 64), with the XCD block remap on, as
-    bench.py --mixed runs it: hard decisions, soft output and iterations used
-    all equal the oracle's (syndrome after every iteration)."""
+    """coop (5, in-kernel early termination), coop2 (6, per-iteration
+    launches) and coop3 (8, in-kernel) with early termination on whole and
+    partial workgroups and, at batch 1024 (grid 64), with the XCD block remap
+    on, as bench.py --mixed runs it: hard decisions, soft output and iterations
+    used all equal the oracle's (syndrome after every iteration)."""
     torch = _torch()
     t = load_table("dvbs2_r1_2")
     dec = decoder("dvbs2_r1_2", kernel, max(64, batch))
@@ -310,7 +311,7 @@ def test_coop2_early_termination_vs_oracle(batch, ebn0, kernel):
         dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, 50, params=default_params(early_term=1),
                              soft=d_soft, iters_used=d_its)
         torch.cuda.synchronize()
-        assert dec.last_kernel == {6: "coop2", 8: "coop3"}[kernel]
+        assert dec.last_kernel == {5: "coop", 6: "coop2", 8: "coop3"}[kernel]
         assert np.array_equal(d_its.cpu().numpy(), ref_its), rep
         assert np.array_equal(d_soft.cpu().numpy(), ref_soft), rep
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard), rep
