@@ -217,9 +217,18 @@ int ldpc_dvbs2_encode(const ldpc_code *h, const uint8_t *info, uint8_t *codeword
 /* ---- synthetic channel -------------------------------------------------- */
 /* sigma = sqrt(10^(-(EbN0 + 10 log10(rate))/10) / 2)  (CChanelAWGN_MKL.cpp:102-105) */
 double ldpc_awgn_sigma(double ebn0_db, double rate);
+/* the same with the reference's es_n0 option (:97-104): es_n0 != 0 reads
+ * snr_db as Es/N0 of a 2-bit (QPSK) symbol, Eb/N0 = Es/N0 - 10 log10(2 rate) */
+double ldpc_awgn_sigma_ex(double snr_db, double rate, int es_n0);
 /* Threshold table (63 entries) for the integer-exact quantised AWGN generator:
  * q = clamp(trunc(factor*y), -sat, sat), y = -1 + sigma*z (bit 0). */
 int ldpc_awgn_i8_table(double sigma, int factor, int sat, uint32_t *table /*[64]*/);
+/* General channel of CChanelAWGN_MKL::generate (:127-143): y = +-amp + sigma*z
+ * (amp 1 for BPSK, 0.707106781 for QPSK, one bit per real dimension) scaled by
+ * norm (1, or 2 / sigma^2 with the reference's normalize option, :114-121),
+ * then q = clamp(trunc(factor * y), -sat, sat); the same generators
+ * (ldpc_awgn_i8_host / _async) draw from it. */
+int ldpc_awgn_i8_table_ex(double sigma, double amp, double norm, int factor, int sat, uint32_t *table /*[64]*/);
 /* llr[b][i] for codewords first_cw .. first_cw+batch-1; codeword bits
  * (0/1, [batch][N]) or NULL for the all-zero codeword. */
 int ldpc_awgn_i8_host(int n, int batch, uint64_t first_cw, uint64_t seed, const uint32_t *table,

@@ -70,6 +70,8 @@ SIGNATURES = {
     "ldpc_dvbs2_encode": (I, [P, P, P, I]),
     "ldpc_awgn_sigma": (C.c_double, [C.c_double, C.c_double]),
     "ldpc_awgn_i8_table": (I, [C.c_double, I, I, P]),
+    "ldpc_awgn_sigma_ex": (C.c_double, [C.c_double, C.c_double, I]),
+    "ldpc_awgn_i8_table_ex": (I, [C.c_double, C.c_double, C.c_double, I, I, P]),
     "ldpc_awgn_i8_host": (I, [I, I, U64, U64, P, P, P]),
     "ldpc_awgn_i8_async": (I, [P, P, P, I, U64, U64, P, P]),
     "ldpc_count_errors_async": (I, [P, P, P, I, I, P, P]),

@@ -28,9 +28,23 @@ def sigma_from_ebn0(ebn0_db, rate):
     return float(_lib.lib().ldpc_awgn_sigma(float(ebn0_db), float(rate)))
 
 
-def i8_table(sigma, factor=8, sat=31):
+def sigma_from_snr(snr_db, rate, es_n0=False):
+    """CChanelAWGN_MKL::configure with its es_n0 option (:97-104)."""
+    return float(_lib.lib().ldpc_awgn_sigma_ex(float(snr_db), float(rate), int(bool(es_n0))))
+
+
+QPSK = 0.707106781   # CChanelAWGN_MKL.cpp:124
+BPSK = 1.0
+
+
+def i8_table(sigma, factor=8, sat=31, amp=BPSK, normalize=False):
+    """Thresholds of q = clamp(trunc(factor * norm * (-amp + sigma z)), +-sat):
+    BPSK / QPSK amplitude, norm = 2 / sigma^2 with the reference's normalize
+    option (CChanelAWGN_MKL.cpp:114-143), else 1."""
     t = np.empty(64, dtype=np.uint32)
-    _lib.check(_lib.lib().ldpc_awgn_i8_table(float(sigma), int(factor), int(sat), t.ctypes.data))
+    norm = 2.0 / (sigma * sigma) if normalize else 1.0
+    _lib.check(_lib.lib().ldpc_awgn_i8_table_ex(float(sigma), float(amp), float(norm), int(factor), int(sat),
+                                                t.ctypes.data))
     return t
 
 

@@ -365,19 +365,36 @@ extern "C" double ldpc_awgn_sigma(double ebn0_db, double rate)
     return std::sqrt(std::pow(10.0, interm) / 2.0);
 }
 
-// P(q <= v) for q = clamp(trunc(factor*y), -sat, sat), y = -1 + sigma*z.
-// trunc(f*y) <= v  <=>  y < (v+1)/f  (v >= 0)   or   y <= v/f  (v < 0).
+// CChanelAWGN_MKL::configure with its es_n0 option (:97-104): the SNR given in
+// Es/N0 (QPSK, 2 bits per symbol) is first turned into Eb/N0
+extern "C" double ldpc_awgn_sigma_ex(double snr_db, double rate, int es_n0)
+{
+    const double ebn0 = es_n0 ? snr_db - 10.0 * std::log10(2.0 * rate) : snr_db;
+    return ldpc_awgn_sigma(ebn0, rate);
+}
+
 extern "C" int ldpc_awgn_i8_table(double sigma, int factor, int sat, uint32_t *table)
 {
-    if (!table || sigma <= 0.0 || factor <= 0 || sat < 1 || sat > 31)
-        return ldpc_set_error(LDPC_EINVAL, "awgn table: sigma>0, factor>0, 1<=sat<=31");
+    return ldpc_awgn_i8_table_ex(sigma, 1.0, 1.0, factor, sat, table);
+}
+
+// P(q <= v) for q = clamp(trunc(factor * norm * y), -sat, sat),
+// y = -amp + sigma*z (bit 0; amp 1 BPSK, 0.707106781 QPSK, norm 1 or the
+// 2 / sigma^2 normalisation: CChanelAWGN_MKL::generate, :127-143, and
+// configure, :114-121).  With f = factor * norm:
+// trunc(f*y) <= v  <=>  y < (v+1)/f  (v >= 0)   or   y <= v/f  (v < 0).
+extern "C" int ldpc_awgn_i8_table_ex(double sigma, double amp, double norm, int factor, int sat, uint32_t *table)
+{
+    if (!table || sigma <= 0.0 || factor <= 0 || sat < 1 || sat > 31 || !(amp > 0.0) || !(norm > 0.0))
+        return ldpc_set_error(LDPC_EINVAL, "awgn table: sigma>0, amp>0, norm>0, factor>0, 1<=sat<=31");
+    const double f = (double)factor * norm;
     // 2*sat+1 levels -sat..sat need 2*sat thresholds; table[63] holds sat.
     for (int k = 0; k < 63; k++) table[k] = 0xFFFFFFFFu;
     table[63] = (uint32_t)sat;
     for (int k = 0; k < 2 * sat; k++) {
         int v = -sat + k;
-        double t = (v >= 0) ? (double)(v + 1) / factor : (double)v / factor;
-        double p = 0.5 * std::erfc(-((t + 1.0) / sigma) / std::sqrt(2.0));
+        double t = (v >= 0) ? (double)(v + 1) / f : (double)v / f;
+        double p = 0.5 * std::erfc(-((t + amp) / sigma) / std::sqrt(2.0));
         double u = std::floor(p * 4294967296.0);
         if (u < 0) u = 0;
         if (u > 4294967295.0) u = 4294967295.0;

@@ -99,3 +99,38 @@ def test_codeword_bits_flip_sign():
     flipped = channel.awgn_i8_host(576, 2, 11, t, codeword=cw)
     assert np.array_equal(flipped[:, ::3], -zero[:, ::3])
     assert np.array_equal(np.delete(flipped, np.s_[::3], 1), np.delete(zero, np.s_[::3], 1))
+
+
+def test_channel_options_qpsk_esn0_normalize():
+    """CChanelAWGN_MKL's options (code/x86/CChanel/CChanelAWGN_MKL.cpp:97-143):
+    Es/N0 input (Eb/N0 = Es/N0 - 10 log10(2R)), QPSK amplitude 0.707106781 and
+    the 2/sigma^2 normalisation.  Every threshold of the integer-exact
+    generator's table sits where clamp(trunc(factor * norm * (-amp + sigma z)))
+    steps by one level, and the defaults reproduce the plain BPSK table."""
+    import math
+    from scipy.stats import norm as N
+    from ldpcgputegra_amd import channel
+    r = 0.5
+    assert channel.sigma_from_snr(1.0, r) == channel.sigma_from_ebn0(1.0, r)
+    assert channel.sigma_from_snr(1.0, r, es_n0=True) == pytest.approx(
+        channel.sigma_from_ebn0(1.0 - 10 * math.log10(2 * r), r))
+    s = channel.sigma_from_ebn0(1.2, r)
+    assert np.array_equal(channel.i8_table(s), channel.i8_table(s, amp=channel.BPSK, normalize=False))
+    for amp, normalize, factor, sat in ((channel.QPSK, False, 8, 31), (1.0, True, 8, 31), (channel.QPSK, True, 4, 15)):
+        t = channel.i8_table(s, factor, sat, amp=amp, normalize=normalize)
+        assert t[63] == sat
+        nm = 2.0 / (s * s) if normalize else 1.0
+        q = lambda y: int(np.clip(np.trunc(factor * nm * y), -sat, sat))   # noqa: E731
+        th = t[:2 * sat].astype(np.float64)
+        assert np.all(np.diff(th) >= 0)
+        for k in range(2 * sat):
+            if th[k] <= 0 or th[k] >= 2.0 ** 32 - 1:
+                continue
+            z = N.ppf(th[k] / 2.0 ** 32)
+            y = -amp + s * z
+            # the threshold is p rounded to 2^-32: in y that is s * 2^-32 / pdf(z)
+            eps = max(1e-7, 4 * s * 2.0 ** -32 / N.pdf(z))
+            if factor * nm * eps > 0.25:
+                continue                                       # deep tail: resolution coarser than a level
+            assert q(y + eps) - q(y - eps) == 1, (amp, normalize, k)
+            assert q(y + eps) == -sat + k + 1

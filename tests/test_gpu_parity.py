@@ -214,12 +214,13 @@ def test_float_decoder_vs_oracle(code, algo, beta, batch):
 def test_device_channel_matches_host_generator():
     torch = _torch()
     t = load_table("dvbs2_r1_2")
-    table = channel.i8_table(0.87)
     dec = decoder("dvbs2_r1_2", 0, 64)
-    d = torch.empty((7, t.n), dtype=torch.int8, device="cuda")
-    dec.awgn_i8_device(d, first_cw=123, seed=42, table=table)
-    torch.cuda.synchronize()
-    assert np.array_equal(d.cpu().numpy(), channel.awgn_i8_host(t.n, 7, 42, table, first_cw=123))
+    # BPSK, and QPSK with the 2/sigma^2 normalisation (CChanelAWGN_MKL options)
+    for table in (channel.i8_table(0.87), channel.i8_table(0.87, 8, 31, amp=channel.QPSK, normalize=True)):
+        d = torch.empty((7, t.n), dtype=torch.int8, device="cuda")
+        dec.awgn_i8_device(d, first_cw=123, seed=42, table=table)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), channel.awgn_i8_host(t.n, 7, 42, table, first_cw=123))
 
 
 def test_error_counter():
