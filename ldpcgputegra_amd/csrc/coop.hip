@@ -978,7 +978,7 @@ static int launch_coop_iters(const DecodeLaunch &L, const CoopCode &cc, int iter
     a.V = (int8_t *)L.V;
     a.Mc = L.msg;
     a.tab = cc.d_tab;
-    a.stride = L.stride;
+    a.stride = L.vpitch;   // V row pitch (the grid follows L.stride)
     a.G = cc.nw * iters;
     a.live = live;
     a.nw = cc.nw;
@@ -1020,6 +1020,7 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     }
     // early termination: one launch per iteration (V, messages and the chain
     // input V[p_0] carry the state), then the syndrome of the live codewords
+    if (L.vpitch != L.stride) return -1;   // the per-iteration helpers address V by the stride
     if (coop_early_begin(L, s)) return -1;
     for (int it = 0; it < L.iters; it++)
         if (launch_coop_iters(L, cc, 1, L.live, s) || coop_early_after_iter(L, it, s)) return -1;

@@ -1095,6 +1095,7 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
         return launch_coop3_iters(L, cc, L.iters, nullptr, s);
     }
     if (L.early) {
+        if (L.vpitch != L.stride) return -1;   // the per-iteration helpers address V by the stride
         // one launch per iteration; converged codewords keep iterating inside
         // live workgroups, so their V is snapshot when they converge and
         // merged back at the end (L.Vs), as coop2
@@ -1117,7 +1118,7 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.V = (int8_t *)L.V;
     a.Mc = (uint8_t *)L.msg;
     a.tab = cc.d_tab;
-    a.pitch = L.stride;
+    a.pitch = L.vpitch;
     a.G = cc.nw * iters;
     a.nw = cc.nw;
     a.tail = cc.tail;

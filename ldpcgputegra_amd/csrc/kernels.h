@@ -7,7 +7,8 @@ struct DecodeLaunch {
     // state, codeword-fastest layout: V[N][stride], messages per kernel family
     void *V;
     void *msg;
-    int stride;          // row stride in codewords (multiple of 64)
+    int stride;          // codeword slots (multiple of 64): the batch padded
+    int vpitch;          // V row pitch in codewords (>= stride; coop3 may pad it)
     int batch;
     int iters;
     int is_float;
