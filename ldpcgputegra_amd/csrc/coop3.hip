@@ -109,6 +109,9 @@ struct alignas(16) Smem3 {
                                       // V stores' staging and the forwarding ring (ring slot g % NR, 8 KB apart
                                       // so that a forwarding code + (g << 13) addresses its entry)
     uint4 mst[WS][8][4];              // new messages of a window per slab wave, [slot] x 64 B
+    uint4 et_spare[320];              // early termination: between segments the whole struct holds the
+                                      // hard bits of every variable (u16 x 64800 for DVB-S2; one
+                                      // workgroup per CU either way)
 };
 
 struct Coop3Args {
@@ -135,6 +138,7 @@ struct St3 {                          // one window's state from pre to post (R 
     uint32_t mn1, mn2, sacc, mx;      // min1 / min2 / sign parity over info + o; x-edge old message
                                       // tail: mn1 = MA, mn2 = MB
     uint32_t xs;                      // the slot's chain step: u16 index of its x input in xo[buf]
+    uint32_t v[X];                    // FZ (early termination): the info edges' V as read (R pairs)
 };
 
 // record meta (word D0): check | COOP_M_ACT | chain step << STEP_SHIFT.  The
@@ -179,6 +183,8 @@ struct Slab3 {
     const char *g1base, *g2base;
     uint32_t g1mul, g1mask, recsel;
     uint32_t vrd, mrd;                // byte offsets of this lane's V dword / message pair in an In record
+    uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
+                                      // their V is rewritten unchanged and the chain passes V[p_i] unchanged
 
     // ---- reads
     // in.mf = mfc (window g's codes, read in the previous period); mfn <- window g+1's
@@ -286,9 +292,14 @@ struct Slab3 {
     }
 
     // pre of window g: chain constants -> cst[g & 1], state -> s
-    template <bool TL>
+    template <bool TL, bool FZ_ = false>
     LDPC_DEV void pre(int g, const PreIn &in, St3 &s) const
     {
+#ifdef C3X_NOFZ   // timing experiment only: no freezing of converged codewords (results are wrong)
+        constexpr bool FZ = false;
+#else
+        constexpr bool FZ = FZ_;
+#endif
         const uint32_t meta = in.mf.x;
         uint32_t v[D0 - 1];
         // V pair of edge j: this pair's two bytes of the loaded V dword, or the
@@ -338,6 +349,13 @@ struct Slab3 {
             B = pk_add(base, a.offp);
             L = pk_max(pk_sub(COV, TV), VNEG127);
             H = pk_min(pk_add(COV, TV), V127);
+            if constexpr (FZ) {   // converged codewords: L = H = V[p_i] as read, the step returns it
+#pragma unroll
+                for (int j = 0; j < X; j++) s.v[j] = v[j];
+                const uint32_t VO = pk_ashr8(v[X]);
+                L = bfi(fm, VO, L);
+                H = bfi(fm, VO, H);
+            }
         } else {
             // the tail check (later degree group: a = |min(c, msg_max)|,
             // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
@@ -358,6 +376,7 @@ struct Slab3 {
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
                 s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn, neg127);
+                if constexpr (FZ) s.c[J] = bfi(fm, v[J], s.c[J]);   // converged codewords keep their V
             });
             s.mx = 0;
             s.sacc = 0;
@@ -393,9 +412,14 @@ struct Slab3 {
 
     // post of window g (x inputs xr): new V pairs -> stg[g % NR], messages ->
     // mst[w]; they leave in the stores of the same period
-    template <bool TL>
+    template <bool TL, bool FZ_ = false>
     LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
     {
+#ifdef C3X_NOFZ
+        constexpr bool FZ = false;
+#else
+        constexpr bool FZ = FZ_;
+#endif
         unsigned short *st = (unsigned short *)&sm.stg[g % NR][k];      // [entry][..S slots..][8 pairs] u16
         constexpr int ES = (S + 1) * 8;                                 // u16 between entries
         uint32_t MA, MB;
@@ -411,9 +435,12 @@ struct Slab3 {
             uint32_t nv[X + 1];
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                nv[J] = pack_v(new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127));
+                const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
+                nv[J] = pack_v(FZ ? bfi(fm, s.v[J], n) : n);
             });
-            nv[X] = pack_v(new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127));
+            // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
+            const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127);
+            nv[X] = pack_v(FZ ? bfi(fm, xr, nx) : nx);
             // the o edge: message bits only (the next check rewrites V[o] as its x edge)
             (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
             MB = perm(k2, k1, 0x07030501u);
@@ -511,21 +538,6 @@ LDPC_DEV uint32_t high_bits16(uint4 x)   // byte high bits -> 16-bit codeword ma
     auto c4 = [](uint32_t v) { return ((v >> 7) & 1u) | ((v >> 14) & 2u) | ((v >> 21) & 4u) | ((v >> 28) & 8u); };
     return c4(x.x) | c4(x.y) << 4 | c4(x.z) << 8 | c4(x.w) << 12;
 }
-LDPC_DEV uint32_t byte_mask4(uint32_t b)   // 4 codeword bits -> 4 byte masks
-{
-    return (b & 1u) * 0xFFu | ((b >> 1) & 1u) * 0xFF00u | ((b >> 2) & 1u) * 0xFF0000u | ((b >> 3) & 1u) * 0xFF000000u;
-}
-LDPC_DEV uint4 byte_mask16(uint32_t m)
-{
-    return make_uint4(byte_mask4(m & 15u), byte_mask4((m >> 4) & 15u), byte_mask4((m >> 8) & 15u),
-                      byte_mask4((m >> 12) & 15u));
-}
-LDPC_DEV uint4 blend16(uint4 a, uint4 b, uint4 m)   // (a & ~m) | (b & m)
-{
-    return make_uint4((a.x & ~m.x) | (b.x & m.x), (a.y & ~m.y) | (b.y & m.y), (a.z & ~m.z) | (b.z & m.z),
-                      (a.w & ~m.w) | (b.w & m.w));
-}
-
 // Wave CHW: the chain; the others: slab waves (slab index w: slots 8w .. 8w+7).
 // ET: in-kernel early termination -- the decode runs one iteration per
 // segment (pipeline drained at its end), then the whole workgroup checks the
@@ -589,92 +601,149 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         __syncthreads();
         if (et_sh[0] == 0) return;   // padding columns only
     }
-    // after iteration `it` (ET): syndrome, snapshot, decision -- every thread,
-    // uniform result (true: decode another iteration)
+    // after iteration `it` (ET): syndrome and decision -- every thread,
+    // uniform result (true: decode another iteration).  Codewords converged
+    // earlier are frozen by the slab waves (Slab3::fm: their V rows are
+    // rewritten with the values they had), so no V snapshot is taken.
+    // Parity bits of check c over the 16 codewords (byte high bits)
+    auto et_check = [&](int c) -> uint4 {
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (c < a.m0) {
+            const uint32_t *e = a.ev + (size_t)c * D0;
+            uint4 y[D0];
+#pragma unroll
+            for (int j = 0; j < D0; j++) y[j] = *et_row(e[j]);
+#pragma unroll
+            for (int j = 0; j < D0; j++) {
+                x.x ^= pos_bits(y[j].x);
+                x.y ^= pos_bits(y[j].y);
+                x.z ^= pos_bits(y[j].z);
+                x.w ^= pos_bits(y[j].w);
+            }
+        } else if (c < a.m) {
+            const uint32_t *e = a.ev + (size_t)a.m0 * D0 + (size_t)(c - a.m0) * a.d1;
+            for (int j = 0; j < a.d1; j++) {
+                const uint4 y = *et_row(e[j]);
+                x.x ^= pos_bits(y.x);
+                x.y ^= pos_bits(y.y);
+                x.z ^= pos_bits(y.z);
+                x.w ^= pos_bits(y.w);
+            }
+        }
+        return x;
+    };
+    // a failing check per codeword, kept across iterations (a codeword that
+    // does not converge tends to keep failing the same checks): round 0 tests
+    // these first
+    __shared__ uint32_t et_hint[CW];
+    if constexpr (ET) {
+        if (threadIdx.x < CW) et_hint[threadIdx.x] = 0;
+    }
+    auto et_note = [&](uint32_t x, int c) {
+        for (uint32_t b = x; b; b &= b - 1u) et_hint[__builtin_ctz(b)] = (uint32_t)c;
+    };
+    // exit test of a scan round: true once every live codeword has a failing check
+    auto et_round = [&](uint32_t f, uint32_t live) -> bool {
+        if (f & live) atomicOr(&et_sh[1], f & live);
+        __syncthreads();
+        const uint32_t fail = et_sh[1];
+        __syncthreads();
+        return (fail & live) == live;
+    };
+#ifdef C3X_ET_PROF   // diagnostic: cycles of et_after and its full syndromes (printf by workgroup 0)
+    unsigned long long ep_tot = 0, ep_stage = 0, ep_chk = 0, ep_t0 = 0, ep_t1 = 0, ep_seg0 = 0, ep_seg = 0;
+    int ep_full = 0, ep_n = 0;
+    ep_seg0 = __builtin_amdgcn_s_memtime();
+#define C3_EP(x) x
+#else
+#define C3_EP(x)
+#endif
     auto et_after = [&](int it) -> bool {
+        C3_EP(ep_t0 = __builtin_amdgcn_s_memtime(); ep_seg += ep_t0 - ep_seg0; ep_n++;)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the iteration's stores and table DMAs
         __syncthreads();
         const uint32_t live = et_sh[0];
-        // each thread: 2 checks per round, 4 rounds between exit tests
-        for (int c0 = 0; c0 < a.m; c0 += NT * 8) {
-            uint4 acc = make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                uint4 x[2];
-#pragma unroll
-                for (int i = 0; i < 2; i++) {
-                    const int c = c0 + (2 * r + i) * NT + (int)threadIdx.x;
-                    x[i] = make_uint4(0, 0, 0, 0);
-                    if (c < a.m0) {
-                        const uint32_t *e = a.ev + (size_t)c * D0;
-                        uint4 y[D0];
-#pragma unroll
-                        for (int j = 0; j < D0; j++) y[j] = *et_row(e[j]);
-#pragma unroll
-                        for (int j = 0; j < D0; j++) {
-                            x[i].x ^= pos_bits(y[j].x);
-                            x[i].y ^= pos_bits(y[j].y);
-                            x[i].z ^= pos_bits(y[j].z);
-                            x[i].w ^= pos_bits(y[j].w);
-                        }
-                    } else if (c < a.m) {
-                        const uint32_t *e = a.ev + (size_t)a.m0 * D0 + (size_t)(c - a.m0) * a.d1;
-                        for (int j = 0; j < a.d1; j++) {
-                            const uint4 y = *et_row(e[j]);
-                            x[i].x ^= pos_bits(y.x);
-                            x[i].y ^= pos_bits(y.y);
-                            x[i].z ^= pos_bits(y.z);
-                            x[i].w ^= pos_bits(y.w);
-                        }
-                    }
-                }
-                acc.x |= x[0].x | x[1].x;
-                acc.y |= x[0].y | x[1].y;
-                acc.z |= x[0].z | x[1].z;
-                acc.w |= x[0].w | x[1].w;
-            }
-            const uint32_t f = high_bits16(acc) & live;
-            if (f) atomicOr(&et_sh[1], f);
-            __syncthreads();
-            const uint32_t fail = et_sh[1];
-            __syncthreads();
-            if ((fail & live) == live) break;   // every live codeword has a failing check
+#ifdef C3X_ET_NOSCAN   // timing experiment only (no codeword ever converges): segments without the syndrome
+        if (threadIdx.x == 0) et_sh[1] = live;
+        __syncthreads();
+        if (false) {
+#else
+        // round 0: one check per thread, gathered directly -- threads 0..15
+        // the codewords' hint checks, the others checks spread over the code
+        // (a codeword still decoding fails many checks: this usually settles
+        // every live one)
+        {
+            const int c = threadIdx.x < CW ? (int)et_hint[threadIdx.x]
+                                           : (int)((threadIdx.x + (size_t)it * NT * 5) % (size_t)a.m);
+            const uint32_t x = high_bits16(et_check(c)) & live;
+            et_note(x, c);
+            if (et_round(x, live)) goto et_done;
         }
+        {
+#endif
+            // the full syndrome: every variable's hard bits staged in LDS (the
+            // pipeline's LDS is idle between segments; the launch checks n
+            // fits), then the checks, 8 per thread and round with an exit
+            // test after each; loads unconditional (clamped check index) so a
+            // round's index loads are in flight together
+            uint16_t *hb = reinterpret_cast<uint16_t *>(&sm);
+            C3_EP(ep_t1 = __builtin_amdgcn_s_memtime(); ep_full++;)
+#pragma unroll 16
+            for (int r = threadIdx.x; r < a.n; r += NT) {
+                const uint4 y = *et_row((uint32_t)r);
+                hb[r] = (uint16_t)high_bits16(make_uint4(pos_bits(y.x), pos_bits(y.y), pos_bits(y.z), pos_bits(y.w)));
+            }
+            __syncthreads();
+            C3_EP({ const unsigned long long t = __builtin_amdgcn_s_memtime(); ep_stage += t - ep_t1; ep_t1 = t; })
+            bool done = false;
+            for (int c0 = 0; c0 < a.m0 && !done; c0 += NT * 8) {
+                uint32_t ev[8][D0];
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const int cc = min(c0 + r * NT + (int)threadIdx.x, a.m0 - 1);
+#pragma unroll
+                    for (int j = 0; j < D0; j++) ev[r][j] = a.ev[(size_t)cc * D0 + j];
+                }
+                uint32_t f = 0;
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const int c = c0 + r * NT + (int)threadIdx.x;
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int j = 0; j < D0; j++) x ^= hb[ev[r][j]];
+                    x = c < a.m0 ? x & live : 0u;
+                    f |= x;
+                    if (x) et_note(x, c);
+                }
+                done = et_round(f, live);
+            }
+            if (!done && a.m > a.m0) {   // the later degree group (DVB-S2: the tail check)
+                uint32_t f = 0;
+                for (int c = a.m0 + (int)threadIdx.x; c < a.m; c += NT) {
+                    const uint32_t *e = a.ev + (size_t)a.m0 * D0 + (size_t)(c - a.m0) * a.d1;
+                    uint32_t x = 0;
+                    for (int j = 0; j < a.d1; j++) x ^= hb[e[j]];
+                    x &= live;
+                    f |= x;
+                    if (x) et_note(x, c);
+                }
+                et_round(f, live);
+            }
+            C3_EP(ep_chk += __builtin_amdgcn_s_memtime() - ep_t1;)
+        }
+#ifndef C3X_ET_NOSCAN
+    et_done:
+#endif
         const uint32_t fresh = live & ~et_sh[1];   // converged after this iteration
         __syncthreads();
         if (threadIdx.x == 0) {
             et_sh[0] = live & ~fresh;
             et_sh[1] = 0;
         }
-        if (fresh) {
-            if (threadIdx.x < CW && ((fresh >> threadIdx.x) & 1u)) a.iters_used[wg * CW + threadIdx.x] = it + 1;
-            // snapshot of the fresh codewords' bytes of every row (Vs: V layout)
-            const uint4 M = byte_mask16(fresh);
-            char *vs = (char *)a.Vs + (size_t)wg * CW;
-#pragma unroll 8
-            for (int r = threadIdx.x; r < a.n; r += NT) {
-                uint4 *d = (uint4 *)(vs + (size_t)r * (size_t)a.pitch);
-                *d = blend16(*d, *et_row((uint32_t)r), M);
-            }
-        }
+        if (fresh && threadIdx.x < CW && ((fresh >> threadIdx.x) & 1u)) a.iters_used[wg * CW + threadIdx.x] = it + 1;
         __syncthreads();
+        C3_EP(ep_seg0 = __builtin_amdgcn_s_memtime(); ep_tot += ep_seg0 - ep_t0;)
         return (live & ~fresh) != 0 && it + 1 < a.iters;
-    };
-    // the end (ET): converged codewords take their snapshot back
-    auto et_merge = [&]() {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const int valid = min(CW, max(0, a.batch - wg * CW));
-        const uint32_t conv = ((1u << valid) - 1u) & ~et_sh[0];
-        if (conv) {
-            const uint4 M = byte_mask16(conv);
-            const char *vs = (const char *)a.Vs + (size_t)wg * CW;
-#pragma unroll 8
-            for (int r = threadIdx.x; r < a.n; r += NT) {
-                uint4 *d = (uint4 *)et_row((uint32_t)r);
-                *d = blend16(*d, *(const uint4 *)(vs + (size_t)r * (size_t)a.pitch), M);
-            }
-        }
     };
     // stamps (diagnostic build): per wave 8 words: busy, phases 1..3 (slab:
     // vmcnt, first and second half), -, elapsed, -, G
@@ -730,7 +799,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if (!ET || !et_after(it)) break;
         }
         write_stamps();
-        if (ET) et_merge();
         parity_out();
         return;
     }
@@ -774,6 +842,11 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     constexpr int NI = CF::NI, NS = CF::NS;
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
         __syncthreads();   // prologue 1: tables in LDS
+        if constexpr (ET) {   // codewords 2q (low half) and 2q+1 (high half) of this lane: converged?
+            const int valid = min(CW, max(0, a.batch - wg * CW));
+            const uint32_t conv = (((1u << valid) - 1u) & ~et_sh[0]) >> (2 * q);
+            sl.fm = ((conv & 1u) ? 0x0000FFFFu : 0u) | ((conv & 2u) ? 0xFFFF0000u : 0u);
+        }
         St3 st[NS];
         uint4 mfc;   // records D0 .. D0+3 of the next pre's window
         {
@@ -789,9 +862,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             sl.mask_early(0, in.mf);
             sl.fwd_read(0, in);
             if (a.tail == 0)
-                sl.template pre<true>(0, in, st[0]);
+                sl.template pre<true, ET>(0, in, st[0]);
             else
-                sl.template pre<false>(0, in, st[0]);
+                sl.template pre<false, ET>(0, in, st[0]);
         }
         __syncthreads();   // prologue 2
         if (STAMP) t0 = stamp3();
@@ -840,21 +913,21 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 sl.read_pf(p + 1 + R, pi);
                 if (sw == 0) {
                     C3_MARK("post0");
-                    sl.template post<false>(p - 1, xr, sp);
+                    sl.template post<false, ET>(p - 1, xr, sp);
                     sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values
                     sl.gathers(pi, (s + R + 1) % NI);
                     sl.read_st(p - 1, sc);
                     if (STAMP) t2 = stampL();
                     C3_MARK("pre0");
-                    sl.template pre<false>(p + 1, in, sn);
+                    sl.template pre<false, ET>(p + 1, in, sn);
                 } else {
                     sl.fwd_read(p + 1, in);   // windows <= p-2, staged before the barrier
                     C3_MARK("pre");
-                    sl.template pre<false>(p + 1, in, sn);
+                    sl.template pre<false, ET>(p + 1, in, sn);
                     sl.gathers(pi, (s + R + 1) % NI);
                     if (STAMP) t2 = stampL();
                     C3_MARK("post");
-                    sl.template post<false>(p - 1, xr, sp);
+                    sl.template post<false, ET>(p - 1, xr, sp);
                     sl.read_st(p - 1, sc);
                 }
                 if (STAMP) t3 = stampL();
@@ -864,9 +937,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 if (dst) sl.stores(sc, sc_tl);
                 if (dpo) {
                     if (uA == a.tail)
-                        sl.template post<true>(p - 1, sl.read_x(p - 1, sp), sp);
+                        sl.template post<true, ET>(p - 1, sl.read_x(p - 1, sp), sp);
                     else
-                        sl.template post<false>(p - 1, sl.read_x(p - 1, sp), sp);
+                        sl.template post<false, ET>(p - 1, sl.read_x(p - 1, sp), sp);
                 }
                 if (STAMP) t1 = t2 = t3 = stampL();
                 if (dpo) {
@@ -879,9 +952,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     sl.fwd_read(p + 1, in);
                     sl.read_pf(p + 1 + R, pi);
                     if (uB == a.tail)
-                        sl.template pre<true>(p + 1, in, sn);
+                        sl.template pre<true, ET>(p + 1, in, sn);
                     else
-                        sl.template pre<false>(p + 1, in, sn);
+                        sl.template pre<false, ET>(p + 1, in, sn);
                     sl.gathers(pi, (s + R + 1) % NI);
                 }
             }
@@ -919,8 +992,8 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         sl.stores(sc, sc_tl);   // window G-1
         if (!ET || !et_after(it)) break;
     }
+    C3_EP(if (threadIdx.x == 0 && id == 0) printf("ET prof wg0: segments %d  full %d  cycles: segments %llu  et_after %llu  staging %llu  checks %llu\n", ep_n, ep_full, ep_seg, ep_tot, ep_stage, ep_chk);)
     write_stamps();
-    if (ET) et_merge();
     parity_out();
 }
 
@@ -1087,7 +1160,8 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     if (!cc.valid || !coop3_stride_ok(L.stride)) return -1;
     if (L.early && cc.S == 48) {
         // in-kernel early termination (one launch, coop3_decode<.., ET>)
-        if (!L.Vs || !L.iters_used) return -1;
+        if (!L.iters_used) return -1;
+        if ((size_t)L.n * 2 > sizeof(Smem3<6, 2>)) return -1;   // et_after's LDS copy of the hard bits
         if (L.iters == 0) {
             hipLaunchKernelGGL(fill_iters3_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used, 0);
             return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1142,7 +1216,7 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.prio = env_int3("LDPC_COOP3_PRIO", 1);
     a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 0);
     const int grid = L.stride / CW;
-    a.remap = (grid % 8) == 0;
+    a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups
     const int ws = cc.S / 8;
     const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0;
     if (stamped) {
