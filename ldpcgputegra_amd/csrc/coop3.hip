@@ -185,6 +185,7 @@ struct Slab3 {
     uint32_t vrd, mrd;                // byte offsets of this lane's V dword / message pair in an In record
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
+    uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
 
     // ---- reads
     // in.mf = mfc (window g's codes, read in the previous period); mfn <- window g+1's
@@ -436,11 +437,11 @@ struct Slab3 {
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
                 const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
-                nv[J] = pack_v(FZ ? bfi(fm, s.v[J], n) : n);
+                nv[J] = FZ ? perm(n, s.v[J], psel) : pack_v(n);   // FZ: pack_v of new / old per codeword
             });
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
             const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127);
-            nv[X] = pack_v(FZ ? bfi(fm, xr, nx) : nx);
+            nv[X] = FZ ? perm(nx, xr, psel) : pack_v(nx);
             // the o edge: message bits only (the next check rewrites V[o] as its x edge)
             (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
             MB = perm(k2, k1, 0x07030501u);
@@ -635,12 +636,13 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     // a failing check per codeword, kept across iterations (a codeword that
     // does not converge tends to keep failing the same checks): round 0 tests
     // these first
-    __shared__ uint32_t et_hint[CW];
+    constexpr int NH = 4;   // hint checks per codeword
+    __shared__ uint32_t et_hint[CW * NH];
     if constexpr (ET) {
-        if (threadIdx.x < CW) et_hint[threadIdx.x] = 0;
+        if (threadIdx.x < CW * NH) et_hint[threadIdx.x] = (uint32_t)threadIdx.x;
     }
     auto et_note = [&](uint32_t x, int c) {
-        for (uint32_t b = x; b; b &= b - 1u) et_hint[__builtin_ctz(b)] = (uint32_t)c;
+        for (uint32_t b = x; b; b &= b - 1u) et_hint[__builtin_ctz(b) * NH + (c & (NH - 1))] = (uint32_t)c;
     };
     // exit test of a scan round: true once every live codeword has a failing check
     auto et_round = [&](uint32_t f, uint32_t live) -> bool {
@@ -668,12 +670,12 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         __syncthreads();
         if (false) {
 #else
-        // round 0: one check per thread, gathered directly -- threads 0..15
+        // round 0: one check per thread, gathered directly -- threads 0..63
         // the codewords' hint checks, the others checks spread over the code
         // (a codeword still decoding fails many checks: this usually settles
         // every live one)
         {
-            const int c = threadIdx.x < CW ? (int)et_hint[threadIdx.x]
+            const int c = threadIdx.x < CW * NH ? (int)et_hint[threadIdx.x]
                                            : (int)((threadIdx.x + (size_t)it * NT * 5) % (size_t)a.m);
             const uint32_t x = high_bits16(et_check(c)) & live;
             et_note(x, c);
@@ -688,10 +690,27 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             // round's index loads are in flight together
             uint16_t *hb = reinterpret_cast<uint16_t *>(&sm);
             C3_EP(ep_t1 = __builtin_amdgcn_s_memtime(); ep_full++;)
-#pragma unroll 16
-            for (int r = threadIdx.x; r < a.n; r += NT) {
-                const uint4 y = *et_row((uint32_t)r);
-                hb[r] = (uint16_t)high_bits16(make_uint4(pos_bits(y.x), pos_bits(y.y), pos_bits(y.z), pos_bits(y.w)));
+            // (16 unconditional loads in flight per thread: clamped rows)
+            auto hbits = [](uint4 y) {
+                return (uint16_t)high_bits16(make_uint4(pos_bits(y.x), pos_bits(y.y), pos_bits(y.z), pos_bits(y.w)));
+            };
+            for (int r0 = 0; r0 < a.k; r0 += NT * 16) {   // information rows: V
+                uint4 y[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    y[i] = *(const uint4 *)(etV + (size_t)min(r0 + i * NT + (int)threadIdx.x, a.k - 1) * (size_t)a.pitch);
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    if (r0 + i * NT + (int)threadIdx.x < a.k) hb[r0 + i * NT + threadIdx.x] = hbits(y[i]);
+            }
+            for (int r0 = 0; r0 < a.m; r0 += NT * 16) {   // parity rows: P
+                uint4 y[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    y[i] = *(const uint4 *)(etP + (size_t)min(r0 + i * NT + (int)threadIdx.x, a.m - 1) * 16);
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    if (r0 + i * NT + (int)threadIdx.x < a.m) hb[a.k + r0 + i * NT + threadIdx.x] = hbits(y[i]);
             }
             __syncthreads();
             C3_EP({ const unsigned long long t = __builtin_amdgcn_s_memtime(); ep_stage += t - ep_t1; ep_t1 = t; })
@@ -846,6 +865,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             const int valid = min(CW, max(0, a.batch - wg * CW));
             const uint32_t conv = (((1u << valid) - 1u) & ~et_sh[0]) >> (2 * q);
             sl.fm = ((conv & 1u) ? 0x0000FFFFu : 0u) | ((conv & 2u) ? 0xFFFF0000u : 0u);
+            sl.psel = 0x0c0c0000u | ((conv & 2u) ? 0x0300u : 0x0700u) | ((conv & 1u) ? 0x01u : 0x05u);
         }
         St3 st[NS];
         uint4 mfc;   // records D0 .. D0+3 of the next pre's window
