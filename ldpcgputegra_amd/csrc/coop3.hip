@@ -93,6 +93,10 @@ template <int WS, int R>
 struct alignas(16) Smem3 {
     using CF = Cfg<WS, R>;
     static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
+    uint4 stg[NR][STG_RING / 16];     // new V of a window, [record entry * (S + 1) + slot] x 16 codewords (int8,
+                                      // entries padded: the stores' reads of 8 entries are conflict-free): the
+                                      // V stores' staging and the forwarding ring (ring slot g % NR, 8 KB apart
+                                      // so that a forwarding code + (g << 13) addresses its entry)
     uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
@@ -104,10 +108,6 @@ struct alignas(16) Smem3 {
         uint4 b[2][8];                //   [0..1][slot] message 32..63 B
     } in[WS][NI];                     // (entry-major: the 8 slots of one read are in different banks)
     static constexpr uint32_t IN_B = sizeof(uint4) * (8 * 8 + 4);   // byte offset of In::b
-    uint4 stg[NR][STG_RING / 16];     // new V of a window, [record entry * (S + 1) + slot] x 16 codewords (int8,
-                                      // entries padded: the stores' reads of 8 entries are conflict-free): the
-                                      // V stores' staging and the forwarding ring (ring slot g % NR, 8 KB apart
-                                      // so that a forwarding code + (g << 13) addresses its entry)
     uint4 mst[WS][8][4];              // new messages of a window per slab wave, [slot] x 64 B
     uint4 et_spare[320];              // early termination: between segments the whole struct holds the
                                       // hard bits of every variable (u16 x 64800 for DVB-S2; one
@@ -178,6 +178,7 @@ struct Slab3 {
     i32x4 mr;                         // message rows in 16-B units
     int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
     uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
+    uint32_t fsel;                    // ... of a forwarded u16 (0x050d040d, in a VGPR)
     PkK K;
     // per-lane constants of the LDS-DMA gathers (lane (kl, j): j < 6 a V row, j >= 6 a message piece)
     const char *g1base, *g2base;
@@ -208,7 +209,7 @@ struct Slab3 {
     LDPC_DEV void fwd_read(int g, PreIn &in) const
     {
         const char *sbase = (const char *)&sm.stg[0][0];
-        const uint32_t gs = (uint32_t)g << 13, q2 = 2u * (uint32_t)q;
+        const uint32_t gs = (uint32_t)__builtin_amdgcn_readfirstlane(g << 13), q2 = 2u * (uint32_t)q;
         const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
 #pragma unroll
         for (int j = 0; j < X; j++) {
@@ -293,7 +294,7 @@ struct Slab3 {
     }
 
     // pre of window g: chain constants -> cst[g & 1], state -> s
-    template <bool TL, bool FZ_ = false>
+    template <bool TL, bool FZ_ = false, int MP = -1>
     LDPC_DEV void pre(int g, const PreIn &in, St3 &s) const
     {
 #ifdef C3X_NOFZ   // timing experiment only: no freezing of converged codewords (results are wrong)
@@ -308,8 +309,8 @@ struct Slab3 {
         const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
 #pragma unroll
         for (int j = 0; j < X; j++) {
-            const uint32_t m = 0u - ((fw[j >> 1] >> (16 * (j & 1))) & 1u);
-            v[j] = perm(in.fv[j], in.v[j], (usel & ~m) | (0x050d040du & m));
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)fw[j >> 1], 16 * (j & 1), 1);   // 0 / -1
+            v[j] = perm(in.fv[j], in.v[j], bfi(m, fsel, usel));
         }
         v[X] = unpack_v(in.v[X], usel);
         const MsgTab t = msg_tab(in.mb);
@@ -330,6 +331,7 @@ struct Slab3 {
                 min2 = pk_max(min1, pk_min(aj, min2));
                 min1 = pk_min(min1, aj);
             });
+            if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t T = pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0);   // cst over the info edges
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
             const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), neg127);
@@ -413,7 +415,7 @@ struct Slab3 {
 
     // post of window g (x inputs xr): new V pairs -> stg[g % NR], messages ->
     // mst[w]; they leave in the stores of the same period
-    template <bool TL, bool FZ_ = false>
+    template <bool TL, bool FZ_ = false, int MP = -1>
     LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
     {
 #ifdef C3X_NOFZ
@@ -439,6 +441,7 @@ struct Slab3 {
                 const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
                 nv[J] = FZ ? perm(n, s.v[J], psel) : pack_v(n);   // FZ: pack_v of new / old per codeword
             });
+            if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
             const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127);
             nv[X] = FZ ? perm(nx, xr, psel) : pack_v(nx);
@@ -827,7 +830,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     // the second-dispatched half of the slab waves loses VALU arbitration to
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
-    if (a.slab_prio && wave > CHW) __builtin_amdgcn_s_setprio(1);
+    if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
     const int kl = lane >> 3, q = lane & 7;
     const char *Vb = (const char *)a.V + (size_t)wg * CW;
     const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
@@ -845,6 +848,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     lane,
                     a.tail,
                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
+                    opaque(0x050d040du),
                     PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
                     // DMA lane 8e + slot: entry e < 6 a V row (record entry e, the
                     // o edge's D0-1 for e = X), e >= 6 message piece e - 6
@@ -910,6 +914,8 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         // The gathers of window p+1 were the last vector memory operations of
         // period p-R, followed by 4 in each later period: in the main loop (every
         // period does everything, no tail window) vmcnt(4(R-1)) covers them.
+        constexpr int MP1 = -1, MP2 = -1;   // mid-phase priorities (none: quarter-period levels measured the same)
+        const bool fair = a.slab_prio == 2;
         auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
             constexpr bool GU = decltype(guarded)::value;
@@ -927,27 +933,35 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 // chain inputs of window p-1, records of window p+1+R
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1)) : "memory");
                 if (STAMP) t1 = stampL();
+                // fair issue between the two slab waves of a SIMD: each runs the
+                // first phase of its period at priority 1 and the second at 0, so
+                // a wave that lags behind its partner (the arbiter otherwise
+                // favours the older wave) catches up and neither finishes the
+                // period alone on the SIMD (49.7 -> 47.8 ms)
+                if (fair) __builtin_amdgcn_s_setprio(1);
                 sl.stores(sc, false);
                 const uint32_t xr = sl.read_x(p - 1, sp);
                 sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
                 sl.read_pf(p + 1 + R, pi);
                 if (sw == 0) {
                     C3_MARK("post0");
-                    sl.template post<false, ET>(p - 1, xr, sp);
+                    sl.template post<false, ET, MP1>(p - 1, xr, sp);
                     sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values
                     sl.gathers(pi, (s + R + 1) % NI);
                     sl.read_st(p - 1, sc);
                     if (STAMP) t2 = stampL();
+                    if (fair) __builtin_amdgcn_s_setprio(0);
                     C3_MARK("pre0");
-                    sl.template pre<false, ET>(p + 1, in, sn);
+                    sl.template pre<false, ET, MP2>(p + 1, in, sn);
                 } else {
                     sl.fwd_read(p + 1, in);   // windows <= p-2, staged before the barrier
                     C3_MARK("pre");
-                    sl.template pre<false, ET>(p + 1, in, sn);
+                    sl.template pre<false, ET, MP1>(p + 1, in, sn);
                     sl.gathers(pi, (s + R + 1) % NI);
                     if (STAMP) t2 = stampL();
+                    if (fair) __builtin_amdgcn_s_setprio(0);
                     C3_MARK("post");
-                    sl.template post<false, ET>(p - 1, xr, sp);
+                    sl.template post<false, ET, MP2>(p - 1, xr, sp);
                     sl.read_st(p - 1, sc);
                 }
                 if (STAMP) t3 = stampL();
@@ -1234,7 +1248,7 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.coff = (uint32_t)(L.param * 256) * 0x00010001u;
     a.offp = (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
     a.prio = env_int3("LDPC_COOP3_PRIO", 1);
-    a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 0);
+    a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 0 none, 1 static (second waves), 2 fair by phase
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups
     const int ws = cc.S / 8;
