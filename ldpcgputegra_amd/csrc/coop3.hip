@@ -915,6 +915,11 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         // period p-R, followed by 4 in each later period: in the main loop (every
         // period does everything, no tail window) vmcnt(4(R-1)) covers them.
         constexpr int MP1 = -1, MP2 = -1;   // mid-phase priorities (none: quarter-period levels measured the same)
+#ifdef C3X_PREFIRST   // r02k order: slab waves 1-5 run pre first, wait for their gathers at the period start
+        constexpr bool POSTFIRST = false;
+#else
+        constexpr bool POSTFIRST = true;
+#endif
         const bool fair = a.slab_prio == 2;
         auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
@@ -926,7 +931,27 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             PfIn pi;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
-            if (fast) {
+            if (fast && POSTFIRST) {
+                // every slab wave posts first (window p-1: chain outputs and the
+                // state in VGPRs, nothing from memory) and waits for its window
+                // p+1 gathers only before its pre, half a period later than at
+                // the period start (the stores of this period are 2 more
+                // operations in flight): 47.6 -> 46.9 ms
+                if (fair) __builtin_amdgcn_s_setprio(1);
+                sl.stores(sc, false);
+                const uint32_t xr = sl.read_x(p - 1, sp);
+                sl.read_pf(p + 1 + R, pi);
+                sl.template post<false, ET, MP1>(p - 1, xr, sp);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1) + 2) : "memory");
+                sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
+                sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values (wave 0)
+                sl.gathers(pi, (s + R + 1) % NI);
+                sl.read_st(p - 1, sc);
+                if (STAMP) t1 = t2 = stampL();
+                if (fair) __builtin_amdgcn_s_setprio(0);
+                sl.template pre<false, ET, MP2>(p + 1, in, sn);
+                if (STAMP) t3 = stampL();
+            } else if (fast) {
                 // every read of the period that does not depend on this period's
                 // own writes goes first (one exposed LDS latency): the gathers of
                 // window p+1 have landed (the vmcnt count of the main loop),
