@@ -941,11 +941,29 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 sl.stores(sc, false);
                 const uint32_t xr = sl.read_x(p - 1, sp);
                 sl.read_pf(p + 1 + R, pi);
-                sl.template post<false, ET, MP1>(p - 1, xr, sp);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1) + 2) : "memory");
-                sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
-                sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values (wave 0)
+#ifdef C3X_GATHER_TOP   // experiment: the gathers of window p+1+R right after the stores
                 sl.gathers(pi, (s + R + 1) % NI);
+                constexpr int VMW = 4 * (R - 1) + 4;
+#else
+                constexpr int VMW = 4 * (R - 1) + 2;
+#endif
+#ifdef C3X_FWD_TOP   // experiment: waves 1-5 read their forwarded values (windows <= p-2) before the post
+                if (sw != 0) {
+                    in.mf = mfc;
+                    sl.fwd_read(p + 1, in);
+                }
+#endif
+                sl.template post<false, ET, MP1>(p - 1, xr, sp);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMW) : "memory");
+                sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
+#ifdef C3X_FWD_TOP
+                if (sw == 0) sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values
+#else
+                sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values (wave 0)
+#endif
+#ifndef C3X_GATHER_TOP
+                sl.gathers(pi, (s + R + 1) % NI);
+#endif
                 sl.read_st(p - 1, sc);
                 if (STAMP) t1 = t2 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(0);
