@@ -295,7 +295,8 @@ def bench_mixed(a, rank, world, local, torch, dist):
         out = {
             "metric": "decoded Mbit/s, configs[4]: mixed-rate DVB-S2 (%s) int8 + early termination"
                       % ", ".join(n.split("_", 1)[1].replace("_", "/") for n in names),
-            "value": round(value, 3), "unit": "Mbit/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "value": round(value, 3), "unit": "Mbit/s", "n_gpus": world,
+            "ranks_seen": dist.get_world_size() if dist.is_initialized() else 1, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int8",
             "data": "synthetic (device AWGN generator, all-zero codeword per rate)" + (
@@ -329,13 +330,44 @@ def bench_mixed(a, rank, world, local, torch, dist):
     mx.close()
 
 
+def launch_ranks(a):
+    """`python bench.py --gpus N` (N > 1) outside a torch.distributed launcher:
+    start one as a CHILD process -- before this process has touched the GPU
+    (no torch import yet) -- with N ranks on 127.0.0.1, rank 0's JSON line
+    passing through on the shared stdout, and return its exit status."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode
+
+
+def rank_list(value, world, dist):
+    """[value of rank 0, ..., value of rank world-1] (any backend)."""
+    if world == 1:
+        return [value]
+    out = [None] * world
+    dist.all_gather_object(out, value)
+    return out
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.exit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, a.gpus))
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # "gloo" rehearses N ranks on fewer GPUs (ranks share devices round-robin);
@@ -343,6 +375,9 @@ def main():
     backend = os.environ.get("LDPC_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(torch.cuda.device_count(), 1)
+    elif world > torch.cuda.device_count():
+        sys.exit("bench.py: %d ranks but %d visible GPUs (LDPC_BENCH_BACKEND=gloo shares devices)"
+                 % (world, torch.cuda.device_count()))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
@@ -400,13 +435,16 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
+    el = el_local = time.perf_counter() - t0
     kms, launches = dec.kernel_time(reset=True)
     dec.profile(False)
 
     be_l, fe_l = counts.tolist()
     el, be, fe, _ = reduce_results(el, be_l, fe_l, B * a.steps, device="cuda")
     kernel_ms, _, _, _ = reduce_results(kms / max(launches, 1), 0, 0, 0, device="cuda")
+    per_rank = rank_list({"device": local, "kernel_ms": round(kms / max(launches, 1), 4),
+                          "elapsed_s": round(el_local, 6)}, world, dist)
+    ranks_seen = dist.get_world_size() if dist.is_initialized() else 1
 
     if rank == 0:
         frames = world * B * a.steps
@@ -431,6 +469,7 @@ def main():
             "value": round(value, 3),
             "unit": "Mbit/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 4),
@@ -481,6 +520,9 @@ def main():
                                    cpu_baseline(a.code, a.iters, a.cpu_seconds, thr, a.seed))
         else:
             out["cpu_baseline"] = None
+        if world > 1:   # one entry per rank: its device and its own decode-kernel time
+            out["per_rank"] = per_rank
+            out["backend"] = backend
         if dec.last_skipped:   # a faster kernel did not apply at this batch size
             out["config"]["kernel_skipped"] = dec.last_skipped
         print(json.dumps(out), flush=True)

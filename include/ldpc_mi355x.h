@@ -148,7 +148,8 @@ int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
  * 2 = windowed layered kernel (compressed messages), 3 / 4 = windowed2
  * (S = 16 / 32), 5 = workgroup-cooperative DVB-S2 kernel, 6 = its packed-pair
  * variant (two codewords per lane; first-group degree 7; early termination by per-iteration launches),
- * 7 = LDS-resident short-code kernel (whole state in LDS; int8 and float). */
+ * 7 = LDS-resident short-code kernel (whole state in LDS; int8 and float),
+ * 8 = coop3 (DVB-S2 first-group degree 7: slab waves doing pre + post, i16 chain). */
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel family the last decode actually ran (1 generic, 2 windowed,
@@ -208,6 +209,9 @@ void ldpc_mixed_destroy(ldpc_mixed *mx);
 int ldpc_decode_i8_mixed_async(ldpc_mixed *mx, void *hip_stream, const int8_t *d_llr, uint8_t *d_hard,
                                int32_t *d_iters_used, const int32_t *code_id, int batch, int n_iter,
                                const ldpc_params *p);
+/* Kernel family the last mixed decode ran for code `code_index` (numbering of
+ * ldpc_ctx_last_kernel; 0 if that code had no codewords in any decode yet). */
+int ldpc_mixed_last_kernel(ldpc_mixed *mx, int code_index, int *kernel);
 
 /* DVB-S2 IRA encoder (codes built from an Annex-B table), as the
  * reference's GenericEncoder::encode (code/x86/CEncoder/GenericEncoder.cpp:38-78):

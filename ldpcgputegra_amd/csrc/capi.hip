@@ -196,13 +196,18 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
     return LDPC_OK;
 }
 
+bool ldpc_ctx_has_kernel(const ldpc_ctx *c, int k)
+{
+    if (!c || k < 0 || k > 8) return false;
+    return !((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid) ||
+             (k == 5 && !c->coop.valid) || (k == 6 && !c->coop2.valid) || (k == 7 && !c->lds.valid) ||
+             (k == 8 && !c->coop3.valid));
+}
+
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
 {
     if (!c || k < 0 || k > 8) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 8");
-    if ((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid) ||
-        (k == 5 && !c->coop.valid) || (k == 6 && !c->coop2.valid) || (k == 7 && !c->lds.valid) ||
-        (k == 8 && !c->coop3.valid))
-        return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
+    if (!ldpc_ctx_has_kernel(c, k)) return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
     c->kernel = k;
     return LDPC_OK;
 }
@@ -425,7 +430,9 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         L.bad = (uint32_t *)sc.d_early;
         if (!L.iters_used) L.iters_used = (int32_t *)((char *)sc.d_early + (size_t)stride * 4);
         L.live = (uint8_t *)sc.d_early + (size_t)stride * 8;
-        if (kern == 6 || kern == 8) {
+        // V snapshots: only the per-iteration launches need them (coop2, and
+        // coop3 where its in-kernel early termination does not apply)
+        if (kern == 6 || (kern == 8 && !coop3_et_in_kernel(c->coop3, h->n))) {
             if ((rc = ensure(&sc.d_Vs, &sc.Vs_bytes, (size_t)(h->n + 1) * vpitch)) != LDPC_OK) return rc;
             L.Vs = (int8_t *)sc.d_Vs;
         }
@@ -447,7 +454,11 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         HIP_TRY(hipEventRecord(ev1, s));
         c->events.emplace_back(ev0, ev1);
     }
-    if (lr) return ldpc_set_error(LDPC_EDEVICE, "decode launch: %s", hipGetErrorString(hipGetLastError()));
+    if (lr) {
+        const hipError_t e = hipGetLastError();
+        return ldpc_set_error(LDPC_EDEVICE, "decode launch (kernel %d): %s", kern,
+                              e != hipSuccess ? hipGetErrorString(e) : "launch configuration rejected by the host side");
+    }
     if (d_hard || d_soft) {
         int r2 = is_float ? launch_deinterleave_f32((const float *)sc.d_V, d_hard, (float *)d_soft, h->n, batch,
                                                     vpitch, s)

@@ -66,3 +66,5 @@ bool coop3_params_ok(const ldpc_params *p);
 bool coop3_stride_ok(int stride);
 int coop3_upload(const ldpc_code *h, CoopCode *cc);
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
+// early termination inside the coop3 launch (else per-iteration launches + V snapshots)
+bool coop3_et_in_kernel(const CoopCode &cc, int n);

@@ -1007,10 +1007,8 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     }
     // early termination in the kernel (coop_decode<.., ET>): one launch
     // (LDPC_COOP_ET_KERNEL=0: the per-iteration launches below)
-    static const bool in_kernel = [] {
-        const char *e = getenv("LDPC_COOP_ET_KERNEL");
-        return !(e && *e && atoi(e) == 0);
-    }();
+    const char *ek = getenv("LDPC_COOP_ET_KERNEL");
+    const bool in_kernel = !(ek && *ek && atoi(ek) == 0);
     if (in_kernel && L.iters_used) {
         if (L.iters == 0) {
             hipLaunchKernelGGL(fill_iters_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used, 0);
@@ -1020,7 +1018,6 @@ int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     }
     // early termination: one launch per iteration (V, messages and the chain
     // input V[p_0] carry the state), then the syndrome of the live codewords
-    if (L.vpitch != L.stride) return -1;   // the per-iteration helpers address V by the stride
     if (coop_early_begin(L, s)) return -1;
     for (int it = 0; it < L.iters; it++)
         if (launch_coop_iters(L, cc, 1, L.live, s) || coop_early_after_iter(L, it, s)) return -1;
@@ -1047,12 +1044,14 @@ int coop_early_after_iter(const DecodeLaunch &L, int it, hipStream_t s)
         const int v = (e && *e) ? atoi(e) : 64;
         return v >= 4 && v <= 4096 ? v : 64;
     }();
+    // V (and its snapshot Vs) rows are L.vpitch codewords apart (the padded
+    // pitch of the coop kernels); live / bad / iters_used are per codeword
     const dim3 sgrid((L.batch + 63) / 64, (L.m + kChunk - 1) / kChunk);
-    hipLaunchKernelGGL(syndrome_k, sgrid, dim3(64), 0, s, (const int8_t *)L.V, L.stride, L.batch, L.d_edge_var,
+    hipLaunchKernelGGL(syndrome_k, sgrid, dim3(64), 0, s, (const int8_t *)L.V, L.vpitch, L.batch, L.d_edge_var,
                        L.d_group_deg, L.d_group_cnt, L.n_groups, L.m, kChunk, (const uint8_t *)L.live, L.bad);
     if (L.Vs)
         hipLaunchKernelGGL(snapshot_k, dim3((L.batch + 63) / 64, (L.n + kSnapRows - 1) / kSnapRows), dim3(64), 0, s,
-                           (const int8_t *)L.V, L.Vs, L.stride, L.batch, L.n, (const uint8_t *)L.live,
+                           (const int8_t *)L.V, L.Vs, L.vpitch, L.batch, L.n, (const uint8_t *)L.live,
                            (const uint32_t *)L.bad);
     hipLaunchKernelGGL(syndrome_finish_k, dim3(nb), dim3(256), 0, s, L.batch, L.live, L.bad, L.iters_used, it + 1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1062,6 +1061,6 @@ int coop_early_end(const DecodeLaunch &L, hipStream_t s)
 {
     if (!L.Vs) return 0;
     hipLaunchKernelGGL(merge_snapshot_k, dim3((L.batch + 63) / 64, (L.n + kSnapRows - 1) / kSnapRows), dim3(64), 0, s,
-                       (int8_t *)L.V, (const int8_t *)L.Vs, L.stride, L.batch, L.n, (const uint8_t *)L.live);
+                       (int8_t *)L.V, (const int8_t *)L.Vs, L.vpitch, L.batch, L.n, (const uint8_t *)L.live);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1232,13 +1232,16 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
 static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
                               hipStream_t s);
 
+// the ET kernel is instantiated for WS = 6 only, and et_after stages the hard
+// bits of all n variables (u16 each) in the workgroup's LDS
+bool coop3_et_in_kernel(const CoopCode &cc, int n) { return cc.S == 48 && (size_t)n * 2 <= sizeof(Smem3<6, 2>); }
+
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
 {
     if (!cc.valid || !coop3_stride_ok(L.stride)) return -1;
-    if (L.early && cc.S == 48) {
+    if (L.early && coop3_et_in_kernel(cc, L.n)) {
         // in-kernel early termination (one launch, coop3_decode<.., ET>)
         if (!L.iters_used) return -1;
-        if ((size_t)L.n * 2 > sizeof(Smem3<6, 2>)) return -1;   // et_after's LDS copy of the hard bits
         if (L.iters == 0) {
             hipLaunchKernelGGL(fill_iters3_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used, 0);
             return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1246,7 +1249,6 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
         return launch_coop3_iters(L, cc, L.iters, nullptr, s);
     }
     if (L.early) {
-        if (L.vpitch != L.stride) return -1;   // the per-iteration helpers address V by the stride
         // one launch per iteration; converged codewords keep iterating inside
         // live workgroups, so their V is snapshot when they converge and
         // merged back at the end (L.Vs), as coop2

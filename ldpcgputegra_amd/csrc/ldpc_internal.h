@@ -36,6 +36,9 @@ struct ldpc_code {
 
 // windowed2 dynamic-LDS pad of a context (capi.hip; mixed batches)
 int ldpc_ctx_set_lds_pad(ldpc_ctx *c, int bytes);
+// can kernel k (ldpc_ctx_set_kernel numbering) schedule this context's code?
+// (no error is recorded either way)
+bool ldpc_ctx_has_kernel(const ldpc_ctx *c, int k);
 
 // error reporting (capi.cpp)
 int ldpc_set_error(int status, const char *fmt, ...);

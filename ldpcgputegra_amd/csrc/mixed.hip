@@ -117,8 +117,7 @@ extern "C" int ldpc_mixed_create(const ldpc_code *const *codes, int n_codes, int
     std::vector<bool> c3(nc, false);
     bool any_c3 = false;
     for (int c = 0; c < n_codes; c++) {
-        c3[c] = ldpc_ctx_set_kernel(mx->ctx[c], 8) == LDPC_OK;
-        (void)ldpc_ctx_set_kernel(mx->ctx[c], 0);
+        c3[c] = ldpc_ctx_has_kernel(mx->ctx[c], 8);
         any_c3 = any_c3 || c3[c];
     }
     const char *pp = getenv("LDPC_MIXED_LDS_PAD");
@@ -191,4 +190,11 @@ extern "C" int ldpc_decode_i8_mixed_async(ldpc_mixed *mx, void *hip_stream, cons
             return join_all(c, ldpc_set_error(LDPC_EDEVICE, "mixed: join"));
     }
     return LDPC_OK;
+}
+
+extern "C" int ldpc_mixed_last_kernel(ldpc_mixed *mx, int code_index, int *kernel)
+{
+    if (!mx || !kernel || code_index < 0 || code_index >= (int)mx->ctx.size())
+        return ldpc_set_error(LDPC_EINVAL, "mixed last kernel: bad arguments");
+    return ldpc_ctx_last_kernel(mx->ctx[code_index], kernel);
 }

@@ -203,6 +203,16 @@ class MixedDecoder:
             self._mx, s, Decoder._ptr(llr), Decoder._ptr(hard), Decoder._ptr(iters_used), ids.ctypes.data,
             ids.size, n_iter, C.byref(p))), self.device)
 
+    def last_kernels(self):
+        """Kernel family each code's sub-batch ran in the last decode (names as
+        Decoder.last_kernel; "none" for a code without codewords so far)."""
+        out = []
+        for c in range(len(self.codes)):
+            k = C.c_int()
+            _lib.check(_lib.lib().ldpc_mixed_last_kernel(self._mx, c, C.byref(k)))
+            out.append(Decoder.KERNEL_NAMES.get(k.value, str(k.value)))
+        return out
+
     def close(self):
         if getattr(self, "_mx", None) is not None and _lib._lib is not None:
             _lib._lib.ldpc_mixed_destroy(self._mx)

@@ -92,9 +92,10 @@ def test_two_rank_bench_on_gpu_matches_single_process():
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
     args = ["--batch", "256", "--iters", "10", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"]
     env = dict(os.environ, LDPC_BENCH_BACKEND="gloo")
-    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                          os.path.join(root, "bench.py"), "--gpus", "2"] + args,
+    env.pop("WORLD_SIZE", None)
+    # plain `python bench.py --gpus 2`, as the driver runs it: bench.py starts
+    # torch.distributed.run itself (a child process, before any GPU call)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"] + args,
                          capture_output=True, text=True, timeout=300, env=env, cwd=root)
     assert out.returncode == 0, out.stderr[-2000:]
     two = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
@@ -104,5 +105,28 @@ def test_two_rank_bench_on_gpu_matches_single_process():
     assert out1.returncode == 0, out1.stderr[-2000:]
     one = json.loads([l for l in out1.stdout.splitlines() if l.startswith("{")][-1])
     assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 512 and one["config"]["global_batch"] == 512
+    assert two["ranks_seen"] == 2 and len(two["per_rank"]) == 2 and all(r["kernel_ms"] > 0 for r in two["per_rank"])
+    assert one["n_gpus"] == 1 and one["ranks_seen"] == 1
     assert two["ber"] == one["ber"] and two["fer"] == one["fer"] and one["fer"] > 0
     assert two["value"] > 0
+
+
+def test_bench_rank_count_checks():
+    """bench.py refuses a rank count it cannot honour instead of silently
+    decoding on fewer GPUs: WORLD_SIZE != --gpus, and more nccl ranks than
+    visible devices (here: none) -- both exit non-zero before any decode."""
+    import subprocess
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    bench = os.path.join(root, "bench.py")
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, bench, "--gpus", "1", "--cpu-seconds", "0"], capture_output=True,
+                         text=True, timeout=120, env=env, cwd=root)
+    assert out.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in out.stderr
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["LDPC_BENCH_BACKEND"] = "nccl"
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    out = subprocess.run([sys.executable, bench, "--gpus", "2", "--cpu-seconds", "0"], capture_output=True,
+                         text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode != 0 and "2 ranks but 0 visible GPUs" in out.stderr

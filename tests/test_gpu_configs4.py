@@ -1,0 +1,144 @@
+"""GPU parity of the configs[4] path exactly as bench.py --mixed runs it, and of
+the coop kernel (5) with its XCD block remap on.
+
+bench.py --mixed decodes ONE 4096-codeword batch per GPU mixing DVB-S2 r1/2
+and the DVB-S2-shaped r3/4, r5/6 (codeword c has rate c % 3: 1366 / 1365 /
+1365 codewords), each rate at its own Eb/N0, 50 iterations at most, early
+termination on.  The per-rate sub-batches run coop3 (r1/2) and coop at grid
+88 (the shaped rates) -- grid % 8 == 0, so the XCD-aware workgroup remap is
+ON; the tests here check exactly those launches against the oracle's
+early-termination semantics (syndrome after every iteration; the reference's
+commented `arret` test, code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:551-553,
+as restated in oracle/ldpc_oracle.c; per-check recurrence :172-546).  The
+shaped codes have no reference build (their tables are not the reference's),
+so the oracle -- pinned against the reference on every code it ships -- is the
+checker.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from ldpcgputegra_amd import Code, Decoder, channel, default_params, load_table
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _bench_mixed_inputs(torch, names, B, seed, ebn0):
+    """The LLR batch bench_mixed() builds (bench.py): rate c % len(names) per
+    codeword, each rate's all-zero codeword through its own device channel."""
+    ids = np.arange(B, dtype=np.int32) % len(names)
+    n = Code(names[0]).n
+    llr = torch.empty((B, n), dtype=torch.int8, device="cuda")
+    for c, name in enumerate(names):
+        code = Code(name)
+        sel = torch.from_numpy(np.where(ids == c)[0]).cuda()
+        tmp = torch.empty((sel.numel(), n), dtype=torch.int8, device="cuda")
+        gen = Decoder(code, max_batch=max(1, sel.numel()))
+        table = channel.i8_table(channel.sigma_from_ebn0(ebn0[name], code.k_info / code.n), 8, 31)
+        gen.awgn_i8_device(tmp, first_cw=c * B, seed=seed, table=table)
+        llr[sel] = tmp
+        gen.close()
+    torch.cuda.synchronize()
+    return ids, llr
+
+
+def test_configs4_mixed_batch_as_benched_vs_oracle():
+    """The whole configs[4] step of bench.py --mixed (MIXED_SETS["configs4"],
+    MIXED_EBN0, batch 4096, 50 it, early termination, seed 2024): every
+    codeword's hard decisions and iterations used equal the oracle's decode
+    under its own code; the kernels that ran are coop3 (r1/2) and coop with
+    the XCD remap on (grid 88 for 1365 / 1366 codewords)."""
+    torch = _torch()
+    import bench
+    from ldpcgputegra_amd.decoder import MixedDecoder
+    names = bench.MIXED_SETS["configs4"]
+    B, iters = 4096, 50
+    ids, llr = _bench_mixed_inputs(torch, names, B, 2024, bench.MIXED_EBN0)
+    mx = MixedDecoder([Code(n) for n in names], max_batch=B)
+    hard = torch.empty((B, llr.shape[1]), dtype=torch.uint8, device="cuda")
+    its = torch.empty(B, dtype=torch.int32, device="cuda")
+    mx.decode_i8_device(llr, hard, ids, iters, params=default_params(early_term=1), iters_used=its)
+    torch.cuda.synchronize()
+    got_h, got_i, host = hard.cpu().numpy(), its.cpu().numpy(), llr.cpu().numpy()
+    kernels = mx.last_kernels()
+    assert kernels == ["coop3", "coop", "coop"], kernels
+    thr = O.host_threads()
+    for c, name in enumerate(names):
+        sel = np.where(ids == c)[0]
+        assert sel.size in (1365, 1366)
+        eh, _, eit = O.decode_i8(load_table(name), host[sel], iters, early_term=True, return_soft=True, threads=thr)
+        assert np.array_equal(got_i[sel], eit), (name, int((got_i[sel] != eit).sum()))
+        bad = np.nonzero((got_h[sel] != eh).any(axis=1))[0]
+        assert bad.size == 0, (name, bad[:16])
+        assert eit.min() < iters                       # early termination is exercised
+    mx.close()
+
+
+@pytest.mark.parametrize("code", ["dvbs2shape_r3_4", "dvbs2shape_r5_6", "dvbs2_r2_3"])
+@pytest.mark.parametrize("early", [False, True])
+def test_coop_xcd_remap_vs_oracle(code, early):
+    """kernel 5 (coop) at batch 128 (grid 8: remap on), fixed iterations and
+    early termination: soft output, hard decisions and iterations used all
+    equal the oracle's."""
+    torch = _torch()
+    t = load_table(code)
+    B, iters = 128, 20
+    ebn0 = {"dvbs2shape_r3_4": 2.8, "dvbs2shape_r5_6": 3.5, "dvbs2_r2_3": 2.2}[code]
+    llr = channel.awgn_i8_host(t.n, B, seed=17, table=channel.i8_table(channel.sigma_from_ebn0(ebn0, t.k_info / t.n)))
+    thr = O.host_threads()
+    eh, es, eit = O.decode_i8(t, llr, iters, early_term=early, return_soft=True, threads=thr)
+    if early:
+        assert eit.min() < iters
+    dec = Decoder(Code(code), max_batch=B, kernel=5)
+    d_hard = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+    d_soft = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
+    d_its = torch.empty(B, dtype=torch.int32, device="cuda")
+    dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=default_params(early_term=int(early)),
+                         soft=d_soft, iters_used=d_its)
+    torch.cuda.synchronize()
+    assert dec.last_kernel == "coop"
+    assert np.array_equal(d_its.cpu().numpy(), eit)
+    assert np.array_equal(d_soft.cpu().numpy(), es)
+    assert np.array_equal(d_hard.cpu().numpy(), eh)
+    dec.close()
+
+
+@pytest.mark.parametrize("kernel,env", [(5, {"LDPC_COOP_ET_KERNEL": "0"}), (8, {"LDPC_COOP3_WS": "4"})])
+def test_per_iteration_early_termination_padded_pitch(kernel, env):
+    """The per-iteration early-termination launches (coop with
+    LDPC_COOP_ET_KERNEL=0; coop3 at WS = 4, whose ET is not in-kernel) address
+    V by its padded row pitch (LDPC_VPITCH_PAD, default 64 codewords): results
+    equal the oracle's (regression: they used to fail with LDPC_EDEVICE)."""
+    torch = _torch()
+    t = load_table("dvbs2_r1_2")
+    B, iters = 64, 30
+    llr = channel.awgn_i8_host(t.n, B, seed=23, table=channel.i8_table(channel.sigma_from_ebn0(1.1, 0.5)))
+    eh, es, eit = O.decode_i8(t, llr, iters, early_term=True, return_soft=True, threads=O.host_threads())
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        dec = Decoder(Code("dvbs2_r1_2"), max_batch=B, kernel=kernel)
+        d_hard = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+        d_soft = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
+        d_its = torch.empty(B, dtype=torch.int32, device="cuda")
+        dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=default_params(early_term=1),
+                             soft=d_soft, iters_used=d_its)
+        torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    assert np.array_equal(d_its.cpu().numpy(), eit)
+    assert np.array_equal(d_soft.cpu().numpy(), es)
+    assert np.array_equal(d_hard.cpu().numpy(), eh)
+    dec.close()
