@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--iters", type=int, default=None, help="default 50 (i8) / 20 (f32)")
     ap.add_argument("--ebn0", type=float, default=1.0, help="Eb/N0 (dB) of the synthetic channel")
     ap.add_argument("--kernel", type=int, default=0,
-                    help="0 auto, 1 generic, 2 windowed, 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2 (packed pairs), 7 lds, 8 coop3")
+                    help="0 auto, 1 generic, 2 windowed, 3 windowed2 S=16, 5 coop, 7 lds, 8 coop3")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (cgroup quota / affinity)")
@@ -523,7 +523,7 @@ def main():
         if world > 1:   # one entry per rank: its device and its own decode-kernel time
             out["per_rank"] = per_rank
             out["backend"] = backend
-        if dec.last_skipped:   # a faster kernel did not apply at this batch size
+        if dec.last_skipped:   # a faster kernel did not apply to these parameters
             out["config"]["kernel_skipped"] = dec.last_skipped
         print(json.dumps(out), flush=True)
     if world > 1:

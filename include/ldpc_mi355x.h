@@ -145,19 +145,20 @@ int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ldpc_ctx **ou
 void ldpc_ctx_destroy(ldpc_ctx *ctx);
 int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
 /* Select kernel family: 0 = auto, 1 = generic (per-edge messages),
- * 2 = windowed layered kernel (compressed messages), 3 / 4 = windowed2
- * (S = 16 / 32), 5 = workgroup-cooperative DVB-S2 kernel, 6 = its packed-pair
- * variant (two codewords per lane; first-group degree 7; early termination by per-iteration launches),
+ * 2 = windowed layered kernel (compressed messages), 3 = windowed2 (S = 16),
+ * 5 = workgroup-cooperative DVB-S2 kernel (coop),
  * 7 = LDS-resident short-code kernel (whole state in LDS; int8 and float),
- * 8 = coop3 (DVB-S2 first-group degree 7: slab waves doing pre + post, i16 chain). */
+ * 8 = coop3 (DVB-S2 first-group degree 7: slab waves doing pre + post, i16 chain).
+ * 4 and 6 (windowed2 S = 32, coop2) were superseded and are rejected
+ * with LDPC_EUNSUPPORTED. */
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel family the last decode actually ran (1 generic, 2 windowed,
- * 3 windowed2 S=16, 4 windowed2 S=32, 5 coop, 6 coop2, 7 lds, 8 coop3; 0 before the first decode). */
+ * 3 windowed2 S=16, 5 coop, 7 lds, 8 coop3; 0 before the first decode). */
 int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
-/* The faster kernel the last automatic selection had to skip because of the
- * batch size (6: coop2, whose V descriptor caps the batch at 16320
- * codewords), 0 when none was. */
+/* The fastest kernel of this code that the last automatic selection could
+ * not use for the call's parameters (8: coop3, 5: coop -- they take OMS / MS
+ * with msg_max <= 63 and var range +-127), 0 when none was skipped. */
 int ldpc_ctx_last_skipped(ldpc_ctx *ctx, int *kernel);
 /* Kernel timing (bench / profiling): when enabled, every decode records HIP
  * events around the decode kernel on the stream it is launched on;

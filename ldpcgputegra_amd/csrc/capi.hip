@@ -35,7 +35,7 @@ struct Scratch {
     size_t msg_bytes = 0;
     void *d_early = nullptr;        // coop early termination: live[stride] u8, bad[stride] u32, iters[stride]
     size_t early_bytes = 0;
-    void *d_Vs = nullptr;           // coop2/coop3 early termination: V snapshot [N+1][stride]
+    void *d_Vs = nullptr;           // coop3 per-iteration early termination: V snapshot [N+1][vpitch]
     size_t Vs_bytes = 0;
     void release()
     {
@@ -59,7 +59,8 @@ struct ldpc_ctx {
     int device = 0;
     int max_batch = 0;
     int max_stride = 0;
-    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3/4 windowed2 S16/S32, 5 coop, 6 coop2, 7 lds, 8 coop3
+    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3 windowed2 (S16), 5 coop, 7 lds, 8 coop3
+                                    // (4 and 6, windowed2 S32 and coop2, were superseded and removed)
     int last_kernel = 0;
     int last_skipped = 0;   // the preferred kernel the last decode could not use at its batch size (0: none)
     int lds_pad = 0;        // extra dynamic LDS per windowed2 workgroup (ldpc_ctx_set_lds_pad)
@@ -68,9 +69,8 @@ struct ldpc_ctx {
     uint32_t *d_edge_var = nullptr;
     int *d_group_deg = nullptr, *d_group_cnt = nullptr;
     WindowedCode wcode{};           // windowed-kernel tables (windowed.hip)
-    Windowed2Code w16{}, w32{};     // windowed2.hip tables, S = 16 and S = 32
+    Windowed2Code w16{};            // windowed2.hip tables, S = 16
     CoopCode coop{};                // coop.hip tables (workgroup-cooperative DVB-S2 path)
-    CoopCode coop2{};               // coop2.hip tables (packed-pair variant, D0 = 7)
     CoopCode coop3{};               // coop3.hip tables (pre + post slab waves, i16 chain, D0 = 7)
     LdsCode lds{};                  // lds.hip tables (LDS-resident short-code decoder)
     Scratch sc;                     // device-API decodes and the unchunked host path
@@ -149,9 +149,7 @@ extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ld
         return fail(ldpc_set_error(LDPC_EDEVICE, "code table upload"));
     if ((rc = windowed_code_upload(h, &c->wcode)) != LDPC_OK) return fail(rc);
     if ((rc = windowed2_upload(h, 16, 2, &c->w16)) != LDPC_OK) return fail(rc);
-    if ((rc = windowed2_upload(h, 32, 1, &c->w32)) != LDPC_OK) return fail(rc);
     if ((rc = coop_upload(h, &c->coop)) != LDPC_OK) return fail(rc);
-    if ((rc = coop2_upload(h, &c->coop2)) != LDPC_OK) return fail(rc);
     if ((rc = coop3_upload(h, &c->coop3)) != LDPC_OK) return fail(rc);
     if ((rc = lds_upload(h, &c->lds)) != LDPC_OK) return fail(rc);
     *out = c;
@@ -165,9 +163,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     windowed_code_free(&c->wcode);
     windowed2_free(&c->w16);
-    windowed2_free(&c->w32);
     coop_free(&c->coop);
-    coop_free(&c->coop2);
     coop_free(&c->coop3);
     lds_free(&c->lds);
     for (auto &pr : c->events) {
@@ -199,9 +195,8 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 bool ldpc_ctx_has_kernel(const ldpc_ctx *c, int k)
 {
     if (!c || k < 0 || k > 8) return false;
-    return !((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || (k == 4 && !c->w32.valid) ||
-             (k == 5 && !c->coop.valid) || (k == 6 && !c->coop2.valid) || (k == 7 && !c->lds.valid) ||
-             (k == 8 && !c->coop3.valid));
+    return !((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || k == 4 ||
+             (k == 5 && !c->coop.valid) || k == 6 || (k == 7 && !c->lds.valid) || (k == 8 && !c->coop3.valid));
 }
 
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
@@ -295,10 +290,11 @@ static int check_params(const ldpc_ctx *c, int batch, int n_iter, const ldpc_par
     return LDPC_OK;
 }
 
-// kernel family for this call: 1 generic, 2 windowed, 3 windowed2/S16,
-// 4 windowed2/S32, 5 coop (workgroup-cooperative), 6 coop2 (packed pairs),
-// 7 lds (LDS-resident short codes, int8 and float), 8 coop3 (slab waves doing
-// pre + post, i16 chain)
+// kernel family for this call: 1 generic, 2 windowed, 3 windowed2 (S=16),
+// 5 coop (workgroup-cooperative), 7 lds (LDS-resident short codes, int8 and
+// float), 8 coop3 (slab waves doing pre + post, i16 chain).  last_skipped
+// records the fastest kernel of this code that the automatic choice could not
+// use for these parameters (algorithm, message / variable ranges), 0 if none
 static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int stride)
 {
     c->last_skipped = 0;
@@ -308,22 +304,20 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
     const bool w2 = windowed2_params_ok(p);
     const bool co = c->coop.valid && coop_params_ok(p);
-    const bool co2 = c->coop2.valid && coop2_params_ok(p) && coop2_stride_ok(stride);
     const bool co3 = c->coop3.valid && coop3_params_ok(p) && coop3_stride_ok(stride);
     switch (c->kernel) {
     case 1: return 1;
     case 2: return w1 ? 2 : -1;
     case 3: return (w2 && c->w16.valid) ? 3 : -1;
-    case 4: return (w2 && c->w32.valid) ? 4 : -1;
     case 5: return co ? 5 : -1;
-    case 6: return co2 ? 6 : -1;
     case 8: return co3 ? 8 : -1;
+    case 4:
+    case 6: return -1;
     default:
-        if (co3 && getenv_int("LDPC_DEFAULT_COOP3", 1)) return 8;
-        if (co2) return 6;
-        // coop2's V descriptor caps its batch (coop2_stride_ok): say so
-        if (c->coop2.valid && coop2_params_ok(p)) c->last_skipped = 6;
+        if (co3) return 8;
+        if (c->coop3.valid) c->last_skipped = 8;
         if (co) return 5;
+        if (c->coop.valid && !c->last_skipped) c->last_skipped = 5;
         if (w2 && c->w16.valid) return 3;
         if (lds_preferred(c->code, c->lds, false)) return 7;
         if (w1) return 2;
@@ -373,7 +367,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     }
     const bool win = kern >= 2;
     // + a sink row / sink words for the masked stores of the coop kernel
-    const size_t msg_zero = (kern == 6 || kern == 8 ? coop2_msg_bytes(h, stride)
+    const size_t msg_zero = (kern == 8   ? coop3_msg_bytes(h, stride)
                              : win    ? windowed_msg_bytes(h, stride)
                                       : (size_t)h->e * stride * esz) +
                             4096;
@@ -386,7 +380,12 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     // on the same few L2 channels.  Measured (DVB-S2 r1/2, 4096 cw, 50 it,
     // coop3): pitch 4096 57.6 ms, 4160 / 4224 49.7 / 49.6 ms, 4352 50.4,
     // 4608 52.7, 5120 57.2
-    const int vpad = (kern == 8 || kern == 5) ? std::max(0, getenv_int("LDPC_VPITCH_PAD", 64)) / 64 * 64 : 0;
+    // coop3 with LDPC_COOP3_GROUPED=1: V in the grouped layout [stride / 16][N + 1][16]
+    // (a workgroup's rows contiguous) -- not with the per-iteration
+    // early-termination helpers, which address V[row][pitch]
+    const bool vpriv = kern == 8 && !is_float && getenv_int("LDPC_COOP3_GROUPED", 0) != 0 &&
+                       (!p->early_term || coop3_et_in_kernel(c->coop3, h->n));
+    const int vpad = (kern == 8 || kern == 5) && !vpriv ? std::max(0, getenv_int("LDPC_VPITCH_PAD", 64)) / 64 * 64 : 0;
     const int vpitch = stride + vpad;
     if ((rc = ensure(&sc.d_V, &sc.V_bytes, (size_t)(h->n + 1) * vpitch * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_need)) != LDPC_OK) return rc;
@@ -397,7 +396,8 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         if (launch_interleave_f32((const float *)d_llr, (float *)sc.d_V, h->n, batch, vpitch, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
     } else {
-        if (launch_interleave_i8((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, vpitch, s))
+        if (vpriv ? launch_interleave_i8_grouped((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, stride, s)
+                  : launch_interleave_i8((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, vpitch, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
     }
     DecodeLaunch L{};
@@ -406,6 +406,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     if (kern == 8) L.P = (int8_t *)sc.d_msg + msg_zero;
     L.stride = stride;
     L.vpitch = vpitch;
+    L.vpriv = vpriv;
     L.batch = batch;
     L.iters = n_iter;
     L.is_float = is_float;
@@ -424,15 +425,15 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
     L.iters_used = d_iters;
     L.lds_pad = c->lds_pad;
-    if ((kern == 5 || kern == 6 || kern == 8) && p->early_term) {
+    if ((kern == 5 || kern == 8) && p->early_term) {
         // live u8 | bad u32 | iterations used i32 (when the caller passed none)
         if ((rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
         L.bad = (uint32_t *)sc.d_early;
         if (!L.iters_used) L.iters_used = (int32_t *)((char *)sc.d_early + (size_t)stride * 4);
         L.live = (uint8_t *)sc.d_early + (size_t)stride * 8;
-        // V snapshots: only the per-iteration launches need them (coop2, and
-        // coop3 where its in-kernel early termination does not apply)
-        if (kern == 6 || (kern == 8 && !coop3_et_in_kernel(c->coop3, h->n))) {
+        // V snapshots: only coop3's per-iteration launches need them (where
+        // its in-kernel early termination does not apply)
+        if (kern == 8 && !coop3_et_in_kernel(c->coop3, h->n)) {
             if ((rc = ensure(&sc.d_Vs, &sc.Vs_bytes, (size_t)(h->n + 1) * vpitch)) != LDPC_OK) return rc;
             L.Vs = (int8_t *)sc.d_Vs;
         }
@@ -444,9 +445,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         HIP_TRY(hipEventRecord(ev0, s));
     }
     int lr = kern == 8   ? launch_coop3(L, c->coop3, s)
-             : kern == 6 ? launch_coop2(L, c->coop2, s)
              : kern == 5 ? launch_coop(L, c->coop, s)
-             : kern == 4 ? launch_windowed2(L, c->w32, s)
              : kern == 3 ? launch_windowed2(L, c->w16, s)
              : kern == 2 ? launch_windowed(L, c->wcode, s)
                          : launch_generic(L, s);
@@ -462,6 +461,8 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     if (d_hard || d_soft) {
         int r2 = is_float ? launch_deinterleave_f32((const float *)sc.d_V, d_hard, (float *)d_soft, h->n, batch,
                                                     vpitch, s)
+                 : vpriv  ? launch_deinterleave_i8_grouped((const int8_t *)sc.d_V, d_hard, (int8_t *)d_soft, h->n,
+                                                           batch, s)
                           : launch_deinterleave_i8((const int8_t *)sc.d_V, d_hard, (int8_t *)d_soft, h->n,
                                                    batch, vpitch, s);
         if (r2) return ldpc_set_error(LDPC_EDEVICE, "deinterleave: %s", hipGetErrorString(hipGetLastError()));

@@ -19,7 +19,7 @@ bool coop_params_ok(const ldpc_params *p);
 int coop_upload(const ldpc_code *h, CoopCode *cc);
 void coop_free(CoopCode *cc);
 int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
-// early termination around per-iteration launches (coop and coop2): init,
+// early termination around per-iteration launches (coop, coop3 at WS != 6): init,
 // syndrome after iteration `it` (0-based; with L.Vs, snapshot of the codewords
 // converging now), and the final merge of the snapshots into V (L.Vs only)
 int coop_early_begin(const DecodeLaunch &L, hipStream_t s);
@@ -29,7 +29,7 @@ int coop_early_end(const DecodeLaunch &L, hipStream_t s);
 int coop_plan_windows(const ldpc_code *h, int S, int R, int dist, std::vector<int> &first, std::vector<int> &count,
                       int *tail, int *n_fwd);
 
-// ---- window plan shared by coop.hip and coop2.hip ----
+// ---- window plan shared by coop.hip and coop3.hip ----
 // Slot record [recw] u32: edge variables [D0], meta, forwarding codes (u16 per
 // information edge: dW << (6 + EB) | slot << EB | edge, EB = coop_fwd_eb(X);
 // 0xFFFF = none); codes with more than 8 information edges (X > 8) carry the
@@ -54,16 +54,11 @@ struct CoopPlan {
 // forwarded through the LDS ring; -1: no cooperative schedule
 int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPlan &o, bool want_tab);
 
-// ---- coop2.hip: packed-pair variant (two codewords per lane, 16-bit halves) ----
-bool coop2_params_ok(const ldpc_params *p);
-bool coop2_stride_ok(int stride);                    // V row pitch fits the buffer descriptor
-size_t coop2_msg_bytes(const ldpc_code *h, int stride);
-int coop2_upload(const ldpc_code *h, CoopCode *cc);
-int launch_coop2(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
-
 // ---- coop3.hip: slab waves doing pre + post, i16 chain (D0 = 7) ----
 bool coop3_params_ok(const ldpc_params *p);
 bool coop3_stride_ok(int stride);
+// compressed messages: [stride / 16][m + 1][8 pairs][2] u32 (4 B per codeword and check; row m is the sink)
+size_t coop3_msg_bytes(const ldpc_code *h, int stride);
 int coop3_upload(const ldpc_code *h, CoopCode *cc);
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
 // early termination inside the coop3 launch (else per-iteration launches + V snapshots)

@@ -129,6 +129,7 @@ struct Coop3Args {
     int32_t *iters_used;
     int iters, batch, m0, d1;
     int pitch, G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
+    size_t wgoff;                     // bytes between two codeword groups' V (see DecodeLaunch::vpriv)
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
 };
 
@@ -569,7 +570,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     // contiguous: a wave's 8 o-edge gathers / x-edge stores touch 1-2 lines,
     // not 8), back into V at the end
     {
-        int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * CW;
+        int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * a.wgoff;
         int8_t *ppar = a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
 #pragma unroll 8
         for (int j = threadIdx.x; j < a.m; j += blockDim.x)
@@ -580,7 +581,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     auto parity_out = [&]() {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * CW;
+        int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * a.wgoff;
         const int8_t *ppar = a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
 #pragma unroll 8
         for (int j = threadIdx.x; j < a.m; j += blockDim.x)
@@ -589,7 +590,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     // ---- ET state: [0] live codewords, [1] failing codewords (syndrome)
     __shared__ uint32_t et_sh[2];
     constexpr int NT = 64 * (WS + 1);
-    const char *etV = (const char *)a.V + (size_t)wg * CW;
+    const char *etV = (const char *)a.V + (size_t)wg * a.wgoff;
     const char *etP = (const char *)a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
     auto et_row = [&](uint32_t v) -> const uint4 * {   // V row piece of variable v (parity rows: in P)
         return (int)v < a.k ? (const uint4 *)(etV + (size_t)v * (size_t)a.pitch)
@@ -832,7 +833,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     // "Two waves per SIMD", item 4)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
     const int kl = lane >> 3, q = lane & 7;
-    const char *Vb = (const char *)a.V + (size_t)wg * CW;
+    const char *Vb = (const char *)a.V + (size_t)wg * a.wgoff;
     const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
     // parity rows k + j of this group at Pb + 16 j: row r at Pb - 16 k + 16 r
     char *Pr = (char *)a.P + ((size_t)wg * (size_t)(a.m + 1) - (size_t)a.k) * 16;
@@ -1138,8 +1139,10 @@ static uint32_t fwd_code3(int dW, int slot, int e, int S)
 
 bool coop3_params_ok(const ldpc_params *p) { return coop_params_ok(p); }
 
-// V and P are addressed with 64-bit flat addresses: no batch cap (coop2 has one)
+// V and P are addressed with 64-bit flat addresses: no batch cap
 bool coop3_stride_ok(int stride) { return stride > 0 && stride % 64 == 0; }
+
+size_t coop3_msg_bytes(const ldpc_code *h, int stride) { return (size_t)(h->m + 1) * (size_t)stride * 4; }
 
 int coop3_upload(const ldpc_code *h, CoopCode *cc)
 {
@@ -1251,7 +1254,7 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     if (L.early) {
         // one launch per iteration; converged codewords keep iterating inside
         // live workgroups, so their V is snapshot when they converge and
-        // merged back at the end (L.Vs), as coop2
+        // merged back at the end (L.Vs)
         if (!L.Vs || coop_early_begin(L, s)) return -1;
         for (int it = 0; it < L.iters; it++)
             if (launch_coop3_iters(L, cc, 1, L.live, s) || coop_early_after_iter(L, it, s)) return -1;
@@ -1271,7 +1274,10 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.V = (int8_t *)L.V;
     a.Mc = (uint8_t *)L.msg;
     a.tab = cc.d_tab;
-    a.pitch = L.vpitch;
+    // V layout: rows of L.vpitch codewords, a group's 16 B at wg * 16 in each;
+    // or (L.vpriv) every group's rows contiguous, [stride / 16][n + 1][16]
+    a.pitch = L.vpriv ? CW : L.vpitch;
+    a.wgoff = L.vpriv ? (size_t)(L.n + 1) * CW : (size_t)CW;
     a.G = cc.nw * iters;
     a.nw = cc.nw;
     a.tail = cc.tail;

@@ -530,20 +530,12 @@ int launch_windowed2(const DecodeLaunch &L, const Windowed2Code &w, hipStream_t 
     a.iters_used = L.iters_used;
     const int G = 64 / w.S;
     const int grid = L.stride / G;   // stride % 64 == 0 -> grid % 8 == 0
-    if (w.S == 32) {
-        if (w.d0 == 7) return launch3<7, 32, 1>(a, grid, s, L.lds_pad);
-        if (w.d0 == 10) return launch3<10, 32, 1>(a, grid, s, L.lds_pad);
-        if (w.d0 == 14) return launch3<14, 32, 1>(a, grid, s, L.lds_pad);
-        if (w.d0 == 22) return launch3<22, 32, 1>(a, grid, s, L.lds_pad);
-        if (w.d0 == 27) return launch3<27, 32, 1>(a, grid, s, L.lds_pad);
-        if (w.d0 == 30) return launch3<30, 32, 1>(a, grid, s, L.lds_pad);
-    } else {
-        if (w.d0 == 7) return launch3<7, 16, 2>(a, grid, s, L.lds_pad);
-        if (w.d0 == 10) return launch3<10, 16, 2>(a, grid, s, L.lds_pad);
-        if (w.d0 == 14) return launch3<14, 16, 2>(a, grid, s, L.lds_pad);
-        if (w.d0 == 22) return launch3<22, 16, 2>(a, grid, s, L.lds_pad);
-        if (w.d0 == 27) return launch3<27, 16, 2>(a, grid, s, L.lds_pad);
-        if (w.d0 == 30) return launch3<30, 16, 2>(a, grid, s, L.lds_pad);
-    }
+    if (w.S != 16) return -1;   // S = 32 (one codeword per 32 lanes) was superseded and removed
+    if (w.d0 == 7) return launch3<7, 16, 2>(a, grid, s, L.lds_pad);
+    if (w.d0 == 10) return launch3<10, 16, 2>(a, grid, s, L.lds_pad);
+    if (w.d0 == 14) return launch3<14, 16, 2>(a, grid, s, L.lds_pad);
+    if (w.d0 == 22) return launch3<22, 16, 2>(a, grid, s, L.lds_pad);
+    if (w.d0 == 27) return launch3<27, 16, 2>(a, grid, s, L.lds_pad);
+    if (w.d0 == 30) return launch3<30, 16, 2>(a, grid, s, L.lds_pad);
     return -1;
 }

@@ -54,11 +54,11 @@ class Decoder:
 
     # -- configuration
     def set_kernel(self, kernel):
-        """0 = auto, 1 = generic (per-edge messages), 2 = windowed, 3/4 =
-        windowed2 (S = 16/32), 5 = workgroup-cooperative DVB-S2 kernel, 6 = its
-        packed-pair variant (two codewords per lane; DVB-S2 r1/2, early termination by per-iteration launches),
+        """0 = auto, 1 = generic (per-edge messages), 2 = windowed, 3 =
+        windowed2 (S = 16), 5 = workgroup-cooperative DVB-S2 kernel (coop),
         7 = LDS-resident short-code kernel (int8 and float), 8 = coop3 (slab waves
-        doing pre + post, i16 chain; the DVB-S2 r1/2 default)."""
+        doing pre + post, i16 chain; the DVB-S2 r1/2 default).  4 and 6
+        (windowed2 S = 32, coop2) were superseded and removed."""
         _lib.check(_lib.lib().ldpc_ctx_set_kernel(self._ctx, int(kernel)))
 
     @property
@@ -87,8 +87,9 @@ class Decoder:
 
     @property
     def last_skipped(self):
-        """Name of the faster kernel the last decode skipped because of its
-        batch size (coop2's batch cap), None when none was."""
+        """Name of the fastest kernel of this code that the last automatic
+        selection could not use for its parameters (e.g. msg_max > 63 on the
+        DVB-S2 fast paths), None when none was skipped."""
         k = C.c_int()
         _lib.check(_lib.lib().ldpc_ctx_last_skipped(self._ctx, C.byref(k)))
         return self.KERNEL_NAMES.get(k.value, str(k.value)) if k.value else None

@@ -1,7 +1,8 @@
-"""CPU model of coop2.hip's packed-pair check arithmetic (test infrastructure,
-no GPU).
+"""CPU model of the packed-pair check arithmetic of pk16.h (test
+infrastructure, no GPU), which coop3.hip's slab waves use (first written for
+the since-removed coop2 kernel).
 
-coop2.hip keeps two codewords per VGPR (one per 16-bit half): V in the "R
+The kernel keeps two codewords per VGPR (one per 16-bit half): V in the "R
 form" 256 x + 255, messages in the "C form" 256 m, and a check's messages for
 a codeword pair as two dwords -- MA (a 2-bit code per edge and codeword) and
 MB (the cst1 / cst2 bytes) -- decoded with v_perm_b32 through the byte table

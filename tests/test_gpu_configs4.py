@@ -142,3 +142,32 @@ def test_per_iteration_early_termination_padded_pitch(kernel, env):
     assert np.array_equal(d_soft.cpu().numpy(), es)
     assert np.array_equal(d_hard.cpu().numpy(), eh)
     dec.close()
+
+
+@pytest.mark.parametrize("early,batch", [(False, 200), (True, 200), (False, 1024)])
+def test_coop3_grouped_layout_vs_oracle(early, batch):
+    """coop3 with V in the grouped layout (LDPC_COOP3_GROUPED=1: each
+    16-codeword group's rows contiguous, [stride/16][N+1][16]) -- ragged and
+    whole-workgroup batches, fixed iterations and in-kernel early termination:
+    soft output, hard decisions and iterations used equal the oracle's."""
+    torch = _torch()
+    t = load_table("dvbs2_r1_2")
+    iters = 20
+    llr = channel.awgn_i8_host(t.n, batch, seed=29, table=channel.i8_table(channel.sigma_from_ebn0(1.1, 0.5)))
+    eh, es, eit = O.decode_i8(t, llr, iters, early_term=early, return_soft=True, threads=O.host_threads())
+    os.environ["LDPC_COOP3_GROUPED"] = "1"
+    try:
+        dec = Decoder(Code("dvbs2_r1_2"), max_batch=batch, kernel=8)
+        d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+        d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
+        d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
+        dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=default_params(early_term=int(early)),
+                             soft=d_soft, iters_used=d_its)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["LDPC_COOP3_GROUPED"]
+    assert dec.last_kernel == "coop3"
+    assert np.array_equal(d_its.cpu().numpy(), eit)
+    assert np.array_equal(d_soft.cpu().numpy(), es)
+    assert np.array_equal(d_hard.cpu().numpy(), eh)
+    dec.close()

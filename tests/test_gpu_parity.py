@@ -31,19 +31,17 @@ def decoder(code, kernel=0, max_batch=4096):
 
 def kernels_for(code):
     """Kernel families that can run this code: 1 generic, 2 windowed,
-    3 windowed2 (S=16), 4 windowed2 (S=32), 5 coop (workgroup-cooperative),
-    6 coop2 (its packed-pair variant, first-group degree 7), 7 lds (LDS-resident
-    short codes), 8 coop3 (slab waves doing pre + post, i16 chain)."""
+    3 windowed2 (S=16), 5 coop (workgroup-cooperative), 7 lds (LDS-resident
+    short codes), 8 coop3 (slab waves doing pre + post, i16 chain; first-group
+    degree 7).  (4 = windowed2 S=32 and 6 = coop2 were superseded and removed.)"""
     ks = [1]
     c = Code(code)
     if c.plan_info()["windowed"]:
         ks.append(2)
     if c.window_plan(16, 2):
-        ks += [3, 4]
+        ks.append(3)
     if c.coop_plan() is not None and c.max_deg in (7, 10, 14, 22):
         ks.append(5)
-    if c.coop_plan(24, 3) is not None and c.max_deg == 7:
-        ks.append(6)
     if c.coop_plan(32, 2, 2) is not None and c.max_deg == 7:
         ks.append(8)
     if c.layer_info()["lds_i8"]:
@@ -268,7 +266,7 @@ def test_dvbs2_full_batch_vs_reference():
     s1 = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
     h2 = torch.empty_like(h1)
     dec.decode_i8_device(llr, h1, 50, soft=s1)
-    assert dec.last_kernel in ("coop2", "coop3")
+    assert dec.last_kernel == "coop3"
     dec.decode_i8_device(llr[:1000], h2[:1000], 50)           # ragged shard
     dec.decode_i8_device(llr[1000:], h2[1000:], 50)
     torch.cuda.synchronize()
@@ -289,11 +287,10 @@ def test_dvbs2_full_batch_vs_reference():
     assert np.array_equal(s1.cpu().numpy()[sel], ref_soft)
 
 
-@pytest.mark.parametrize("kernel", [5, 6, 8])
+@pytest.mark.parametrize("kernel", [5, 8])
 @pytest.mark.parametrize("batch,ebn0", [(40, 1.1), (64, 1.1), (1024, 1.0)])
 def test_coop2_early_termination_vs_oracle(batch, ebn0, kernel):
-    """coop (5, in-kernel early termination), coop2 (6, per-iteration
-    launches) and coop3 (8, in-kernel) with early termination on whole and
+    """coop (5) and coop3 (8), both with in-kernel early termination, on whole and
     partial workgroups and, at batch 1024 (grid 64), with the XCD block remap
     on, as bench.py --mixed runs it: hard decisions, soft output and iterations
     used all equal the oracle's (syndrome after every iteration)."""
@@ -312,7 +309,7 @@ def test_coop2_early_termination_vs_oracle(batch, ebn0, kernel):
         dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, 50, params=default_params(early_term=1),
                              soft=d_soft, iters_used=d_its)
         torch.cuda.synchronize()
-        assert dec.last_kernel == {5: "coop", 6: "coop2", 8: "coop3"}[kernel]
+        assert dec.last_kernel == {5: "coop", 8: "coop3"}[kernel]
         assert np.array_equal(d_its.cpu().numpy(), ref_its), rep
         assert np.array_equal(d_soft.cpu().numpy(), ref_soft), rep
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard), rep
@@ -418,11 +415,10 @@ def test_quantize_f32_i8_vs_oracle():
         assert np.array_equal(qd.cpu().numpy(), ref), (factor, lo, hi)
 
 
-def test_dvbs2_batch_above_coop2_cap_vs_reference():
-    """A batch above coop2's 16320-codeword cap (coop2_stride_ok): coop3 has
-    no cap and runs it -- every hard decision equals the reference SSE
-    decoder's (10 iterations); with coop3 disabled the automatic selection
-    falls back and reports the skipped coop2 (ldpc_ctx_last_skipped)."""
+def test_dvbs2_large_batch_vs_reference():
+    """A batch of 16464 codewords (1029 workgroups: four per CU and a ragged
+    last one): coop3 has no batch cap -- every hard decision equals the
+    reference SSE decoder's (10 iterations)."""
     torch = _torch()
     t = load_table("dvbs2_r1_2")
     B = 16384 + 80
@@ -442,15 +438,27 @@ def test_dvbs2_batch_above_coop2_cap_vs_reference():
         exp = O.decode_i8(t, host_llr, 10, threads=thr)
     diff = np.nonzero((got != exp).any(axis=1))[0]
     assert diff.size == 0, "codewords differing from the reference: %s" % diff[:16]
-    os.environ["LDPC_DEFAULT_COOP3"] = "0"
-    try:
-        dec.decode_i8_device(llr[:B // 2 + 64], hard[:B // 2 + 64], 2)
-        assert dec.last_skipped is None                        # 8256 codewords: coop2 applies
-        assert dec.last_kernel == "coop2"
-        dec.decode_i8_device(llr, hard, 2)
-        assert dec.last_kernel != "coop2" and dec.last_skipped == "coop2"
-    finally:
-        del os.environ["LDPC_DEFAULT_COOP3"]
+
+
+def test_fast_kernel_fallback_is_reported():
+    """Parameters the fast DVB-S2 kernels do not take (msg_max > 63) fall back
+    to a general kernel -- bit-exact with the oracle -- and the context reports
+    the skipped kernel (ldpc_ctx_last_skipped = coop3 for r1/2, coop for r2/3)."""
+    t = load_table("dvbs2_r1_2")
+    llr = channel.awgn_i8_host(t.n, 16, seed=4, table=channel.i8_table(channel.sigma_from_ebn0(1.0, 0.5)))
+    p = default_params(msg_max=100, msg_min=-100)
+    dec = decoder("dvbs2_r1_2", 0, 64)
+    got = dec.decode_i8(llr, 6, p)
+    assert dec.last_kernel not in ("coop3", "coop") and dec.last_skipped == "coop3"
+    assert np.array_equal(got, O.decode_i8(t, llr, 6, O.OMS, 1, msg_max=100))
+    dec.decode_i8(llr, 6)
+    assert dec.last_kernel == "coop3" and dec.last_skipped is None
+    t2 = load_table("dvbs2_r2_3")
+    llr2 = channel.awgn_i8_host(t2.n, 16, seed=4, table=channel.i8_table(channel.sigma_from_ebn0(2.0, 2 / 3)))
+    d2 = decoder("dvbs2_r2_3", 0, 64)
+    got2 = d2.decode_i8(llr2, 6, p)
+    assert d2.last_skipped == "coop"
+    assert np.array_equal(got2, O.decode_i8(t2, llr2, 6, O.OMS, 1, msg_max=100))
 
 
 def test_host_path_chunked_vs_device():
