@@ -304,7 +304,7 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
     const bool w2 = windowed2_params_ok(p);
     const bool co = c->coop.valid && coop_params_ok(p);
-    const bool co3 = c->coop3.valid && coop3_params_ok(p) && coop3_stride_ok(stride);
+    const bool co3 = c->coop3.valid && coop3_params_ok(p, c->coop3) && coop3_stride_ok(stride);
     switch (c->kernel) {
     case 1: return 1;
     case 2: return w1 ? 2 : -1;

@@ -55,7 +55,7 @@ struct CoopPlan {
 int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPlan &o, bool want_tab);
 
 // ---- coop3.hip: slab waves doing pre + post, i16 chain (D0 = 7) ----
-bool coop3_params_ok(const ldpc_params *p);
+bool coop3_params_ok(const ldpc_params *p, const CoopCode &cc);
 bool coop3_stride_ok(int stride);
 // compressed messages: [stride / 16][m + 1][8 pairs][2] u32 (4 B per codeword and check; row m is the sink)
 size_t coop3_msg_bytes(const ldpc_code *h, int stride);

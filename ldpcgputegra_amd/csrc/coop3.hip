@@ -43,6 +43,12 @@
 //   information edges (odd-degree flip included), T = cst(min over them);
 // = med3(med3(eps*Y + A, c_o, eps*Y + B), L, H) with A = c_o - eps*m_x - off,
 //   B = c_o - eps*m_x + off, L = max(c_o - T, -127), H = min(c_o + T, 127).
+// NMS (CDecoder_NMS_fixed_SSE.cpp:188-240: cst = (min * factor) >> 5, no
+// offset): the o message is eps * sign(c_x) * min(trunc(|c_x| f / 32), T), so
+//   V[p_i] = med3(med3(t >> 5, c_o, (t + 31) >> 5), L, H),  t = eps f Y + A,
+// with A = 32 c_o - eps f m_x (floor and ceiling of c_o + eps f c_x / 32 in
+// the two halves of one v_pk_mad_i16, the median with c_o truncates toward
+// c_o): 4 dependent instructions per check.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -129,6 +135,7 @@ struct Coop3Args {
     int32_t *iters_used;
     int iters, batch, m0, d1;
     int pitch, G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
+    uint32_t nmsf;                    // NMS factor per half (value form)
     size_t wgoff;                     // bytes between two codeword groups' V (see DecodeLaunch::vpriv)
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
 };
@@ -153,6 +160,13 @@ LDPC_DEV uint32_t pk_add(uint32_t a, uint32_t b) { return us(sv(a) + sv(b)); }
 
 constexpr uint32_t V127 = 0x007F007Fu, VNEG127 = 0xFF81FF81u;   // +-127 per half (value form)
 
+LDPC_DEV uint32_t pk_mul_lo(uint32_t a, uint32_t b) { return us(__builtin_bit_cast(s16x2, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b))); }
+// NMS constant of a clipped minimum r (R form, value <= 63) for factor f <= 64
+// (value form per half): (v * f) >> 5 as a value / in C form (256 x)
+LDPC_DEV uint32_t nms_v(uint32_t r, uint32_t f) { return us(__builtin_bit_cast(s16x2, __builtin_bit_cast(u16x2, pk_mul_lo(pk_ashr8(r), f)) >> (unsigned short)5)); }
+LDPC_DEV uint32_t nms_c(uint32_t r, uint32_t f) { return (pk_mul_lo(pk_ashr8(r), f) << 3) & HIBYTES; }   // (<= 4032 << 3: no carry between halves)
+LDPC_DEV uint32_t pk_shl5(uint32_t a) { return us(sv(a) << (short)5); }
+
 // what a period reads from LDS, issued together at its start
 struct PreIn {
     uint32_t v[D0 - 1];               // raw V dwords (info edges, entry D0-1)
@@ -168,7 +182,7 @@ struct PfIn {                         // the LDS-DMA gathers of window p+1+R
     uint32_t rv, chk2;
 };
 
-template <int WS, int R>
+template <int WS, int R, bool NMS = false>
 struct Slab3 {
     using SM = Smem3<WS, R>;
     static constexpr int S = SM::S, NR = SM::NR;
@@ -181,6 +195,7 @@ struct Slab3 {
     uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
     uint32_t fsel;                    // ... of a forwarded u16 (0x050d040d, in a VGPR)
     PkK K;
+    uint32_t fk;                      // NMS factor per half (value form)
     // per-lane constants of the LDS-DMA gathers (lane (kl, j): j < 6 a V row, j >= 6 a message piece)
     const char *g1base, *g2base;
     uint32_t g1mul, g1mask, recsel;
@@ -333,7 +348,6 @@ struct Slab3 {
                 min1 = pk_min(min1, aj);
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
-            const uint32_t T = pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0);   // cst over the info edges
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
             const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), neg127);
             const uint32_t ao = abs_r(cor, c510);
@@ -346,11 +360,21 @@ struct Slab3 {
             s.mx = mx;
             // chain constants in value form (R >> 8, C >> 8), both codewords at once
             COV = pk_ashr8(cor);
-            const uint32_t TV = pk_ashr8(T), EM = pk_sra15(kb);   // EM: -1 where eps = -1
-            EPS = EM | 0x00010001u;
-            const uint32_t base = pk_sub(COV, pk_sub(pk_ashr8(mx) ^ EM, EM));   // c_o - eps * m_x
-            A = pk_sub(base, a.offp);
-            B = pk_add(base, a.offp);
+            const uint32_t EM = pk_sra15(kb);   // EM: -1 where eps = -1
+            uint32_t TV;                        // cst over the info edges (value form)
+            if constexpr (NMS) {
+                TV = nms_v(pk_min(min1, K.rmm), fk);
+                EPS = pk_sub(fk ^ EM, EM);                                    // eps * f
+                const uint32_t efm = pk_mul_lo(pk_ashr8(mx), EPS);            // eps * f * m_x
+                A = pk_sub(pk_shl5(COV), efm);                                // 32 c_o - eps f m_x
+                B = pk_add(A, 0x001F001Fu);
+            } else {
+                TV = pk_ashr8(pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0));
+                EPS = EM | 0x00010001u;
+                const uint32_t base = pk_sub(COV, pk_sub(pk_ashr8(mx) ^ EM, EM));   // c_o - eps * m_x
+                A = pk_sub(base, a.offp);
+                B = pk_add(base, a.offp);
+            }
             L = pk_max(pk_sub(COV, TV), VNEG127);
             H = pk_min(pk_add(COV, TV), V127);
             if constexpr (FZ) {   // converged codewords: L = H = V[p_i] as read, the step returns it
@@ -366,15 +390,18 @@ struct Slab3 {
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
                 const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
-                const uint32_t aj = abs_r(pk_min(c, K.rmm), c510);
+                // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2
+                const uint32_t aj = NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510);
                 s.c[J] = c;
                 s.a[J] = aj;
                 sacc ^= c;
                 min2 = pk_max(min1, pk_min(aj, min2));
                 min1 = pk_min(min1, aj);
             });
-            const uint32_t k1 = pk_min(pk_max(pk_sub(min2, K.coff), K.r0), K.rmm) & HIBYTES;
-            const uint32_t k2 = pk_min(pk_max(pk_sub(min1, K.coff), K.r0), K.rmm) & HIBYTES;
+            const uint32_t k1 = NMS ? nms_c(pk_min(min2, K.rmm), fk)
+                                    : pk_min(pk_max(pk_sub(min2, K.coff), K.r0), K.rmm) & HIBYTES;
+            const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
+                                    : pk_min(pk_max(pk_sub(min1, K.coff), K.r0), K.rmm) & HIBYTES;
             const uint32_t P = (sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u)) & SIGNS;
             uint32_t MAn = 0;
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
@@ -387,13 +414,19 @@ struct Slab3 {
             s.mn1 = MAn;
             s.mn2 = perm(k2, k1, 0x07030501u);
             // the chain passes V[p_0] (the tail's last edge) on: A = B = c_o = L = H = y
+            // (NMS: A = 32 y, B = 32 y + 31)
             const uint32_t Y = pk_ashr8(s.c[X]);
             A = B = COV = L = H = Y;
+            if constexpr (NMS) {
+                A = pk_shl5(Y);
+                B = pk_add(A, 0x001F001Fu);
+            }
             EPS = 0;
         }
-        if (!(meta & COOP_M_ACT)) {   // pass-through slot: Y' = Y
-            A = B = COV = 0;
-            EPS = 0x00010001u;
+        if (!(meta & COOP_M_ACT)) {   // pass-through slot: Y' = Y (NMS: t = 32 Y + (0, 31))
+            A = COV = 0;
+            B = NMS ? 0x001F001Fu : 0u;
+            EPS = NMS ? 0x00200020u : 0x00010001u;
             L = VNEG127;
             H = V127;
         }
@@ -432,8 +465,10 @@ struct Slab3 {
             const uint32_t ax = abs_r(cx, K.c510);
             const uint32_t sacc = s.sacc ^ cx;
             const uint32_t min2 = pk_max(s.mn1, pk_min(ax, s.mn2)), min1 = pk_min(ax, s.mn1);
-            const uint32_t k1 = pk_max(pk_sub(pk_min(min2, K.rmm), K.coff), K.r0) & HIBYTES;
-            const uint32_t k2 = pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0) & HIBYTES;
+            const uint32_t k1 = NMS ? nms_c(pk_min(min2, K.rmm), fk)
+                                    : pk_max(pk_sub(pk_min(min2, K.rmm), K.coff), K.r0) & HIBYTES;
+            const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
+                                    : pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0) & HIBYTES;
             const uint32_t P = (sacc ^ ((D0 & 1) ? SIGNS : 0u)) & SIGNS;
             MA = 0;
             uint32_t nv[X + 1];
@@ -480,11 +515,27 @@ struct Slab3 {
                  : "+v"(XO), "=&v"(tmp)                                                       \
                  : "v"(XI), "v"((KV).x), "v"((KV).y), "v"((KV).z))
 
+// NMS: (t, t + 31) = eps f Y + (A, B); >> 5; median with c_o; clamp [L, H]
+#define C3_STEP_SAME_NMS(XW, KV)                                                               \
+    asm volatile("v_pk_mad_i16 %1, %0, %3, %2 op_sel:[0,0,0] op_sel_hi:[0,0,1]\n\t"           \
+                 "v_pk_ashrrev_i16 %1, 5, %1 op_sel_hi:[0,1]\n\t"                              \
+                 "v_med3_i16 %1, %1, %3, %1 op_sel:[0,1,1,0]\n\t"                             \
+                 "v_med3_i16 %0, %1, %4, %4 op_sel:[0,0,1,1]"                                 \
+                 : "+v"(XW), "=&v"(tmp)                                                       \
+                 : "v"((KV).x), "v"((KV).y), "v"((KV).z))
+#define C3_STEP_CROSS_NMS(XI, XO, KV)                                                          \
+    asm volatile("v_pk_mad_i16 %1, %2, %4, %3 op_sel:[1,0,0] op_sel_hi:[1,0,1]\n\t"           \
+                 "v_pk_ashrrev_i16 %1, 5, %1 op_sel_hi:[0,1]\n\t"                              \
+                 "v_med3_i16 %1, %1, %4, %1 op_sel:[0,1,1,0]\n\t"                             \
+                 "v_med3_i16 %0, %1, %5, %5 op_sel:[0,0,1,0]"                                 \
+                 : "+v"(XO), "=&v"(tmp)                                                       \
+                 : "v"(XI), "v"((KV).x), "v"((KV).y), "v"((KV).z))
+
 // the chain steps of one window (lanes 0..15 = codewords).  Step k's input
 // sits at position k % 8 of w (w[i] low / high half = positions 2i, 2i+1) and
 // its output goes to position k+1, so after step 8j+6 positions 0..7 hold the
 // inputs of steps 8j .. 8j+7: the x inputs post needs, stored as one uint4.
-template <int WS, int R, int B0, int B1>
+template <int WS, int R, int B0, int B1, bool NMS = false>
 LDPC_DEV void chain_window3(Smem3<WS, R> &sm, int buf, int c, uint32_t (&w)[4])
 {
     const uint4 *cp = &sm.cst[buf][0][c & 1][c >> 1];
@@ -499,15 +550,27 @@ LDPC_DEV void chain_window3(Smem3<WS, R> &sm, int buf, int c, uint32_t (&w)[4])
             for (int i = 0; i < 8; i++) kq[(b + 1) & 1][i] = cp[((b + 1) * 8 + i) * KST];
         }
         uint32_t tmp;
-        C3_STEP_SAME(w[0], kq[b & 1][0]);          // pos 0 -> 1
-        C3_STEP_CROSS(w[0], w[1], kq[b & 1][1]);   // pos 1 -> 2
-        C3_STEP_SAME(w[1], kq[b & 1][2]);          // 2 -> 3
-        C3_STEP_CROSS(w[1], w[2], kq[b & 1][3]);   // 3 -> 4
-        C3_STEP_SAME(w[2], kq[b & 1][4]);          // 4 -> 5
-        C3_STEP_CROSS(w[2], w[3], kq[b & 1][5]);   // 5 -> 6
-        C3_STEP_SAME(w[3], kq[b & 1][6]);          // 6 -> 7
-        sm.xo[buf][b][c] = make_uint4(w[0], w[1], w[2], w[3]);
-        C3_STEP_CROSS(w[3], w[0], kq[b & 1][7]);   // 7 -> 0 (the next block's first input)
+        if constexpr (NMS) {
+            C3_STEP_SAME_NMS(w[0], kq[b & 1][0]);
+            C3_STEP_CROSS_NMS(w[0], w[1], kq[b & 1][1]);
+            C3_STEP_SAME_NMS(w[1], kq[b & 1][2]);
+            C3_STEP_CROSS_NMS(w[1], w[2], kq[b & 1][3]);
+            C3_STEP_SAME_NMS(w[2], kq[b & 1][4]);
+            C3_STEP_CROSS_NMS(w[2], w[3], kq[b & 1][5]);
+            C3_STEP_SAME_NMS(w[3], kq[b & 1][6]);
+            sm.xo[buf][b][c] = make_uint4(w[0], w[1], w[2], w[3]);
+            C3_STEP_CROSS_NMS(w[3], w[0], kq[b & 1][7]);
+        } else {
+            C3_STEP_SAME(w[0], kq[b & 1][0]);          // pos 0 -> 1
+            C3_STEP_CROSS(w[0], w[1], kq[b & 1][1]);   // pos 1 -> 2
+            C3_STEP_SAME(w[1], kq[b & 1][2]);          // 2 -> 3
+            C3_STEP_CROSS(w[1], w[2], kq[b & 1][3]);   // 3 -> 4
+            C3_STEP_SAME(w[2], kq[b & 1][4]);          // 4 -> 5
+            C3_STEP_CROSS(w[2], w[3], kq[b & 1][5]);   // 5 -> 6
+            C3_STEP_SAME(w[3], kq[b & 1][6]);          // 6 -> 7
+            sm.xo[buf][b][c] = make_uint4(w[0], w[1], w[2], w[3]);
+            C3_STEP_CROSS(w[3], w[0], kq[b & 1][7]);   // 7 -> 0 (the next block's first input)
+        }
     }
 }
 
@@ -551,7 +614,7 @@ LDPC_DEV uint32_t high_bits16(uint4 x)   // byte high bits -> 16-bit codeword ma
 // live; the snapshots are merged back at the end.  Same result as the
 // reference's per-codeword stop (oracle: syndrome after every iteration), with
 // one launch instead of one per iteration plus syndrome / snapshot kernels.
-template <int WS, int R, bool STAMP, bool ET = false>
+template <int WS, int R, bool STAMP, bool ET = false, bool NMS = false>
 __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 {
     using SM = Smem3<WS, R>;
@@ -810,7 +873,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             for (int p = 0; p <= G; p++) {
                 if (STAMP) tx = stamp3();
 #ifndef C3X_NOCHAIN   // timing experiment only: results are wrong
-                if (p < G && cl) chain_window3<WS, R, 0, NB>(sm, p & 1, c, w4);
+                if (p < G && cl) chain_window3<WS, R, 0, NB, NMS>(sm, p & 1, c, w4);
 #endif
                 if (STAMP) sP[0] += stamp3() - tx;
                 stage(un, (p + KAHEAD) & (TQ - 1));
@@ -837,7 +900,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
     // parity rows k + j of this group at Pb + 16 j: row r at Pb - 16 k + 16 r
     char *Pr = (char *)a.P + ((size_t)wg * (size_t)(a.m + 1) - (size_t)a.k) * 16;
-    Slab3<WS, R> sl{sm,
+    Slab3<WS, R, NMS> sl{sm,
                     a,
                     q >= X ? Pr : (char *)Vb,
                     q >= X ? 16u : (uint32_t)a.pitch,
@@ -851,6 +914,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
                     opaque(0x050d040du),
                     PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
+                    opaque(a.nmsf),
                     // DMA lane 8e + slot: entry e < 6 a V row (record entry e, the
                     // o edge's D0-1 for e = X), e >= 6 message piece e - 6
                     kl < X ? Vb : kl == X ? Pr : Mb + (kl - 6) * 16,
@@ -1137,7 +1201,15 @@ static uint32_t fwd_code3(int dW, int slot, int e, int S)
     return ((uint32_t)(-dW) & 3u) << 13 | (uint32_t)(e * (S + 1) + slot) * 16u | (dW == 2 ? 2u : 0u) | 1u;
 }
 
-bool coop3_params_ok(const ldpc_params *p) { return coop_params_ok(p); }
+// OMS / MS as coop (coop_params_ok); NMS with factor <= 64 (msg_max <= 63: the
+// products fit the i16 halves) at the default WS = 6
+bool coop3_params_ok(const ldpc_params *p, const CoopCode &cc)
+{
+    if (p->algo == LDPC_ALGO_NMS)
+        return cc.S == 48 && p->var_min == -127 && p->var_max == 127 && p->msg_max >= 0 && p->msg_max <= 63 &&
+               p->factor >= 0 && p->factor <= 64;
+    return coop_params_ok(p);
+}
 
 // V and P are addressed with 64-bit flat addresses: no batch cap
 bool coop3_stride_ok(int stride) { return stride > 0 && stride % 64 == 0; }
@@ -1296,8 +1368,10 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.m0 = cc.m0;
     a.d1 = cc.d1;
     a.rmm = (uint32_t)(L.msg_max * 256 + 255) * 0x00010001u;
-    a.coff = (uint32_t)(L.param * 256) * 0x00010001u;
-    a.offp = (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
+    const bool nms = L.algo == LDPC_ALGO_NMS;
+    a.coff = nms ? 0u : (uint32_t)(L.param * 256) * 0x00010001u;
+    a.offp = nms ? 0u : (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
+    a.nmsf = nms ? (uint32_t)(L.param & 0xFFFF) * 0x00010001u : 0u;
     a.prio = env_int3("LDPC_COOP3_PRIO", 1);
     a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 0 none, 1 static (second waves), 2 fair by phase
     const int grid = L.stride / CW;
@@ -1312,7 +1386,15 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     int rc;
     if (et) {
         if (stamped) (void)hipFree(a.stamps);
-        hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+        if (L.algo == LDPC_ALGO_NMS)
+            hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+        else
+            hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    if (L.algo == LDPC_ALGO_NMS) {
+        if (ws != 6 || stamped) return -1;
+        hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (ws == 6)

@@ -171,3 +171,30 @@ def test_coop3_grouped_layout_vs_oracle(early, batch):
     assert np.array_equal(d_soft.cpu().numpy(), es)
     assert np.array_equal(d_hard.cpu().numpy(), eh)
     dec.close()
+
+
+@pytest.mark.parametrize("factor,early", [(29, False), (24, True), (32, False)])
+def test_coop3_nms_vs_oracle(factor, early):
+    """NMS (CDecoder_NMS_fixed_SSE.cpp:188-240: cst = (min * factor) >> 5) on
+    the fast DVB-S2 r1/2 kernel: coop3 runs it (no fallback reported) and its
+    soft output, hard decisions and iterations used equal the oracle's."""
+    from ldpcgputegra_amd import ALGO_NMS
+    torch = _torch()
+    t = load_table("dvbs2_r1_2")
+    B, iters = 200, 25
+    llr = channel.awgn_i8_host(t.n, B, seed=factor, table=channel.i8_table(channel.sigma_from_ebn0(1.1, 0.5)))
+    eh, es, eit = O.decode_i8(t, llr, iters, O.NMS, factor, early_term=early, return_soft=True,
+                              threads=O.host_threads())
+    dec = Decoder(Code("dvbs2_r1_2"), max_batch=B)
+    d_hard = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+    d_soft = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
+    d_its = torch.empty(B, dtype=torch.int32, device="cuda")
+    dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters,
+                         params=default_params(algo=ALGO_NMS, factor=factor, early_term=int(early)),
+                         soft=d_soft, iters_used=d_its)
+    torch.cuda.synchronize()
+    assert dec.last_kernel == "coop3" and dec.last_skipped is None
+    assert np.array_equal(d_its.cpu().numpy(), eit)
+    assert np.array_equal(d_soft.cpu().numpy(), es)
+    assert np.array_equal(d_hard.cpu().numpy(), eh)
+    dec.close()
