@@ -30,7 +30,7 @@ for s in ${STEPS//,/ }; do
     bench) step bench 300 python3 bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
     benchg) LDPC_COOP3_GROUPED=1 step bench_grouped 300 python3 bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
     mixed) step bench_mixed 300 python3 bench.py --mixed ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
-    tests) step tests 900 python3 -u -m pytest ${TESTS:-tests} -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS} ;;
+    tests) step tests 900 python3 -u -m pytest ${TESTS:-tests} -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "${TESTK:-not nothing}" ;;
     prof) PROF_OUT=$OUT/prof bash tools/profile.sh || exit $? ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     esac

@@ -60,8 +60,9 @@ __device__ __forceinline__ char *row_addr(const Args &a, int wg, int r, int lane
     if (r >= a.k) return a.P + ((size_t)wg * (a.m + 1) + (r - a.k)) * 16;
     if (a.mode == 0) return a.V + (size_t)r * a.pitch + (size_t)wg * CW;
     if (a.mode == 1) return a.V + ((size_t)wg * a.k + r) * 16;
-    // mode 2: 8 lanes of a slot = one 128-B line (line index from the slot's first row)
-    const size_t line = (size_t)(r >> 3);
+    // mode 2: 8 lanes of a slot = one 128-B line (line index from the slot's first row);
+    // mode 3: the same confined to 512 lines (64 KB) per workgroup (L2-resident)
+    const size_t line = a.mode == 3 ? (size_t)((r >> 3) & 511) : (size_t)(r >> 3);
     return a.V + ((size_t)wg * a.k + line * 8) * 16 + (size_t)(lane & 7) * 16;
 }
 
@@ -212,13 +213,17 @@ int main(int argc, char **argv)
         {"lines", vmem_k<2, false, false, 0>, 2},
         {"lines filler296", vmem_k<2, false, false, 296>, 2},
         {"filler296 only (nostore)", vmem_k<2, true, false, 296>, 2},
+        {"lines64K", vmem_k<3, false, false, 0>, 3},
+        {"lines64K nostore", vmem_k<3, true, false, 0>, 3},
+        {"lines64K filler296", vmem_k<3, false, false, 296>, 3},
+        {"lines64K filler592", vmem_k<3, false, false, 592>, 3},
     };
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     std::vector<unsigned long long> out((size_t)grid * (WS + 1));
     for (const Cfg &c : cfgs) {
-        a.rows = c.mode == 2 ? d_rows2 : d_rows;
+        a.rows = c.mode >= 2 ? d_rows2 : d_rows;
         hipLaunchKernelGGL(c.k, dim3(grid), dim3(64 * (WS + 1)), 0, 0, a);   // warm-up
         hipEventRecord(e0, 0);
         const int reps = 3;
