@@ -27,6 +27,7 @@ for s in ${STEPS//,/ }; do
     case $s in
     valu) step ubench_valu 60 ./tools/ubench_valu ;;
     vmem) step ubench_vmem 120 ./tools/ubench_vmem ldpcgputegra_amd/codes/dvbs2_r1_2.txt ;;
+    lc) step ubench_lc 120 ./tools/ubench_lc ;;
     bench) step bench 300 python3 bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
     benchg) LDPC_COOP3_GROUPED=1 step bench_grouped 300 python3 bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
     mixed) step bench_mixed 300 python3 bench.py --mixed ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
