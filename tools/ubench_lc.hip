@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <type_traits>
 #include <vector>
 
 constexpr int WS = 6, NP = 720, CW = 16;
@@ -65,12 +66,17 @@ __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
     char *Vw = a.V + (size_t)wg * LINES * 128;
     char *Mw = a.Mc + (size_t)wg * (M + 1) * 64;
     uint32_t x0 = lane, x1 = lane * 3u, x2 = lane * 5u, x3 = lane * 7u, acc = 0;
-    uint4 ld[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    uint4 ld[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};   // staged line loads (static indices only)
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     if (wave < WS) {
         const uint32_t mbase = (uint32_t)(uintptr_t)&min_[wave][0][0];
-        for (int p = 0; p < NP; p++) {
+        // one period; S = p % 2 is static (periods unrolled by two) so that the
+        // staged line loads stay in named VGPRs the compiler keeps live and
+        // waits for (compiler-visible loads: its vmcnt counts only its own
+        // operations, which errs on the safe side)
+        auto period = [&](auto sc, int p) __attribute__((always_inline)) {
+            constexpr int S = decltype(sc)::value;
             const uint32_t key = (uint32_t)(p * WS + wave) * 8u + (uint32_t)l;
             // line stores: 8 lines written back (slots of lines whose last post was period p-1)
             if (STORES) {
@@ -82,14 +88,13 @@ __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
             // message store of the wave's 8 checks (window p-2)
             const int chk = (p * 48 + wave * 8 + l) % M;
             if (q < 4) *(uint4 *)(Mw + (size_t)chk * 64 + q * 16) = make_uint4(x0, x1, x2, x3);
+            // the message gathers of window p (issued 3 periods ago) have landed:
+            // per period [line store], message store, line load, 2 message DMA
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STORES ? 12 : 9) : "memory");
             // line loads issued two periods ago land in the cache now
-            // per period: [line store], message store, line load, 2 message DMA;
-            // the load of period p-2 is older than this period's stores and
-            // all of period p-1's operations
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STORES ? 7 : 5) : "memory");
             {
                 const int slot = (int)(hash32(key ^ 0xc2b2ae35u) % CACHE);
-                cache[slot * 8 + q] = ld[p & 1];
+                cache[slot * 8 + q] = ld[S];
             }
             // the window's scattered cache reads / writes (pre + post)
             // (cheap address arithmetic, as the kernel's record offsets are: 2 VALU per access)
@@ -100,7 +105,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
                 const uint32_t off = ((hb + (uint32_t)i * 977u) & 4095u) * 16u + 4u * (uint32_t)(q >> 1);
                 r += *(const uint32_t *)((const char *)cache + off);
             }
-            acc += r;
+            acc += r + min_[wave][p & 3][lane].x;
 #pragma unroll
             for (int i = 0; i < FILLER; i += 4)
                 asm volatile("v_pk_add_u16 %0, %0, %4\n\tv_pk_add_u16 %1, %1, %4\n\tv_pk_add_u16 %2, %2, %4\n\tv_pk_add_u16 %3, %3, %4"
@@ -116,16 +121,17 @@ __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
             // line loads for period p+2
             {
                 const int line = (int)(hash32(key ^ 0x27d4eb2fu) % LINES);
-                // (asm: the compiler must not wait for it; the vmcnt above does)
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ld[p & 1]) : "v"(Vw + (size_t)line * 128 + q * 16)
-                             : "memory");
+                ld[S] = *(const uint4 *)(Vw + (size_t)line * 128 + q * 16);
             }
             // message gathers of window p+3
             const int chn = ((p + 3) * 48 + wave * 8 + l) % M;
             dma16(Mw + (size_t)chn * 64 + (q & 3) * 16, mbase + (uint32_t)(((p + 3) & 3) * 64 * 16));
             if (lane < 16) dma16(Mw + (size_t)chn * 64 + 32 + (q & 1) * 16, mbase + (uint32_t)(((p + 3) & 3) * 64 * 16));
-            acc += min_[wave][p & 3][lane].x;
             __syncthreads();
+        };
+        for (int p = 0; p < NP; p += 2) {
+            period(std::integral_constant<int, 0>{}, p);
+            period(std::integral_constant<int, 1>{}, p + 1);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
