@@ -55,7 +55,11 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x)
     return x ^ (x >> 16);
 }
 
-template <int FILLER, int NLDS, bool STORES>
+// FILLER packed VALU + FILLER / 4 cheap bitwise VALU; NLINE lines loaded and
+// written back per wave and period (8: 48 per CU, 5: 30 = the plan's mean);
+// SEQ: lines swept in order (each loaded once per ~400 periods: HBM), else
+// pseudo-random
+template <int FILLER, int NLDS, bool STORES, int NLINE = 8, bool SEQ = false>
 __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
 {
     __shared__ uint4 cache[CACHE * 8];
@@ -79,10 +83,11 @@ __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
             constexpr int S = decltype(sc)::value;
             const uint32_t key = (uint32_t)(p * WS + wave) * 8u + (uint32_t)l;
             // line stores: 8 lines written back (slots of lines whose last post was period p-1)
-            if (STORES) {
+            if (STORES && l < NLINE) {
                 const int slot = (int)(hash32(key ^ 0x9e3779b9u) % CACHE);
                 const uint4 d = cache[slot * 8 + q];
-                const int line = (int)(hash32(key ^ 0x85ebca6bu) % LINES);
+                const int line = SEQ ? (int)(((uint32_t)p * (WS * NLINE) + (uint32_t)(wave * NLINE + l) + 7000u) % LINES)
+                                     : (int)(hash32(key ^ 0x85ebca6bu) % LINES);
                 *(uint4 *)(Vw + (size_t)line * 128 + q * 16) = d;
             }
             // message store of the wave's 8 checks (window p-2)
@@ -90,9 +95,10 @@ __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
             if (q < 4) *(uint4 *)(Mw + (size_t)chk * 64 + q * 16) = make_uint4(x0, x1, x2, x3);
             // the message gathers of window p (issued 3 periods ago) have landed:
             // per period [line store], message store, line load, 2 message DMA
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STORES ? 12 : 9) : "memory");
+            // (a wave with NLINE = 0 issues no line load or store)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLINE == 0 ? 7 : STORES ? 12 : 9) : "memory");
             // line loads issued two periods ago land in the cache now
-            {
+            if (l < NLINE) {
                 const int slot = (int)(hash32(key ^ 0xc2b2ae35u) % CACHE);
                 cache[slot * 8 + q] = ld[S];
             }
@@ -111,6 +117,11 @@ __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
                 asm volatile("v_pk_add_u16 %0, %0, %4\n\tv_pk_add_u16 %1, %1, %4\n\tv_pk_add_u16 %2, %2, %4\n\tv_pk_add_u16 %3, %3, %4"
                              : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
                              : "v"(acc));
+#pragma unroll
+            for (int i = 0; i < FILLER / 4; i += 4)
+                asm volatile("v_xor_b32 %0, %0, %4\n\tv_xor_b32 %1, %1, %4\n\tv_and_b32 %2, %2, %4\n\tv_or_b32 %3, %3, %4"
+                             : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
+                             : "v"(acc));
             if (NLDS) {
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
@@ -119,8 +130,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) lc_k(Args a)
                 }
             }
             // line loads for period p+2
-            {
-                const int line = (int)(hash32(key ^ 0x27d4eb2fu) % LINES);
+            if (l < NLINE) {
+                const int line = SEQ ? (int)(((uint32_t)p * (WS * NLINE) + (uint32_t)(wave * NLINE + l)) % LINES)
+                                     : (int)(hash32(key ^ 0x27d4eb2fu) % LINES);
                 ld[S] = *(const uint4 *)(Vw + (size_t)line * 128 + q * 16);
             }
             // message gathers of window p+3
@@ -157,13 +169,13 @@ int main()
         const char *name;
         void (*k)(Args);
     } cfgs[] = {
-        {"lc mem only", lc_k<0, 0, true>},
-        {"lc mem, no line stores", lc_k<0, 0, false>},
-        {"lc mem + 32 LDS", lc_k<0, 32, true>},
-        {"lc mem + 260 pk VALU", lc_k<260, 0, true>},
-        {"lc mem + 32 LDS + 260 pk VALU", lc_k<260, 32, true>},
-        {"lc mem + 32 LDS + 220 pk VALU", lc_k<220, 32, true>},
-        {"lc 32 LDS + 260 pk VALU, no line stores", lc_k<260, 32, false>},
+        {"lc mem only (48+48 lines, random)", lc_k<0, 0, true>},
+        {"lc mem only (30+30 lines, seq)", lc_k<0, 0, true, 5, true>},
+        {"lc 30 seq + 32 LDS", lc_k<0, 32, true, 5, true>},
+        {"lc 30 seq + 200 pk + 50 bit VALU", lc_k<200, 0, true, 5, true>},
+        {"lc 30 seq + 32 LDS + 200/50 VALU", lc_k<200, 32, true, 5, true>},
+        {"lc 30 seq + 32 LDS + 160/40 VALU", lc_k<160, 32, true, 5, true>},
+        {"no memory: 32 LDS + 200/50 VALU", lc_k<200, 32, false, 0, true>},
     };
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
