@@ -62,12 +62,6 @@
 __device__ void sbuf_store_v4(i32x4 v, i32x4 rsrc, int index, int offset, int soffset, int aux)
     __asm("llvm.amdgcn.struct.buffer.store.v4i32");
 
-#ifdef C3_MARKERS   // instruction census of the fast period (asm comments; scheduling boundaries)
-#define C3_MARK(s) asm volatile(";C3MARK " s)
-#else
-#define C3_MARK(s)
-#endif
-
 namespace {
 
 constexpr int D0 = 7, X = D0 - 2;   // first-group check degree, information edges per check
@@ -257,40 +251,14 @@ struct Slab3 {
     // message piece c (c < 4) of its wave's slot kl
     LDPC_DEV void stores(const StIn &in, bool tl) const
     {
-#ifndef C3X_NOVSTORE   // timing experiment only: results are wrong
-#if defined(C3X_VSTORE_NT)   // experiment: V row pieces as non-temporal (streaming) stores
-        if (q < (tl ? D0 : D0 - 1))
-            __builtin_nontemporal_store(__builtin_bit_cast(i32x4, in.vd), (i32x4 *)(vsb + (size_t)in.row * vsm));
-#elif defined(C3X_VSTORE2)   // timing experiment: V row pieces as two 8-B stores
-        if (q < (tl ? D0 : D0 - 1)) {
-            uint2 *d = (uint2 *)(vsb + (size_t)in.row * vsm);
-            d[0] = make_uint2(in.vd.x, in.vd.y);
-            d[1] = make_uint2(in.vd.z, in.vd.w);
-        }
-#else
         if (q < (tl ? D0 : D0 - 1)) *(uint4 *)(vsb + (size_t)in.row * vsm) = in.vd;
-#endif
-#endif
         if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
     }
     LDPC_DEV void gathers(const PfIn &in, int ib) const
     {
         static_assert(offsetof(typename SM::In, b) == SM::IN_B, "In layout");
         const uint32_t base = (uint32_t)(uintptr_t)&sm.in[w][ib];
-#ifdef C3X_NOVLOAD   // timing experiment only: results are wrong
-        if (lane >= 8 * X)
-#endif
-#ifdef C3X_DMA_NT   // experiment: V row gathers with the non-temporal policy
-        {
-            unsigned keep;
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                         : "=&s"(keep)
-                         : "v"(g1base + (size_t)in.rv * g1mul), "s"(base)
-                         : "memory");
-        }
-#else
         dma16(g1base + (size_t)in.rv * g1mul, base);
-#endif
         if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + SM::IN_B);
     }
 
@@ -313,11 +281,7 @@ struct Slab3 {
     template <bool TL, bool FZ_ = false, int MP = -1>
     LDPC_DEV void pre(int g, const PreIn &in, St3 &s) const
     {
-#ifdef C3X_NOFZ   // timing experiment only: no freezing of converged codewords (results are wrong)
-        constexpr bool FZ = false;
-#else
         constexpr bool FZ = FZ_;
-#endif
         const uint32_t meta = in.mf.x;
         uint32_t v[D0 - 1];
         // V pair of edge j: this pair's two bytes of the loaded V dword, or the
@@ -452,11 +416,7 @@ struct Slab3 {
     template <bool TL, bool FZ_ = false, int MP = -1>
     LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
     {
-#ifdef C3X_NOFZ
-        constexpr bool FZ = false;
-#else
         constexpr bool FZ = FZ_;
-#endif
         unsigned short *st = (unsigned short *)&sm.stg[g % NR][k];      // [entry][..S slots..][8 pairs] u16
         constexpr int ES = (S + 1) * 8;                                 // u16 between entries
         uint32_t MA, MB;
@@ -719,24 +679,10 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         __syncthreads();
         return (fail & live) == live;
     };
-#ifdef C3X_ET_PROF   // diagnostic: cycles of et_after and its full syndromes (printf by workgroup 0)
-    unsigned long long ep_tot = 0, ep_stage = 0, ep_chk = 0, ep_t0 = 0, ep_t1 = 0, ep_seg0 = 0, ep_seg = 0;
-    int ep_full = 0, ep_n = 0;
-    ep_seg0 = __builtin_amdgcn_s_memtime();
-#define C3_EP(x) x
-#else
-#define C3_EP(x)
-#endif
     auto et_after = [&](int it) -> bool {
-        C3_EP(ep_t0 = __builtin_amdgcn_s_memtime(); ep_seg += ep_t0 - ep_seg0; ep_n++;)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the iteration's stores and table DMAs
         __syncthreads();
         const uint32_t live = et_sh[0];
-#ifdef C3X_ET_NOSCAN   // timing experiment only (no codeword ever converges): segments without the syndrome
-        if (threadIdx.x == 0) et_sh[1] = live;
-        __syncthreads();
-        if (false) {
-#else
         // round 0: one check per thread, gathered directly -- threads 0..63
         // the codewords' hint checks, the others checks spread over the code
         // (a codeword still decoding fails many checks: this usually settles
@@ -749,14 +695,12 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if (et_round(x, live)) goto et_done;
         }
         {
-#endif
             // the full syndrome: every variable's hard bits staged in LDS (the
             // pipeline's LDS is idle between segments; the launch checks n
             // fits), then the checks, 8 per thread and round with an exit
             // test after each; loads unconditional (clamped check index) so a
             // round's index loads are in flight together
             uint16_t *hb = reinterpret_cast<uint16_t *>(&sm);
-            C3_EP(ep_t1 = __builtin_amdgcn_s_memtime(); ep_full++;)
             // (16 unconditional loads in flight per thread: clamped rows)
             auto hbits = [](uint4 y) {
                 return (uint16_t)high_bits16(make_uint4(pos_bits(y.x), pos_bits(y.y), pos_bits(y.z), pos_bits(y.w)));
@@ -780,7 +724,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     if (r0 + i * NT + (int)threadIdx.x < a.m) hb[a.k + r0 + i * NT + threadIdx.x] = hbits(y[i]);
             }
             __syncthreads();
-            C3_EP({ const unsigned long long t = __builtin_amdgcn_s_memtime(); ep_stage += t - ep_t1; ep_t1 = t; })
             bool done = false;
             for (int c0 = 0; c0 < a.m0 && !done; c0 += NT * 8) {
                 uint32_t ev[8][D0];
@@ -815,11 +758,8 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 }
                 et_round(f, live);
             }
-            C3_EP(ep_chk += __builtin_amdgcn_s_memtime() - ep_t1;)
         }
-#ifndef C3X_ET_NOSCAN
     et_done:
-#endif
         const uint32_t fresh = live & ~et_sh[1];   // converged after this iteration
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -828,7 +768,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         }
         if (fresh && threadIdx.x < CW && ((fresh >> threadIdx.x) & 1u)) a.iters_used[wg * CW + threadIdx.x] = it + 1;
         __syncthreads();
-        C3_EP(ep_seg0 = __builtin_amdgcn_s_memtime(); ep_tot += ep_seg0 - ep_t0;)
         return (live & ~fresh) != 0 && it + 1 < a.iters;
     };
     // stamps (diagnostic build): per wave 8 words: busy, phases 1..3 (slab:
@@ -872,9 +811,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if (STAMP) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
                 if (STAMP) tx = stamp3();
-#ifndef C3X_NOCHAIN   // timing experiment only: results are wrong
                 if (p < G && cl) chain_window3<WS, R, 0, NB, NMS>(sm, p & 1, c, w4);
-#endif
                 if (STAMP) sP[0] += stamp3() - tx;
                 stage(un, (p + KAHEAD) & (TQ - 1));
                 un = (un + 1 == a.nw) ? 0 : un + 1;
@@ -980,11 +917,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         // period p-R, followed by 4 in each later period: in the main loop (every
         // period does everything, no tail window) vmcnt(4(R-1)) covers them.
         constexpr int MP1 = -1, MP2 = -1;   // mid-phase priorities (none: quarter-period levels measured the same)
-#ifdef C3X_PREFIRST   // r02k order: slab waves 1-5 run pre first, wait for their gathers at the period start
-        constexpr bool POSTFIRST = false;
-#else
-        constexpr bool POSTFIRST = true;
-#endif
         const bool fair = a.slab_prio == 2;
         auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
@@ -996,7 +928,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             PfIn pi;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
-            if (fast && POSTFIRST) {
+            if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs, nothing from memory) and waits for its window
                 // p+1 gathers only before its pre, half a period later than at
@@ -1006,74 +938,17 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 sl.stores(sc, false);
                 const uint32_t xr = sl.read_x(p - 1, sp);
                 sl.read_pf(p + 1 + R, pi);
-#ifdef C3X_GATHER_TOP   // experiment: the gathers of window p+1+R right after the stores
-                sl.gathers(pi, (s + R + 1) % NI);
-                constexpr int VMW = 4 * (R - 1) + 4;
-#else
                 constexpr int VMW = 4 * (R - 1) + 2;
-#endif
-#ifdef C3X_FWD_TOP   // experiment: waves 1-5 read their forwarded values (windows <= p-2) before the post
-                if (sw != 0) {
-                    in.mf = mfc;
-                    sl.fwd_read(p + 1, in);
-                }
-#endif
                 sl.template post<false, ET, MP1>(p - 1, xr, sp);
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMW) : "memory");
                 sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
-#ifdef C3X_FWD_TOP
-                if (sw == 0) sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values
-#else
                 sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values (wave 0)
-#endif
-#ifndef C3X_GATHER_TOP
                 sl.gathers(pi, (s + R + 1) % NI);
-#endif
                 sl.read_st(p - 1, sc);
                 if (STAMP) t1 = t2 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(0);
                 sl.template pre<false, ET, MP2>(p + 1, in, sn);
                 if (STAMP) t3 = stampL();
-            } else if (fast) {
-                // every read of the period that does not depend on this period's
-                // own writes goes first (one exposed LDS latency): the gathers of
-                // window p+1 have landed (the vmcnt count of the main loop),
-                // chain inputs of window p-1, records of window p+1+R
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R - 1)) : "memory");
-                if (STAMP) t1 = stampL();
-                // fair issue between the two slab waves of a SIMD: each runs the
-                // first phase of its period at priority 1 and the second at 0, so
-                // a wave that lags behind its partner (the arbiter otherwise
-                // favours the older wave) catches up and neither finishes the
-                // period alone on the SIMD (49.7 -> 47.8 ms)
-                if (fair) __builtin_amdgcn_s_setprio(1);
-                sl.stores(sc, false);
-                const uint32_t xr = sl.read_x(p - 1, sp);
-                sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
-                sl.read_pf(p + 1 + R, pi);
-                if (sw == 0) {
-                    C3_MARK("post0");
-                    sl.template post<false, ET, MP1>(p - 1, xr, sp);
-                    sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values
-                    sl.gathers(pi, (s + R + 1) % NI);
-                    sl.read_st(p - 1, sc);
-                    if (STAMP) t2 = stampL();
-                    if (fair) __builtin_amdgcn_s_setprio(0);
-                    C3_MARK("pre0");
-                    sl.template pre<false, ET, MP2>(p + 1, in, sn);
-                } else {
-                    sl.fwd_read(p + 1, in);   // windows <= p-2, staged before the barrier
-                    C3_MARK("pre");
-                    sl.template pre<false, ET, MP1>(p + 1, in, sn);
-                    sl.gathers(pi, (s + R + 1) % NI);
-                    if (STAMP) t2 = stampL();
-                    if (fair) __builtin_amdgcn_s_setprio(0);
-                    C3_MARK("post");
-                    sl.template post<false, ET, MP2>(p - 1, xr, sp);
-                    sl.read_st(p - 1, sc);
-                }
-                if (STAMP) t3 = stampL();
-                C3_MARK("end");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (dst) sl.stores(sc, sc_tl);
@@ -1134,7 +1009,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         sl.stores(sc, sc_tl);   // window G-1
         if (!ET || !et_after(it)) break;
     }
-    C3_EP(if (threadIdx.x == 0 && id == 0) printf("ET prof wg0: segments %d  full %d  cycles: segments %llu  et_after %llu  staging %llu  checks %llu\n", ep_n, ep_full, ep_seg, ep_tot, ep_stage, ep_chk);)
     write_stamps();
     parity_out();
 }
@@ -1216,21 +1090,23 @@ bool coop3_stride_ok(int stride) { return stride > 0 && stride % 64 == 0; }
 
 size_t coop3_msg_bytes(const ldpc_code *h, int stride) { return (size_t)(h->m + 1) * (size_t)stride * 4; }
 
-int coop3_upload(const ldpc_code *h, CoopCode *cc)
+// host side of coop3's schedule: the window plan with every window's slots
+// permuted (distance-2 forwarding sources and readers in slab wave 0) and the
+// records rewritten (forwarding codes, chain steps).  1 = no coop3 schedule
+// for this code, 0 = ok, < 0 = error (status set)
+int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
 {
-    *cc = CoopCode{};
-    if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return LDPC_OK;
-    const int ws = env_int3("LDPC_COOP3_WS", 6);
-    const int r = env_int3("LDPC_COOP3_R", 2);
+    o = Coop3Host{};
+    if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return 1;
     if ((ws != 3 && ws != 4 && ws != 6) || r != 2)
         return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 3 | 4 | 6 and LDPC_COOP3_R 2");
     const int S = 8 * ws;
-    CoopPlan pl;
+    CoopPlan &pl = o.pl;
     // dist 1 (distance-2 sources and readers share slab wave 0); a value is
     // stored at the start of the second period after its window's chain, so
     // reads 2 .. r+3 windows later are forwarded from the LDS stage (plan
     // prefetch depth r + 2)
-    if (coop_build_plan(h, S, r + 2, 1, RECW, pl, true) != 0) return LDPC_OK;
+    if (coop_build_plan(h, S, r + 2, 1, RECW, pl, true) != 0) return 1;
     const int nw = (int)pl.first.size();
     auto rec_at = [&](int u, int k) { return &pl.tab[((size_t)u * S + k) * RECW]; };
     auto code_at = [&](const uint32_t *rec, int j) { return (rec[D0 + 1 + j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
@@ -1252,7 +1128,7 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
             for (int k = 0; k < S; k++) {
                 const bool act = k < pl.count[u], sp = special[(size_t)u * S + k] != 0;
                 if ((pass == 0 && sp) || (pass == 1 && act && !sp) || (pass == 2 && !act)) {
-                    if (pass == 0 && n >= 8) return LDPC_OK;   // more than wave 0 holds: no coop3 schedule
+                    if (pass == 0 && n >= 8) return 1;   // more than wave 0 holds: no coop3 schedule
                     slot_of[(size_t)u * S + k] = n;
                     check_at[(size_t)u * S + n] = k;
                     n++;
@@ -1286,6 +1162,22 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
             rec[D0] |= (uint32_t)k << STEP_SHIFT;
         }
     pl.tab.swap(tab);
+    o.S = S;
+    o.nw = nw;
+    o.recw = RECW;
+    o.d0 = D0;
+    return 0;
+}
+
+int coop3_upload(const ldpc_code *h, CoopCode *cc)
+{
+    *cc = CoopCode{};
+    Coop3Host ho;
+    const int ws = env_int3("LDPC_COOP3_WS", 6), r = env_int3("LDPC_COOP3_R", 2);
+    const int rc = coop3_plan_host(h, ws, r, ho);
+    if (rc != 0) return rc > 0 ? LDPC_OK : rc;
+    CoopPlan &pl = ho.pl;
+    const int S = ho.S, nw = ho.nw;
     if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop3 tables");
     if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         coop_free(cc);
