@@ -383,11 +383,15 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     // coop3 with LDPC_COOP3_GROUPED=1: V in the grouped layout [stride / 16][N + 1][16]
     // (a workgroup's rows contiguous) -- not with the per-iteration
     // early-termination helpers, which address V[row][pitch]
-    const bool vpriv = kern == 8 && !is_float && getenv_int("LDPC_COOP3_GROUPED", 0) != 0 &&
+    // (the line cache, when coop3 has one, needs it)
+    const bool vpriv = kern == 8 && !is_float &&
+                       (c->coop3.lc_valid || getenv_int("LDPC_COOP3_GROUPED", 0) != 0) &&
                        (!p->early_term || coop3_et_in_kernel(c->coop3, h->n));
     const int vpad = (kern == 8 || kern == 5) && !vpriv ? std::max(0, getenv_int("LDPC_VPITCH_PAD", 64)) / 64 * 64 : 0;
     const int vpitch = stride + vpad;
-    if ((rc = ensure(&sc.d_V, &sc.V_bytes, (size_t)(h->n + 1) * vpitch * esz)) != LDPC_OK) return rc;
+    // grouped layout: [stride / 16][n + 8][16] (the sink row n and the rest of its 128-B line)
+    const size_t v_rows = vpriv ? (size_t)h->n + 8 : (size_t)h->n + 1;
+    if ((rc = ensure(&sc.d_V, &sc.V_bytes, v_rows * vpitch * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_need)) != LDPC_OK) return rc;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.

@@ -13,6 +13,10 @@ struct CoopCode {
     int x0;          // coop3: V row of check 0's x edge (the chain's first input)
     int m0, d1;      // coop3: checks of degree d0 (group 0), degree of the later group
     uint32_t *d_tab; // [nw][S][recw]
+    // coop3's LDS line cache (linecache.cpp): window tables [nw] (LcWin), the
+    // lines resident at a segment start / dirty at its end; lc_valid = 0: none
+    int lc_valid, lc_slots, n_pro, n_epi;
+    uint32_t *d_lctab, *d_lcpro, *d_lcepi;
 };
 
 bool coop_params_ok(const ldpc_params *p);

@@ -114,6 +114,31 @@ struct alignas(16) Smem3 {
                                       // workgroup per CU either way)
 };
 
+// ---- the LDS line cache (the V rows of a workgroup's codewords in whole
+// 128-B lines: linecache.cpp plans which line sits in which slot when)
+constexpr int LC_SLOTS = 760;         // cache lines (8 rows x 16 codewords each) beside the pipeline
+struct alignas(16) LcWin {            // one window's table (global [nw] array, LDS-DMA'd by the chain wave)
+    uint4 rec[48];                    // slot k: cache rows (slot * 8 + var % 8) of record entries 0..6 (u16),
+                                      // then meta16 = chain step | active << 6
+    uint16_t chk[48];                 // slot k: its check (message row; the sink row m when inactive)
+    uint32_t loads[LC_LMAX];          // lines whose load is issued in this period (line | slot << 16), entry
+    uint32_t wbs[LC_LMAX];            // li * 6 + w for lane group li of slab wave w; lines written back now
+};
+static_assert(sizeof(LcWin) % 16 == 0, "LcWin is staged in 16-B pieces");
+
+template <int WS, int R>
+struct alignas(16) Smem3LC {
+    using CF = Cfg<WS, R>;
+    static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
+    static constexpr uint32_t IN_B = 0;   // (the forwarding-ring layout's field, unused here)
+    uint4 cache[LC_SLOTS][8];         // the line cache (slot 0: the sink line of the inactive slots)
+    LcWin tab[TQ];                    // window tables, window g in slot g % TQ
+    uint4 cst[2][S][2][NP];           // chain constants (as Smem3)
+    uint4 xo[2][S / 8][CW];           // chain inputs (as Smem3)
+    uint4 inm[WS][NI][8][4];          // one window's old message records per slab wave ([slot] x 64 B)
+    uint4 mst[WS][8][4];              // new messages (as Smem3)
+};
+
 struct Coop3Args {
     int8_t *V;                        // V[n + 1][pitch]; row n is the sink of inactive slots
     uint8_t *Mc;                      // [pitch / 16][mrows][8 pairs][2] u32; row m is the sink
@@ -131,6 +156,8 @@ struct Coop3Args {
     int pitch, G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
     uint32_t nmsf;                    // NMS factor per half (value form)
     size_t wgoff;                     // bytes between two codeword groups' V (see DecodeLaunch::vpriv)
+    const uint32_t *lcpro, *lcepi;    // line cache: lines resident before period -1 / dirty after the last
+    int npro, nepi;
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
 };
 
@@ -176,9 +203,9 @@ struct PfIn {                         // the LDS-DMA gathers of window p+1+R
     uint32_t rv, chk2;
 };
 
-template <int WS, int R, bool NMS = false>
+template <int WS, int R, bool NMS = false, bool LC = false>
 struct Slab3 {
-    using SM = Smem3<WS, R>;
+    using SM = std::conditional_t<LC, Smem3LC<WS, R>, Smem3<WS, R>>;
     static constexpr int S = SM::S, NR = SM::NR;
     SM &sm;
     const Coop3Args &a;
@@ -197,6 +224,72 @@ struct Slab3 {
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
+    const char *lcV = nullptr;        // LC: this group's V rows (grouped layout), lines of 128 B
+
+    // ---- line cache (LC)
+    LDPC_DEV uint4 rec(int g) const { return sm.tab[g & (TQ - 1)].rec[k]; }
+    LDPC_DEV static uint32_t row_of(const uint4 &r, int j)   // cache row of record entry j
+    {
+        const uint32_t x = j < 2 ? r.x : j < 4 ? r.y : j < 6 ? r.z : r.w;
+        return (j & 1) ? x >> 16 : x & 0xFFFFu;
+    }
+    LDPC_DEV const char *cache_b() const { return (const char *)&sm.cache[0][0]; }
+    // window g's V dwords (this pair's 2 bytes in each) and old messages; the
+    // meta word in coop3's form (active, chain step), no forwarding codes
+    LDPC_DEV void read_pre_lc(int g, int ib, PreIn &in) const
+    {
+        const uint4 rr = rec(g);
+        const char *cb = cache_b() + 4 * (q >> 1);
+#pragma unroll
+        for (int j = 0; j < X; j++) in.v[j] = *(const uint32_t *)(cb + row_of(rr, j) * 16);
+        in.v[X] = *(const uint32_t *)(cb + row_of(rr, D0 - 1) * 16);
+        const uint2 mm = *(const uint2 *)((const char *)&sm.inm[w][ib][kl][0] + 8 * q);
+        in.ma = mm.x;
+        in.mb = mm.y;
+        const uint32_t m16 = rr.w >> 16;
+        in.mf = make_uint4(((m16 & 64u) ? COOP_M_ACT : 0u) | (m16 & 63u) << STEP_SHIFT, 0u, 0u, 0u);
+    }
+    // old messages of window g: lanes 0..31 = (slot, 16-B piece) of the wave's 8 checks
+    LDPC_DEV void gathers_lc(int g, int ib) const
+    {
+        if (lane < 32) {
+            const uint32_t c = sm.tab[g & (TQ - 1)].chk[8 * w + (lane >> 2)];
+            dma16(g2base + (size_t)c * MREC + (lane & 3) * 16, (uint32_t)(uintptr_t)&sm.inm[w][ib][0][0]);
+        }
+    }
+    LDPC_DEV void read_st_lc(int g, StIn &in) const
+    {
+        in.md = sm.mst[w][kl][q & 3];
+        in.chk = sm.tab[g & (TQ - 1)].chk[k];
+    }
+    LDPC_DEV void stores_lc(const StIn &in) const
+    {
+        if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
+    }
+    // line lists: lane group li = lane >> 3 of slab wave w handles entry li * WS + w
+    // (16-B piece q of the line); the host fills entries 0..WS-1 of every list
+    // (sink line where a period has fewer), so every wave issues each line
+    // operation every period and the vmcnt counts stay exact
+    LDPC_DEV uint32_t lc_code(const uint32_t *list) const { return list[(lane >> 3) * WS + w]; }
+    LDPC_DEV void lc_wb_read(int p, uint32_t &code, uint4 &d) const
+    {
+        code = lc_code(sm.tab[p & (TQ - 1)].wbs);
+        if (code != LC_NONE) d = sm.cache[code >> 16][q];
+    }
+    LDPC_DEV void lc_wb_store(uint32_t code, const uint4 &d) const
+    {
+        if (code != LC_NONE) *(uint4 *)(lcV + (size_t)(code & 0xFFFFu) * 128 + q * 16) = d;
+    }
+    LDPC_DEV void lc_fill(int p, const uint4 &d) const   // the lines loaded in period p land in their slots
+    {
+        const uint32_t code = lc_code(sm.tab[p & (TQ - 1)].loads);
+        if (code != LC_NONE) sm.cache[code >> 16][q] = d;
+    }
+    LDPC_DEV void lc_load(int p, uint4 &d) const
+    {
+        const uint32_t code = lc_code(sm.tab[p & (TQ - 1)].loads);
+        if (code != LC_NONE) d = *(const uint4 *)(lcV + (size_t)(code & 0xFFFFu) * 128 + q * 16);
+    }
 
     // ---- reads
     // in.mf = mfc (window g's codes, read in the previous period); mfn <- window g+1's
@@ -289,8 +382,12 @@ struct Slab3 {
         const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
 #pragma unroll
         for (int j = 0; j < X; j++) {
-            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)fw[j >> 1], 16 * (j & 1), 1);   // 0 / -1
-            v[j] = perm(in.fv[j], in.v[j], bfi(m, fsel, usel));
+            if constexpr (LC) {
+                v[j] = unpack_v(in.v[j], usel);
+            } else {
+                const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)fw[j >> 1], 16 * (j & 1), 1);   // 0 / -1
+                v[j] = perm(in.fv[j], in.v[j], bfi(m, fsel, usel));
+            }
         }
         v[X] = unpack_v(in.v[X], usel);
         const MsgTab t = msg_tab(in.mb);
@@ -414,10 +511,11 @@ struct Slab3 {
     // post of window g (x inputs xr): new V pairs -> stg[g % NR], messages ->
     // mst[w]; they leave in the stores of the same period
     template <bool TL, bool FZ_ = false, int MP = -1>
-    LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
+    LDPC_DEV void post(int g, uint32_t xr, const St3 &s, const uint4 &rr = uint4{}) const
     {
         constexpr bool FZ = FZ_;
-        unsigned short *st = (unsigned short *)&sm.stg[g % NR][k];      // [entry][..S slots..][8 pairs] u16
+        unsigned short *st = nullptr;                                   // [entry][..S slots..][8 pairs] u16
+        if constexpr (!LC) st = (unsigned short *)&sm.stg[g % NR][k];
         constexpr int ES = (S + 1) * 8;                                 // u16 between entries
         uint32_t MA, MB;
         if constexpr (!TL) {
@@ -444,15 +542,31 @@ struct Slab3 {
             // the o edge: message bits only (the next check rewrites V[o] as its x edge)
             (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
             MB = perm(k2, k1, 0x07030501u);
+            if constexpr (LC) {   // (rr: window g's record of this slot)
+                char *cb = (char *)cache_b() + 2 * q;
 #pragma unroll
-            for (int j = 0; j <= X; j++) st[j * ES + q] = (unsigned short)nv[j];
+                for (int j = 0; j <= X; j++) *(unsigned short *)(cb + row_of(rr, j) * 16) = (unsigned short)nv[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j <= X; j++) st[j * ES + q] = (unsigned short)nv[j];
+            }
         } else {
-            static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
-                constexpr int J = decltype(jc)::value;
-                st[J * ES + q] = (unsigned short)pack_v(s.c[J]);
-            });
-            st[X * ES + q] = (unsigned short)pack_v(xr);               // V of the last group-0 check's o edge
-            st[(D0 - 1) * ES + q] = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
+            if constexpr (LC) {
+                char *cb = (char *)cache_b() + 2 * q;
+                static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int J = decltype(jc)::value;
+                    *(unsigned short *)(cb + row_of(rr, J) * 16) = (unsigned short)pack_v(s.c[J]);
+                });
+                *(unsigned short *)(cb + row_of(rr, X) * 16) = (unsigned short)pack_v(xr);
+                *(unsigned short *)(cb + row_of(rr, D0 - 1) * 16) = (unsigned short)pack_v(s.c[X]);
+            } else {
+                static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int J = decltype(jc)::value;
+                    st[J * ES + q] = (unsigned short)pack_v(s.c[J]);
+                });
+                st[X * ES + q] = (unsigned short)pack_v(xr);               // V of the last group-0 check's o edge
+                st[(D0 - 1) * ES + q] = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
+            }
             MA = s.mn1;
             MB = s.mn2;
         }
@@ -495,8 +609,8 @@ struct Slab3 {
 // sits at position k % 8 of w (w[i] low / high half = positions 2i, 2i+1) and
 // its output goes to position k+1, so after step 8j+6 positions 0..7 hold the
 // inputs of steps 8j .. 8j+7: the x inputs post needs, stored as one uint4.
-template <int WS, int R, int B0, int B1, bool NMS = false>
-LDPC_DEV void chain_window3(Smem3<WS, R> &sm, int buf, int c, uint32_t (&w)[4])
+template <int WS, int R, int B0, int B1, bool NMS = false, typename SMT>
+LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
 {
     const uint4 *cp = &sm.cst[buf][0][c & 1][c >> 1];
     constexpr int KST = 2 * NP;       // uint4 between steps
@@ -574,10 +688,14 @@ LDPC_DEV uint32_t high_bits16(uint4 x)   // byte high bits -> 16-bit codeword ma
 // live; the snapshots are merged back at the end.  Same result as the
 // reference's per-codeword stop (oracle: syndrome after every iteration), with
 // one launch instead of one per iteration plus syndrome / snapshot kernels.
-template <int WS, int R, bool STAMP, bool ET = false, bool NMS = false>
+// LC: V rows live in the LDS line cache during a segment (grouped V layout;
+// linecache.cpp's plan): no parity-row copy, no forwarding ring, the slab waves
+// move whole lines (loads, slot writes, writebacks) beside their checks.
+template <int WS, int R, bool STAMP, bool ET = false, bool NMS = false, bool LC = false>
 __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 {
-    using SM = Smem3<WS, R>;
+    static_assert(!LC || WS == 6, "the line cache's window table holds 48 slots");
+    using SM = std::conditional_t<LC, Smem3LC<WS, R>, Smem3<WS, R>>;
     using CF = Cfg<WS, R>;
     constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U, CHW = CF::CHW, NB = CF::NB;
     __shared__ SM sm;
@@ -591,8 +709,8 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     if (!ET && a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
     // the group's parity rows -> P (consecutive checks' parity values
     // contiguous: a wave's 8 o-edge gathers / x-edge stores touch 1-2 lines,
-    // not 8), back into V at the end
-    {
+    // not 8), back into V at the end (LC: the grouped layout has them so)
+    if constexpr (!LC) {
         int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * a.wgoff;
         int8_t *ppar = a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
 #pragma unroll 8
@@ -602,6 +720,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         __syncthreads();
     }
     auto parity_out = [&]() {
+        if constexpr (LC) return;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * a.wgoff;
@@ -614,9 +733,10 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     __shared__ uint32_t et_sh[2];
     constexpr int NT = 64 * (WS + 1);
     const char *etV = (const char *)a.V + (size_t)wg * a.wgoff;
-    const char *etP = (const char *)a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
+    // (LC: the parity rows follow the information rows in the grouped layout, pitch 16)
+    const char *etP = LC ? etV + (size_t)a.k * 16 : (const char *)a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
     auto et_row = [&](uint32_t v) -> const uint4 * {   // V row piece of variable v (parity rows: in P)
-        return (int)v < a.k ? (const uint4 *)(etV + (size_t)v * (size_t)a.pitch)
+        return (LC || (int)v < a.k) ? (const uint4 *)(etV + (size_t)v * (size_t)a.pitch)
                             : (const uint4 *)(etP + (size_t)(v - (uint32_t)a.k) * 16);
     };
     if constexpr (ET) {
@@ -787,13 +907,14 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     if (wave == CHW) {
         // ------------------------------------------------------------ chain wave
         if (a.prio) __builtin_amdgcn_s_setprio(3);
-        constexpr int NCH = S * RECW / 4;   // 16-B chunks per window table
+        constexpr int TABW = LC ? (int)(sizeof(LcWin) / 4) : S * RECW;   // words per window table
+        constexpr int NCH = TABW / 4;   // 16-B chunks per window table
         constexpr int CPL = (NCH + 63) / 64;
         static_assert(CPL * DPER <= 63, "table staging");
         const int c = lane & 15;
         auto stage = [&](int u, int slot) {
-            const uint4 *src = (const uint4 *)(a.tab + (size_t)u * S * RECW);
-            const uint32_t dst = (uint32_t)(uintptr_t)&sm.tab[slot][0][0];
+            const uint4 *src = (const uint4 *)(a.tab + (size_t)u * TABW);
+            const uint32_t dst = (uint32_t)(uintptr_t)&sm.tab[slot];
 #pragma unroll
             for (int i = 0; i < CPL; i++)
                 if (lane + 64 * i < NCH) dma16(src + 64 * i + lane, dst + 1024 * i);
@@ -807,6 +928,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             w4[0] = (uint32_t)(int)((const int8_t *)et_row((uint32_t)a.x0))[c] & 0xFFFFu;
             int un = KAHEAD % a.nw;
             __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 in LDS
+            if constexpr (LC) __syncthreads();   // LC: the resident lines are in the cache
             __syncthreads();   // prologue 2: constants of window 0 in LDS
             if (STAMP) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
@@ -819,6 +941,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 if (STAMP) sA += stamp3() - tx;
                 __syncthreads();
             }
+            if constexpr (LC) __syncthreads();   // LC: the slab waves write the dirty lines back
             if (!ET || !et_after(it)) break;
         }
         write_stamps();
@@ -837,7 +960,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
     // parity rows k + j of this group at Pb + 16 j: row r at Pb - 16 k + 16 r
     char *Pr = (char *)a.P + ((size_t)wg * (size_t)(a.m + 1) - (size_t)a.k) * 16;
-    Slab3<WS, R, NMS> sl{sm,
+    Slab3<WS, R, NMS, LC> sl{sm,
                     a,
                     q >= X ? Pr : (char *)Vb,
                     q >= X ? 16u : (uint32_t)a.pitch,
@@ -855,7 +978,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     // DMA lane 8e + slot: entry e < 6 a V row (record entry e, the
                     // o edge's D0-1 for e = X), e >= 6 message piece e - 6
                     kl < X ? Vb : kl == X ? Pr : Mb + (kl - 6) * 16,
-                    Mb + (2 + (kl & 1)) * 16,
+                    LC ? Mb : Mb + (2 + (kl & 1)) * 16,
                     kl < X ? (uint32_t)a.pitch : kl == X ? 16u : (uint32_t)MREC,
                     kl < 6 ? 0xFFFFFFFFu : COOP_CHK_MASK,
                     (uint32_t)(kl < X ? kl : (kl == X ? D0 - 1 : D0)),
@@ -863,8 +986,11 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     (uint32_t)(q < 4 ? (6 + (q >> 1)) * 128 + kl * 16 + (q & 1) * 8
                                      : SM::IN_B + ((q >> 1) - 2) * 128 + kl * 16 +
                                            (q & 1) * 8)};
+    sl.lcV = Vb;
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     constexpr int NI = CF::NI, NS = CF::NS;
+    uint4 ld[NS];   // LC: lines loaded in period p (ld[p % NS]), written to their slots in period p + 2
+    const LcWin *gtab = (const LcWin *)a.tab;   // LC: the window tables in global memory
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
         __syncthreads();   // prologue 1: tables in LDS
         if constexpr (ET) {   // codewords 2q (low half) and 2q+1 (high half) of this lane: converged?
@@ -875,7 +1001,31 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         }
         St3 st[NS];
         uint4 mfc;   // records D0 .. D0+3 of the next pre's window
-        {
+        if constexpr (LC) {
+            // lines resident before period -1 -> their slots (a lane group per line)
+            for (int i = kl * WS + sw; i < a.npro; i += 8 * WS) {
+                const uint32_t code = a.lcpro[i];
+                sm.cache[code >> 16][q] = *(const uint4 *)(Vb + (size_t)(code & 0xFFFFu) * 128 + q * 16);
+            }
+            // the loads of periods -2 and -1 (written to their slots in periods 0, 1)
+            ld[(NS - 2) % NS] = make_uint4(0, 0, 0, 0);
+            ld[NS - 1] = make_uint4(0, 0, 0, 0);
+            {
+                const uint32_t c2 = sl.lc_code(gtab[a.nw - 2].loads), c1 = sl.lc_code(gtab[a.nw - 1].loads);
+                if (c2 != LC_NONE) ld[(NS - 2) % NS] = *(const uint4 *)(Vb + (size_t)(c2 & 0xFFFFu) * 128 + q * 16);
+                if (c1 != LC_NONE) ld[NS - 1] = *(const uint4 *)(Vb + (size_t)(c1 & 0xFFFFu) * 128 + q * 16);
+            }
+#pragma unroll
+            for (int i = 0; i <= R; i++) sl.gathers_lc(i, i);   // old messages of windows 0 .. R
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();   // the resident lines are in the cache
+            PreIn in;
+            sl.read_pre_lc(0, 0, in);
+            if (a.tail == 0)
+                sl.template pre<true, ET>(0, in, st[0]);
+            else
+                sl.template pre<false, ET>(0, in, st[0]);
+        } else {
             PfIn pi;
 #pragma unroll
             for (int i = 0; i <= R; i++) {   // window i -> in[w][i]   (nw > R + 3)
@@ -928,7 +1078,67 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             PfIn pi;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
-            if (fast) {
+            if constexpr (LC) {
+                // line cache: (A) read the lines written back now, (B) message
+                // stores of window p-2, post of window p-1 into the cache rows,
+                // (D) the writeback stores, (E, F) the lines loaded in period
+                // p-2 into their slots, (G) pre of window p+1 from the cache,
+                // (H) message gathers of window p+1+R, (I) this period's line
+                // loads.  Vector memory per period: B, D, H, I -- at (E) the
+                // loads of period p-2 (and the gathers before them) have 6
+                // younger operations
+                uint32_t wbc;
+                uint4 wbd = make_uint4(0, 0, 0, 0);
+                if (fast) {
+                    if (fair) __builtin_amdgcn_s_setprio(1);
+                    sl.lc_wb_read(p, wbc, wbd);
+                    sl.stores_lc(sc);
+                    const uint32_t xr = sl.read_x(p - 1, sp);
+                    sl.template post<false, ET, MP1>(p - 1, xr, sp, sl.rec(p - 1));
+                    sl.lc_wb_store(wbc, wbd);
+                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                    sl.lc_fill(p - 2, ld[(s + NS - 2) % NS]);
+                    sl.read_pre_lc(p + 1, (s + 1) % NI, in);
+                    sl.gathers_lc(p + 1 + R, (s + R + 1) % NI);
+                    sl.lc_load(p, ld[s]);
+                    sl.read_st_lc(p - 1, sc);
+                    if (STAMP) t1 = t2 = stampL();
+                    if (fair) __builtin_amdgcn_s_setprio(0);
+                    sl.template pre<false, ET, MP2>(p + 1, in, sn);
+                    if (STAMP) t3 = stampL();
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    sl.lc_wb_read(p, wbc, wbd);
+                    if (dst) sl.stores_lc(sc);
+                    if (dpo) {
+                        const uint32_t xr = sl.read_x(p - 1, sp);
+                        if (uA == a.tail)
+                            sl.template post<true, ET>(p - 1, xr, sp, sl.rec(p - 1));
+                        else
+                            sl.template post<false, ET>(p - 1, xr, sp, sl.rec(p - 1));
+                    }
+                    sl.lc_wb_store(wbc, wbd);
+                    {   // periods 0, 1: the prologue's loads, listed in the tables of windows nw-2, nw-1
+                        const uint32_t *fl = p >= 2 ? sm.tab[(p - 2) & (TQ - 1)].loads : gtab[a.nw - 2 + p].loads;
+                        const uint32_t code = sl.lc_code(fl);
+                        if (code != LC_NONE) sm.cache[code >> 16][q] = ld[(s + NS - 2) % NS];
+                    }
+                    if (STAMP) t1 = t2 = t3 = stampL();
+                    if (dpr) {
+                        sl.read_pre_lc(p + 1, (s + 1) % NI, in);
+                        if (uB == a.tail)
+                            sl.template pre<true, ET>(p + 1, in, sn);
+                        else
+                            sl.template pre<false, ET>(p + 1, in, sn);
+                        sl.gathers_lc(p + 1 + R, (s + R + 1) % NI);
+                    }
+                    sl.lc_load(p, ld[s]);
+                    if (dpo) {
+                        sl.read_st_lc(p - 1, sc);
+                        sc_tl = uA == a.tail;
+                    }
+                }
+            } else if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs, nothing from memory) and waits for its window
                 // p+1 gathers only before its pre, half a period later than at
@@ -1006,7 +1216,18 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)
                 period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
         });
-        sl.stores(sc, sc_tl);   // window G-1
+        if constexpr (LC) {
+            sl.stores_lc(sc);   // window G-1
+            // the dirty lines still in the cache go back to V
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            for (int i = kl * WS + sw; i < a.nepi; i += 8 * WS) {
+                const uint32_t code = a.lcepi[i];
+                *(uint4 *)(Vb + (size_t)(code & 0xFFFFu) * 128 + q * 16) = sm.cache[code >> 16][q];
+            }
+        } else {
+            sl.stores(sc, sc_tl);   // window G-1
+        }
         if (!ET || !et_after(it)) break;
     }
     write_stamps();
@@ -1188,6 +1409,49 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
     cc->S = S;
     cc->R = r;
     cc->nw = nw;
+    // the LDS line cache (LDPC_COOP3_LC=1): plan, window tables, prologue /
+    // epilogue lists; without a plan coop3 runs its forwarding-ring path
+    if (S == 48 && env_int3("LDPC_COOP3_LC", 0) != 0 && h->m < 65536 && h->n % 8 == 0) {
+        LcPlan lp;
+        if (lc_build_plan(pl.tab, RECW, nw, S, D0, pl.tail, h->n, LC_SLOTS, lp) == 0) {
+            std::vector<LcWin> wt((size_t)nw);
+            const uint32_t sink = (uint32_t)(h->n / 8);   // slot 0
+            for (int u = 0; u < nw; u++) {
+                LcWin &W = wt[(size_t)u];
+                for (int k = 0; k < S; k++) {
+                    const uint32_t *rec = &pl.tab[((size_t)u * S + k) * RECW];
+                    const uint16_t *ro = &lp.rowoff[((size_t)u * S + k) * 8];
+                    const uint32_t act = (rec[D0] & COOP_M_ACT) ? 1u : 0u, step = (rec[D0] >> STEP_SHIFT) & 63u;
+                    W.rec[k] = make_uint4(ro[0] | (uint32_t)ro[1] << 16, ro[2] | (uint32_t)ro[3] << 16,
+                                          ro[4] | (uint32_t)ro[5] << 16, ro[6] | (step | act << 6) << 16);
+                    W.chk[k] = (uint16_t)(rec[D0] & COOP_CHK_MASK);
+                }
+                for (int i = 0; i < LC_LMAX; i++) {
+                    // entries 0 .. 5 always present (one per slab wave: every wave
+                    // issues each line operation every period, for the vmcnt counts)
+                    const uint32_t l = lp.loads[(size_t)u * LC_LMAX + i], b = lp.wbs[(size_t)u * LC_LMAX + i];
+                    W.loads[i] = (l == LC_NONE && i < 6) ? sink : l;
+                    W.wbs[i] = (b == LC_NONE && i < 6) ? sink : b;
+                }
+            }
+            const size_t tb = wt.size() * sizeof(LcWin);
+            if (hipMalloc(&cc->d_lctab, tb) != hipSuccess ||
+                hipMalloc(&cc->d_lcpro, 4 * std::max<size_t>(1, lp.pro.size())) != hipSuccess ||
+                hipMalloc(&cc->d_lcepi, 4 * std::max<size_t>(1, lp.epi.size())) != hipSuccess ||
+                hipMemcpy(cc->d_lctab, wt.data(), tb, hipMemcpyHostToDevice) != hipSuccess ||
+                (lp.pro.size() && hipMemcpy(cc->d_lcpro, lp.pro.data(), 4 * lp.pro.size(), hipMemcpyHostToDevice) !=
+                                      hipSuccess) ||
+                (lp.epi.size() && hipMemcpy(cc->d_lcepi, lp.epi.data(), 4 * lp.epi.size(), hipMemcpyHostToDevice) !=
+                                      hipSuccess)) {
+                coop_free(cc);
+                return ldpc_set_error(LDPC_EDEVICE, "coop3 line-cache tables");
+            }
+            cc->lc_valid = 1;
+            cc->lc_slots = lp.slots;
+            cc->n_pro = (int)lp.pro.size();
+            cc->n_epi = (int)lp.epi.size();
+        }
+    }
     cc->tail = pl.tail;
     cc->n_fwd = pl.n_fwd;
     cc->x0 = (int)h->edge_var[h->check_start[0] + X];
@@ -1209,6 +1473,7 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     if (L.early && coop3_et_in_kernel(cc, L.n)) {
         // in-kernel early termination (one launch, coop3_decode<.., ET>)
         if (!L.iters_used) return -1;
+        if (L.vpriv && cc.lc_valid && (size_t)L.n * 2 > sizeof(Smem3LC<6, 2>)) return -1;
         if (L.iters == 0) {
             hipLaunchKernelGGL(fill_iters3_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used, 0);
             return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1241,7 +1506,15 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     // V layout: rows of L.vpitch codewords, a group's 16 B at wg * 16 in each;
     // or (L.vpriv) every group's rows contiguous, [stride / 16][n + 1][16]
     a.pitch = L.vpriv ? CW : L.vpitch;
-    a.wgoff = L.vpriv ? (size_t)(L.n + 1) * CW : (size_t)CW;
+    a.wgoff = L.vpriv ? (size_t)(L.n + 8) * CW : (size_t)CW;
+    const bool lc = L.vpriv && cc.lc_valid;   // the line cache needs the grouped layout
+    if (lc) {
+        a.tab = cc.d_lctab;
+        a.lcpro = cc.d_lcpro;
+        a.lcepi = cc.d_lcepi;
+        a.npro = cc.n_pro;
+        a.nepi = cc.n_epi;
+    }
     a.G = cc.nw * iters;
     a.nw = cc.nw;
     a.tail = cc.tail;
@@ -1276,6 +1549,23 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
     int rc;
+    if (lc) {
+        if (stamped) (void)hipFree(a.stamps);
+        if (ws != 6) return -1;
+        if (et) {
+            if (L.algo == LDPC_ALGO_NMS)
+                hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+            else
+                hipLaunchKernelGGL((coop3_decode<6, 2, false, true, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+        } else {
+            if (L.algo == LDPC_ALGO_NMS)
+                hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+            else
+                hipLaunchKernelGGL((coop3_decode<6, 2, false, false, false, true>), dim3(grid), dim3(64 * 7), 0, s,
+                                   a);
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (et) {
         if (stamped) (void)hipFree(a.stamps);
         if (L.algo == LDPC_ALGO_NMS)

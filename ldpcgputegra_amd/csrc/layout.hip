@@ -16,11 +16,11 @@
 namespace {
 
 // V element (node i, codeword b): row-major V[i][stride], or (GROUPED) the
-// 16-codeword-group layout V[b / 16][n + 1][16]
+// 16-codeword-group layout V[b / 16][n + 8][16] (rows n .. n+7: the sink line)
 template <bool GROUPED>
 __device__ __forceinline__ size_t vidx(int i, int b, int n, int stride)
 {
-    return GROUPED ? ((size_t)(b >> 4) * (size_t)(n + 1) + (size_t)i) * 16 + (size_t)(b & 15)
+    return GROUPED ? ((size_t)(b >> 4) * (size_t)(n + 8) + (size_t)i) * 16 + (size_t)(b & 15)
                    : (size_t)i * stride + b;
 }
 

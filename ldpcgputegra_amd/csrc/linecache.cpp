@@ -379,8 +379,12 @@ int lc_check_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
         staged[cmod(p, 3)].assign(o.loads.begin() + (size_t)pm * LC_LMAX,
                                   o.loads.begin() + (size_t)(pm + 1) * LC_LMAX);
         staged_at[cmod(p, 3)] = p;
-        for (uint32_t c : staged[cmod(p, 3)])
-            if (c != LC_NONE && p - last_store[line_of(c)] < 2) return -8;
+        for (uint32_t c : staged[cmod(p, 3)]) {
+            if (c == LC_NONE) continue;
+            if (p - last_store[line_of(c)] < 2) return -8;   // its last writeback too recent
+            for (int s = 1; s < NS; s++)                     // a dirty copy still cached: the load is stale
+                if (holds[s] == (int64_t)line_of(c) && dirty[s]) return -11;
+        }
     }
     // epilogue: every dirty slot must be in the list
     std::vector<char> flushed(NS, 0);
