@@ -52,6 +52,7 @@ struct Lane {
     Scratch sc;
     void *d_io = nullptr;           // chunk input (LLRs) | output (hard decisions)
     size_t io_bytes = 0;
+    hipEvent_t h2d_done = nullptr;  // this lane's input copy finished (the next lane's copy waits on it)
 };
 
 struct ldpc_ctx {
@@ -179,6 +180,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
         if (l.stream) (void)hipStreamSynchronize(l.stream);
         l.sc.release();
         (void)hipFree(l.d_io);
+        if (l.h2d_done) (void)hipEventDestroy(l.h2d_done);
         if (l.stream) (void)hipStreamDestroy(l.stream);
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -325,8 +327,12 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
     }
 }
 
+// alloc_only: size the scratch for this decode and return (decode_host sizes
+// every lane before it queues any work: a hipFree mid-pipeline would wait for
+// the device)
 static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_llr, uint8_t *d_hard, void *d_soft,
-                         int32_t *d_iters, int batch, int n_iter, const ldpc_params *p, bool is_float)
+                         int32_t *d_iters, int batch, int n_iter, const ldpc_params *p, bool is_float,
+                         bool alloc_only = false)
 {
     int rc = check_params(c, batch, n_iter, p, is_float);
     if (rc != LDPC_OK) return rc;
@@ -339,6 +345,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     if (kern < 0)
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d selected but not applicable to these params", c->kernel);
     c->last_kernel = kern;
+    if (kern == 7 && alloc_only) return LDPC_OK;
     if (kern == 7) {   // LDS-resident: frame-major in and out, no scratch, no transposes
         DecodeLaunch L{};
         L.batch = batch;
@@ -393,6 +400,14 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     const size_t v_rows = vpriv ? (size_t)h->n + 8 : (size_t)h->n + 1;
     if ((rc = ensure(&sc.d_V, &sc.V_bytes, v_rows * vpitch * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_need)) != LDPC_OK) return rc;
+    // early termination: live u8 | bad u32 | iterations used i32 (when the caller passed none)
+    const bool et_state = (kern == 5 || kern == 8) && p->early_term;
+    // V snapshots: only coop3's per-iteration launches need them (where its
+    // in-kernel early termination does not apply)
+    const bool et_vs = et_state && kern == 8 && !coop3_et_in_kernel(c->coop3, h->n);
+    if (et_state && (rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
+    if (et_vs && (rc = ensure(&sc.d_Vs, &sc.Vs_bytes, (size_t)(h->n + 1) * vpitch)) != LDPC_OK) return rc;
+    if (alloc_only) return LDPC_OK;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
     HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));
@@ -429,18 +444,11 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
     L.iters_used = d_iters;
     L.lds_pad = c->lds_pad;
-    if ((kern == 5 || kern == 8) && p->early_term) {
-        // live u8 | bad u32 | iterations used i32 (when the caller passed none)
-        if ((rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
+    if (et_state) {
         L.bad = (uint32_t *)sc.d_early;
         if (!L.iters_used) L.iters_used = (int32_t *)((char *)sc.d_early + (size_t)stride * 4);
         L.live = (uint8_t *)sc.d_early + (size_t)stride * 8;
-        // V snapshots: only coop3's per-iteration launches need them (where
-        // its in-kernel early termination does not apply)
-        if (kern == 8 && !coop3_et_in_kernel(c->coop3, h->n)) {
-            if ((rc = ensure(&sc.d_Vs, &sc.Vs_bytes, (size_t)(h->n + 1) * vpitch)) != LDPC_OK) return rc;
-            L.Vs = (int8_t *)sc.d_Vs;
-        }
+        if (et_vs) L.Vs = (int8_t *)sc.d_Vs;
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (c->profile) {
@@ -489,34 +497,41 @@ extern "C" int ldpc_decode_f32_async(ldpc_ctx *c, void *s, const float *d_llr, u
 }
 
 // Chunks of the host-buffer path: whole 64-codeword rows, at least 256
-// codewords each (16 coop workgroups), LDPC_HOST_CHUNKS of them (at most 16;
-// default 2 when the input is large enough for its copy time to matter,
-// >= 64 MB, else 1).  Concurrent chunk decodes need hardware queues of their
-// own: HIP maps streams onto GPU_MAX_HW_QUEUES (4) queues per process, and
-// the null stream and the context's stream hold two of them, so a third
-// lane would share a queue -- and wait for -- the first one's decode
-// (measured: 4 lanes on 2 queues, 114 ms per DVB-S2 4096-codeword call vs
-// 68 ms unchunked).
+// codewords each (16 coop workgroups), LDPC_HOST_CHUNKS of them (default 2
+// when the input is large enough for its copy time to matter, >= 64 MB, else
+// 1), and no more than the hardware queues left for them.  Concurrent chunk
+// decodes need hardware queues of their own: HIP maps streams round-robin onto
+// GPU_MAX_HW_QUEUES (default 4) queues per process, and the null stream and
+// the context's stream hold two of them, so a third lane would share a queue
+// -- and wait for -- the first one's decode (measured: 4 lanes on 2 queues,
+// 114 ms per DVB-S2 4096-codeword call vs 68 ms unchunked).
 static int host_chunks(int batch, size_t in_bytes)
 {
     const int def = in_bytes >= ((size_t)64 << 20) ? 2 : 1;
-    const int want = std::min(16, std::max(1, getenv_int("LDPC_HOST_CHUNKS", def)));
+    const int lanes = std::max(1, getenv_int("GPU_MAX_HW_QUEUES", 4) - 2);
+    const int want = std::min(lanes, std::max(1, getenv_int("LDPC_HOST_CHUNKS", def)));
     return std::max(1, std::min(want, batch / 256));
 }
 
 // The host-buffer path (CDecoder::decode(char*, char*, int), synchronous).
 // The batch is cut into chunks; chunk i runs on lane i (own stream, scratch
-// and staging): H2D(i) -> decode(i) are queued chunk by chunk, then the D2H
-// copies, so the copies of one chunk overlap the decodes of the others -- the
-// reference's W streams x F frames scheme (paper/ldpcGpuTegra.tex:279-289;
-// its decode_stream, code/gpu_fixed/decoder_ms/CGPU_Decoder_MS_SIMD.cu:219-275,
-// runs one stream with blocking copies).  A staircase-code decode takes about
-// as long for one 16-codeword workgroup as for a whole chip of them (its
-// serial chain is per workgroup), so the concurrent chunk decodes cost
-// nothing: a call takes ~ H2D(batch) + one decode + D2H(one chunk).  Pinned
-// host buffers (ldpc_host_alloc) make the copies asynchronous DMA; pageable
-// ones are staged by the HIP runtime (the host thread blocks in the copy, the
-// GPU keeps decoding).
+// and staging): H2D(i) -> decode(i) -> D2H(i), so the copies of one chunk
+// overlap the decodes of the others -- the reference's W streams x F frames
+// scheme (paper/ldpcGpuTegra.tex:279-289; its decode_stream,
+// code/gpu_fixed/decoder_ms/CGPU_Decoder_MS_SIMD.cu:219-275, runs one stream
+// with blocking copies).  A staircase-code decode takes about as long for one
+// 16-codeword workgroup as for a whole chip of them (its serial chain is per
+// workgroup), so the concurrent chunk decodes cost nothing.  The input copies
+// are chained (lane i's waits for lane i-1's): two concurrent copies share
+// the link and both finish at the end (measured r03e, pinned, 2 chunks: 4.7
+// ms each, side by side), which held every decode back until all the input
+// had arrived.  A call therefore takes about H2D(batch) + one decode +
+// D2H(one chunk) -- no chunking can do better, since the last chunk cannot
+// start before all the input is on the device.  Every lane's
+// scratch is sized before any work is queued.  Pinned host buffers
+// (ldpc_host_alloc) make the copies asynchronous DMA; pageable ones are
+// staged by the HIP runtime (the host thread blocks in the copy, the GPU
+// keeps decoding).
 static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, int n_iter, const ldpc_params *p,
                        bool is_float)
 {
@@ -526,8 +541,44 @@ static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, i
     HIP_TRY(hipSetDevice(c->device));
     const size_t esz = is_float ? 4 : 1;
     const int n = c->code->n, nc = host_chunks(batch, (size_t)batch * n * esz);
-    const int cs = ((batch + nc - 1) / nc + 63) / 64 * 64;   // codewords per chunk
+    // chunk boundaries (64-codeword rows): sizes falling 2:1 from chunk to
+    // chunk, so each chunk's output copy, which starts when its decode ends,
+    // is hidden under the later chunks' input copies and decodes, and only the
+    // smallest, last chunk's copy trails the call (2 chunks: 2/3 + 1/3)
+    std::vector<int> b0s(1, 0);
+    {
+        const int rows = (batch + 63) / 64;
+        int left = rows, wsum = (1 << nc) - 1;
+        for (int i = 0; i < nc - 1; i++) {
+            const int w = 1 << (nc - 1 - i);
+            const int r = std::max(4, std::min(left - 4 * (nc - 1 - i), (int)(((long)left * w + wsum / 2) / wsum)));
+            b0s.push_back(std::min(batch, b0s.back() + r * 64));
+            left -= r;
+            wsum -= w;
+        }
+        b0s.push_back(batch);
+    }
+    int cs = 0;   // largest chunk (the staging size of every lane)
+    for (int i = 0; i < nc; i++) cs = std::max(cs, b0s[i + 1] - b0s[i]);
     if ((int)c->lanes.size() < nc) c->lanes.resize(nc);
+    auto in_al = [&](int nb) { return ((size_t)nb * n * esz + 255) / 256 * 256; };
+    // streams, events and every lane's buffers first (no hipFree between queued work)
+    for (int i = 0; i < nc; i++) {
+        Lane &l = c->lanes[i];
+        const int b0 = b0s[i], nb = b0s[i + 1] - b0;
+        if (!l.stream && hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess) {
+            l.stream = nullptr;
+            return ldpc_set_error(LDPC_EDEVICE, "host path: hipStreamCreate");
+        }
+        if (!l.h2d_done && hipEventCreateWithFlags(&l.h2d_done, hipEventDisableTiming) != hipSuccess) {
+            l.h2d_done = nullptr;
+            return ldpc_set_error(LDPC_EDEVICE, "host path: hipEventCreate");
+        }
+        if ((rc = ensure(&l.d_io, &l.io_bytes, in_al(nb) + (size_t)cs * n)) != LDPC_OK) return rc;
+        if ((rc = decode_device(c, l.sc, l.stream, l.d_io, nullptr, nullptr, nullptr, nb, n_iter, p, is_float,
+                                true)) != LDPC_OK)
+            return rc;
+    }
     int used = 0;
     // every queued lane is joined before returning, on success and on error
     auto finish = [&](int r) {
@@ -537,28 +588,24 @@ static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, i
         }
         return r;
     };
-    for (int i = 0, b0 = 0; b0 < batch; i++, b0 += cs) {
+    for (int i = 0; i < nc; i++) {
         Lane &l = c->lanes[i];
-        const int nb = std::min(cs, batch - b0);
-        const size_t in_bytes = (size_t)nb * n * esz, in_al = (in_bytes + 255) / 256 * 256;
-        if (!l.stream && hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess) {
-            l.stream = nullptr;
-            return finish(ldpc_set_error(LDPC_EDEVICE, "host path: hipStreamCreate"));
-        }
+        const int b0 = b0s[i], nb = b0s[i + 1] - b0;
+        char *d_in = (char *)l.d_io, *d_out = d_in + in_al(nb);
         used = i + 1;
-        if ((rc = ensure(&l.d_io, &l.io_bytes, in_al + (size_t)cs * n)) != LDPC_OK) return finish(rc);
-        char *d_in = (char *)l.d_io, *d_out = d_in + in_al;
-        if (hipMemcpyAsync(d_in, (const char *)llr + (size_t)b0 * n * esz, in_bytes, hipMemcpyHostToDevice,
-                           l.stream) != hipSuccess)
+        if (i > 0 && hipStreamWaitEvent(l.stream, c->lanes[i - 1].h2d_done, 0) != hipSuccess)
+            return finish(ldpc_set_error(LDPC_EDEVICE, "host path: hipStreamWaitEvent"));
+        if (hipMemcpyAsync(d_in, (const char *)llr + (size_t)b0 * n * esz, (size_t)nb * n * esz,
+                           hipMemcpyHostToDevice, l.stream) != hipSuccess ||
+            hipEventRecord(l.h2d_done, l.stream) != hipSuccess)
             return finish(ldpc_set_error(LDPC_EDEVICE, "host path H2D: %s", hipGetErrorString(hipGetLastError())));
         rc = decode_device(c, l.sc, l.stream, d_in, (uint8_t *)d_out, nullptr, nullptr, nb, n_iter, p, is_float);
         if (rc != LDPC_OK) return finish(rc);
     }
-    for (int i = 0, b0 = 0; b0 < batch; i++, b0 += cs) {
+    for (int i = 0; i < nc; i++) {
         Lane &l = c->lanes[i];
-        const int nb = std::min(cs, batch - b0);
-        const size_t in_al = ((size_t)nb * n * esz + 255) / 256 * 256;
-        if (hipMemcpyAsync(hard + (size_t)b0 * n, (char *)l.d_io + in_al, (size_t)nb * n, hipMemcpyDeviceToHost,
+        const int b0 = b0s[i], nb = b0s[i + 1] - b0;
+        if (hipMemcpyAsync(hard + (size_t)b0 * n, (char *)l.d_io + in_al(nb), (size_t)nb * n, hipMemcpyDeviceToHost,
                            l.stream) != hipSuccess)
             return finish(ldpc_set_error(LDPC_EDEVICE, "host path D2H: %s", hipGetErrorString(hipGetLastError())));
     }

@@ -1077,7 +1077,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             PreIn in;
             PfIn pi;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
-            unsigned long long t1 = 0, t2 = 0, t3 = 0;
+            unsigned long long t1 = 0, t2 = 0, t3 = 0, ta = 0, tb = 0;
             if constexpr (LC) {
                 // line cache: (A) read the lines written back now, (B) message
                 // stores of window p-2, post of window p-1 into the cache rows,
@@ -1095,8 +1095,10 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     sl.stores_lc(sc);
                     const uint32_t xr = sl.read_x(p - 1, sp);
                     sl.template post<false, ET, MP1>(p - 1, xr, sp, sl.rec(p - 1));
+                    if (STAMP) ta = stampL();
                     sl.lc_wb_store(wbc, wbd);
                     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                    if (STAMP) tb = stampL();
                     sl.lc_fill(p - 2, ld[(s + NS - 2) % NS]);
                     sl.read_pre_lc(p + 1, (s + 1) % NI, in);
                     sl.gathers_lc(p + 1 + R, (s + R + 1) % NI);
@@ -1188,7 +1190,12 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if (STAMP) {
                 const unsigned long long t5 = stampL();
                 sA += t5 - tx;
-                if (fast) {
+                if (fast && LC) {   // post | writeback + wait for the loads | cache fill, LDS reads, issue | pre
+                    sP[0] += ta - tx;
+                    sP[1] += tb - ta;
+                    sP[2] += t1 - tb;
+                    sP[3] += t3 - t1;
+                } else if (fast) {
                     sP[0] += t1 - tx;
                     sP[1] += t2 - t1;
                     sP[2] += t3 - t2;
@@ -1248,7 +1255,7 @@ int env_int3(const char *name, int def)
 
 // diagnostic build (LDPC_COOP3_STAMP=1): per-period cycles of each wave
 template <int WS>
-void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
+void report_stamps3(const unsigned long long *d, int grid, hipStream_t s, bool lc = false)
 {
     constexpr int nwaves = WS + 1, CHW = WS >= 3 ? 3 : WS;
     std::vector<unsigned long long> h((size_t)grid * nwaves * 8);
@@ -1269,6 +1276,9 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
         const double *x = &v[w * 8];
         if (w == CHW)
             fprintf(stderr, "  chain %d: busy %.0f steps %.0f\n", w, x[0], x[1]);
+        else if (lc)
+            fprintf(stderr, "  slab %d: busy %.0f | post %.0f wb+vmcnt %.0f fill+lds+issue %.0f pre %.0f\n", w, x[0],
+                    x[1], x[2], x[3], x[4]);
         else
             fprintf(stderr, "  slab %d: busy %.0f | vmcnt %.0f %s %.0f %s %.0f mem %.0f\n", w, x[0], x[1],
                     w == 0 ? "post" : "pre", x[2], w == 0 ? "pre" : "post", x[3], x[0] - x[1] - x[2] - x[3]);
@@ -1550,8 +1560,15 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     }
     int rc;
     if (lc) {
-        if (stamped) (void)hipFree(a.stamps);
         if (ws != 6) return -1;
+        if (stamped && !et && L.algo != LDPC_ALGO_NMS) {
+            hipLaunchKernelGGL((coop3_decode<6, 2, true, false, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+            rc = hipGetLastError() == hipSuccess ? 0 : -1;
+            if (rc == 0) report_stamps3<6>(a.stamps, grid, s, true);
+            (void)hipFree(a.stamps);
+            return rc;
+        }
+        if (stamped) (void)hipFree(a.stamps);
         if (et) {
             if (L.algo == LDPC_ALGO_NMS)
                 hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true, true>), dim3(grid), dim3(64 * 7), 0, s, a);

@@ -34,6 +34,8 @@ for s in ${STEPS//,/ }; do
     mixed) step bench_mixed 300 python3 bench.py --mixed ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
     tests) step tests 900 python3 -u -m pytest ${TESTS:-tests} -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "${TESTK:-not nothing}" ;;
     prof) PROF_OUT=$OUT/prof bash tools/profile.sh || exit $? ;;
+    hostrate) step host_rate 300 python3 tools/host_path_rate.py ${HOST_CHUNKS:-2 1} ;;
+    hptrace) step host_trace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/hptrace" -o hp -- python3 tools/host_path_rate.py 2 ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     esac
 done
