@@ -116,7 +116,7 @@ struct alignas(16) Smem3 {
 
 // ---- the LDS line cache (the V rows of a workgroup's codewords in whole
 // 128-B lines: linecache.cpp plans which line sits in which slot when)
-constexpr int LC_SLOTS = 760;         // cache lines (8 rows x 16 codewords each) beside the pipeline
+constexpr int LC_SLOTS = 800;         // cache lines (8 rows x 16 codewords each) beside the pipeline
 struct alignas(16) LcWin {            // one window's table (global [nw] array, LDS-DMA'd by the chain wave)
     uint4 rec[48];                    // slot k: cache rows (slot * 8 + var % 8) of record entries 0..6 (u16),
                                       // then meta16 = chain step | active << 6
@@ -131,13 +131,17 @@ struct alignas(16) Smem3LC {
     using CF = Cfg<WS, R>;
     static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
     static constexpr uint32_t IN_B = 0;   // (the forwarding-ring layout's field, unused here)
+    uint4 mst[WS][8][4];              // new messages (as Smem3; first: the line loads' M0 bases, slot
+                                      // address - 128 x lane group, stay above LDS address 0)
     uint4 cache[LC_SLOTS][8];         // the line cache (slot 0: the sink line of the inactive slots)
     LcWin tab[TQ];                    // window tables, window g in slot g % TQ
     uint4 cst[2][S][2][NP];           // chain constants (as Smem3)
     uint4 xo[2][S / 8][CW];           // chain inputs (as Smem3)
     uint4 inm[WS][NI][8][4];          // one window's old message records per slab wave ([slot] x 64 B)
-    uint4 mst[WS][8][4];              // new messages (as Smem3)
 };
+static_assert(sizeof(Smem3LC<6, 2>) <= 160 * 1024, "coop3 line cache: 160 KB of LDS per workgroup");
+using Smem3LC62 = Smem3LC<6, 2>;
+static_assert(offsetof(Smem3LC62, cache) >= 7 * 128, "line loads: M0 >= 0");
 
 struct Coop3Args {
     int8_t *V;                        // V[n + 1][pitch]; row n is the sink of inactive slots
@@ -280,15 +284,57 @@ struct Slab3 {
     {
         if (code != LC_NONE) *(uint4 *)(lcV + (size_t)(code & 0xFFFFu) * 128 + q * 16) = d;
     }
-    LDPC_DEV void lc_fill(int p, const uint4 &d) const   // the lines loaded in period p land in their slots
+    // this period's line loads, straight into their slots by LDS-DMA: lane
+    // group li (8 lanes, one 128-B line) of the wave per instruction, M0 =
+    // slot address - 128 li (the DMA writes lane l's 16 B at M0 + 16 l).  Every
+    // list entry is a line (the host pads with the sink line, slot 0), so each
+    // wave issues exactly 8 per period and the vmcnt counts stay exact; the
+    // compiler neither sees nor waits for them (no VGPR destination)
+    LDPC_DEV void lc_dma(uint32_t code) const
     {
-        const uint32_t code = lc_code(sm.tab[p & (TQ - 1)].loads);
-        if (code != LC_NONE) sm.cache[code >> 16][q] = d;
+        const char *ga = lcV + (size_t)(code & 0xFFFFu) * 128 + q * 16;
+        const uint32_t m0v = (uint32_t)(uintptr_t)cache_b() + (code >> 16) * 128u - (uint32_t)kl * 128u;
+#pragma unroll
+        for (int li = 0; li < 8; li++) {
+            const uint32_t m = __builtin_amdgcn_readlane(m0v, 8 * li);
+            if (kl == li) dma16(ga, m);
+        }
     }
-    LDPC_DEV void lc_load(int p, uint4 &d) const
+    // fast periods: every table word of period p read in one batch at its
+    // start (one exposed LDS latency, shared with the chain outputs' read,
+    // instead of a dependent round trip before each line / gather operation)
+    struct LcPf {
+        uint32_t wbc, ldc, gchk, stchk;
+        uint4 rrn, rrp;   // records of windows p+1 (pre) and p-1 (post)
+    };
+    LDPC_DEV void lc_prefetch(int p, LcPf &f) const
     {
-        const uint32_t code = lc_code(sm.tab[p & (TQ - 1)].loads);
-        if (code != LC_NONE) d = *(const uint4 *)(lcV + (size_t)(code & 0xFFFFu) * 128 + q * 16);
+        f.wbc = lc_code(sm.tab[p & (TQ - 1)].wbs);
+        f.ldc = lc_code(sm.tab[p & (TQ - 1)].loads);
+        f.rrn = rec(p + 1);
+        f.rrp = rec(p - 1);
+        f.gchk = sm.tab[(p + 1 + R) & (TQ - 1)].chk[8 * w + ((lane >> 2) & 7)];
+        f.stchk = sm.tab[(p - 1) & (TQ - 1)].chk[k];
+    }
+    LDPC_DEV void lc_line_read(uint32_t code, uint4 &d) const
+    {
+        if (code != LC_NONE) d = sm.cache[code >> 16][q];
+    }
+    LDPC_DEV void read_pre_lc(const uint4 &rr, int ib, PreIn &in) const
+    {
+        const char *cb = cache_b() + 4 * (q >> 1);
+#pragma unroll
+        for (int j = 0; j < X; j++) in.v[j] = *(const uint32_t *)(cb + row_of(rr, j) * 16);
+        in.v[X] = *(const uint32_t *)(cb + row_of(rr, D0 - 1) * 16);
+        const uint2 mm = *(const uint2 *)((const char *)&sm.inm[w][ib][kl][0] + 8 * q);
+        in.ma = mm.x;
+        in.mb = mm.y;
+        const uint32_t m16 = rr.w >> 16;
+        in.mf = make_uint4(((m16 & 64u) ? COOP_M_ACT : 0u) | (m16 & 63u) << STEP_SHIFT, 0u, 0u, 0u);
+    }
+    LDPC_DEV void gathers_lc_c(uint32_t c, int ib) const
+    {
+        if (lane < 32) dma16(g2base + (size_t)c * MREC + (lane & 3) * 16, (uint32_t)(uintptr_t)&sm.inm[w][ib][0][0]);
     }
 
     // ---- reads
@@ -989,8 +1035,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     sl.lcV = Vb;
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     constexpr int NI = CF::NI, NS = CF::NS;
-    uint4 ld[NS];   // LC: lines loaded in period p (ld[p % NS]), written to their slots in period p + 2
-    const LcWin *gtab = (const LcWin *)a.tab;   // LC: the window tables in global memory
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
         __syncthreads();   // prologue 1: tables in LDS
         if constexpr (ET) {   // codewords 2q (low half) and 2q+1 (high half) of this lane: converged?
@@ -1006,14 +1050,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             for (int i = kl * WS + sw; i < a.npro; i += 8 * WS) {
                 const uint32_t code = a.lcpro[i];
                 sm.cache[code >> 16][q] = *(const uint4 *)(Vb + (size_t)(code & 0xFFFFu) * 128 + q * 16);
-            }
-            // the loads of periods -2 and -1 (written to their slots in periods 0, 1)
-            ld[(NS - 2) % NS] = make_uint4(0, 0, 0, 0);
-            ld[NS - 1] = make_uint4(0, 0, 0, 0);
-            {
-                const uint32_t c2 = sl.lc_code(gtab[a.nw - 2].loads), c1 = sl.lc_code(gtab[a.nw - 1].loads);
-                if (c2 != LC_NONE) ld[(NS - 2) % NS] = *(const uint4 *)(Vb + (size_t)(c2 & 0xFFFFu) * 128 + q * 16);
-                if (c1 != LC_NONE) ld[NS - 1] = *(const uint4 *)(Vb + (size_t)(c1 & 0xFFFFu) * 128 + q * 16);
             }
 #pragma unroll
             for (int i = 0; i <= R; i++) sl.gathers_lc(i, i);   // old messages of windows 0 .. R
@@ -1081,29 +1117,32 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if constexpr (LC) {
                 // line cache: (A) read the lines written back now, (B) message
                 // stores of window p-2, post of window p-1 into the cache rows,
-                // (D) the writeback stores, (E, F) the lines loaded in period
-                // p-2 into their slots, (G) pre of window p+1 from the cache,
-                // (H) message gathers of window p+1+R, (I) this period's line
-                // loads.  Vector memory per period: B, D, H, I -- at (E) the
-                // loads of period p-2 (and the gathers before them) have 6
-                // younger operations
+                // (D) the writeback stores, (G) pre of window p+1 from the
+                // cache, (H) message gathers of window p+1+R, (I) this
+                // period's 8 line loads (LDS-DMA into their slots).  Vector
+                // memory per fast period and wave: B, D, H, 8 x I = 11
+                // operations; vmcnt(11) before the barrier leaves the previous
+                // period's complete: its line loads are in the cache for the
+                // next period (first read two periods after the issue) and
+                // the gathers of window p+R, read in period p+R-1, have landed
                 uint32_t wbc;
                 uint4 wbd = make_uint4(0, 0, 0, 0);
                 if (fast) {
                     if (fair) __builtin_amdgcn_s_setprio(1);
-                    sl.lc_wb_read(p, wbc, wbd);
+                    typename decltype(sl)::LcPf f;
+                    sl.lc_prefetch(p, f);
                     sl.stores_lc(sc);
                     const uint32_t xr = sl.read_x(p - 1, sp);
-                    sl.template post<false, ET, MP1>(p - 1, xr, sp, sl.rec(p - 1));
+                    sl.lc_line_read(f.wbc, wbd);
+                    sl.template post<false, ET, MP1>(p - 1, xr, sp, f.rrp);
                     if (STAMP) ta = stampL();
-                    sl.lc_wb_store(wbc, wbd);
-                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                    sl.lc_wb_store(f.wbc, wbd);
                     if (STAMP) tb = stampL();
-                    sl.lc_fill(p - 2, ld[(s + NS - 2) % NS]);
-                    sl.read_pre_lc(p + 1, (s + 1) % NI, in);
-                    sl.gathers_lc(p + 1 + R, (s + R + 1) % NI);
-                    sl.lc_load(p, ld[s]);
-                    sl.read_st_lc(p - 1, sc);
+                    sl.read_pre_lc(f.rrn, (s + 1) % NI, in);
+                    sl.gathers_lc_c(f.gchk, (s + R + 1) % NI);
+                    sl.lc_dma(f.ldc);
+                    sc.md = sm.mst[sw][kl][q & 3];
+                    sc.chk = f.stchk;
                     if (STAMP) t1 = t2 = stampL();
                     if (fair) __builtin_amdgcn_s_setprio(0);
                     sl.template pre<false, ET, MP2>(p + 1, in, sn);
@@ -1120,11 +1159,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                             sl.template post<false, ET>(p - 1, xr, sp, sl.rec(p - 1));
                     }
                     sl.lc_wb_store(wbc, wbd);
-                    {   // periods 0, 1: the prologue's loads, listed in the tables of windows nw-2, nw-1
-                        const uint32_t *fl = p >= 2 ? sm.tab[(p - 2) & (TQ - 1)].loads : gtab[a.nw - 2 + p].loads;
-                        const uint32_t code = sl.lc_code(fl);
-                        if (code != LC_NONE) sm.cache[code >> 16][q] = ld[(s + NS - 2) % NS];
-                    }
                     if (STAMP) t1 = t2 = t3 = stampL();
                     if (dpr) {
                         sl.read_pre_lc(p + 1, (s + 1) % NI, in);
@@ -1134,11 +1168,12 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                             sl.template pre<false, ET>(p + 1, in, sn);
                         sl.gathers_lc(p + 1 + R, (s + R + 1) % NI);
                     }
-                    sl.lc_load(p, ld[s]);
+                    sl.lc_dma(sl.lc_code(sm.tab[p & (TQ - 1)].loads));
                     if (dpo) {
                         sl.read_st_lc(p - 1, sc);
                         sc_tl = uA == a.tail;
                     }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
             } else if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
@@ -1187,10 +1222,13 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     sl.gathers(pi, (s + R + 1) % NI);
                 }
             }
+            if constexpr (LC) {   // the previous period's line loads and gathers have landed (see above)
+                if (fast) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+            }
             if (STAMP) {
                 const unsigned long long t5 = stampL();
                 sA += t5 - tx;
-                if (fast && LC) {   // post | writeback + wait for the loads | cache fill, LDS reads, issue | pre
+                if (fast && LC) {   // post | writeback store | LDS reads, issue | pre (the rest: the end wait)
                     sP[0] += ta - tx;
                     sP[1] += tb - ta;
                     sP[2] += t1 - tb;
@@ -1277,8 +1315,8 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s, bool l
         if (w == CHW)
             fprintf(stderr, "  chain %d: busy %.0f steps %.0f\n", w, x[0], x[1]);
         else if (lc)
-            fprintf(stderr, "  slab %d: busy %.0f | post %.0f wb+vmcnt %.0f fill+lds+issue %.0f pre %.0f\n", w, x[0],
-                    x[1], x[2], x[3], x[4]);
+            fprintf(stderr, "  slab %d: busy %.0f | post %.0f wb %.0f lds+issue %.0f pre %.0f end-wait %.0f\n", w, x[0],
+                    x[1], x[2], x[3], x[4], x[0] - x[1] - x[2] - x[3] - x[4]);
         else
             fprintf(stderr, "  slab %d: busy %.0f | vmcnt %.0f %s %.0f %s %.0f mem %.0f\n", w, x[0], x[1],
                     w == 0 ? "post" : "pre", x[2], w == 0 ? "pre" : "post", x[3], x[0] - x[1] - x[2] - x[3]);
@@ -1440,7 +1478,7 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
                     // entries 0 .. 5 always present (one per slab wave: every wave
                     // issues each line operation every period, for the vmcnt counts)
                     const uint32_t l = lp.loads[(size_t)u * LC_LMAX + i], b = lp.wbs[(size_t)u * LC_LMAX + i];
-                    W.loads[i] = (l == LC_NONE && i < 6) ? sink : l;
+                    W.loads[i] = l == LC_NONE ? sink : l;   // every entry: 8 line loads per wave and period
                     W.wbs[i] = (b == LC_NONE && i < 6) ? sink : b;
                 }
             }

@@ -16,10 +16,11 @@
 //   * window u's pre reads its records' entries 0..X-1 and D0-1 in period
 //     u - 1, its post writes entries 0..X (the tail also D0-1) in period u + 1;
 //   * a line instance (its accesses, split where two are >= LC_GAP periods
-//     apart) is loaded (global -> VGPRs) in period f - 3, written to its cache
-//     slot in period f - 1 (f = first access), and -- if written to -- written
-//     back (slot -> VGPRs -> global) in period e + 1 (e = last access); the
-//     slot is free again from the next period;
+//     apart) is loaded straight into its cache slot (LDS-DMA) in period f - 2
+//     (f = first access; the loading wave waits for it at the end of period
+//     f - 1), so the slot is held from period f - 2; if written to, it is
+//     written back (slot -> VGPRs -> global) in period e + 1 (e = last
+//     access); the slot is free again from the next period;
 //   * a line written back is loaded again >= 2 periods after its store (the
 //     store and the load come from the same CU, in order);
 //   * at most LC_LMAX loads and LC_LMAX writebacks per period (6 slab waves x 8
@@ -118,8 +119,8 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     }
     for (Inst &I : in) {
         if (I.whole) continue;
-        I.tl = I.f - 3;
-        I.tw = I.f - 1;
+        I.tl = I.f - 2;
+        I.tw = I.f - 2;
         I.te = I.dirty ? I.e + 1 : I.e;   // the writeback's slot read is in period e + 1
     }
     // per-period capacity: move loads earlier / writebacks later where a period
@@ -296,7 +297,10 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
 // prologue on) with a model of the cache: every access must find its line in
 // the slot the record names, slots are loaded only when free, lines are
 // loaded >= 2 periods after their previous writeback, and at the end of every
-// iteration the epilogue leaves every dirty line written back.  0 = valid.
+// iteration the epilogue leaves every dirty line written back.  A load of
+// period p may land at any time in periods p and p + 1, so the model puts the
+// new line in its slot at the start of period p (an access to the slot's old
+// line in period p or later fails).  0 = valid.
 int lc_check_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int tail, int n, const LcPlan &o)
 {
     const int X = D0 - 2, NS = o.slots;
@@ -310,13 +314,6 @@ int lc_check_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     for (uint32_t c : o.pro) {
         if (slot_of(c) <= 0 || slot_of(c) >= NS || holds[slot_of(c)] != -1) return -2;
         holds[slot_of(c)] = line_of(c);
-    }
-    std::vector<std::vector<uint32_t>> staged(3);   // loads in flight, by issue period % 3
-    std::vector<int> staged_at(3, -100);
-    for (int p = -2; p <= -1; p++) {   // the prologue issues the loads of periods -2, -1
-        staged[cmod(p, 3)].assign(o.loads.begin() + (size_t)cmod(p, nw) * LC_LMAX,
-                                  o.loads.begin() + (size_t)(cmod(p, nw) + 1) * LC_LMAX);
-        staged_at[cmod(p, 3)] = p;
     }
     auto rec_at = [&](int u, int k) { return &tab[((size_t)u * S + k) * recw]; };
     auto access = [&](int u, int k, int j, bool wr) -> bool {
@@ -337,6 +334,19 @@ int lc_check_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     }
     for (int p = 0; p <= G; p++) {
         const int pm = cmod(p, nw);
+        // (I) the loads of period p claim their slots
+        for (int i = 0; i < LC_LMAX; i++) {
+            const uint32_t c = o.loads[(size_t)pm * LC_LMAX + i];
+            if (c == LC_NONE) continue;
+            const int s = slot_of(c);
+            if (s <= 0 || s >= NS) return -6;
+            if (holds[s] != -1 && dirty[s]) return -6;        // would overwrite unsaved data
+            if (p - last_store[line_of(c)] < 2) return -8;   // its last writeback too recent
+            for (int t = 1; t < NS; t++)                     // a dirty copy still cached: the load is stale
+                if (holds[t] == (int64_t)line_of(c) && dirty[t]) return -11;
+            holds[s] = line_of(c);
+            dirty[s] = 0;
+        }
         // (A, D) writebacks: slot read, store (its line must be the one held)
         for (int i = 0; i < LC_LMAX; i++) {
             const uint32_t c = o.wbs[(size_t)pm * LC_LMAX + i];
@@ -354,20 +364,8 @@ int lc_check_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
                     if (!access(p - 1, k, j, true)) return -5;
                 if (cmod(p - 1, nw) == tail && !access(p - 1, k, D0 - 1, true)) return -5;
             }
-        // slots whose instance ended without a writeback (clean) are free
-        // again: the checker frees a clean slot once no later access of the
-        // window range needs it -- approximated by freeing on the next write
-        // (F) slot writes of the loads issued in period p-2
-        if (staged_at[cmod(p - 2, 3)] == p - 2) {
-            for (uint32_t c : staged[cmod(p - 2, 3)]) {
-                if (c == LC_NONE) continue;
-                const int s = slot_of(c);
-                if (s <= 0 || s >= NS) return -6;
-                if (holds[s] != -1 && dirty[s]) return -6;   // would overwrite unsaved data
-                holds[s] = line_of(c);
-                dirty[s] = 0;
-            }
-        }
+        // (slots whose instance ended without a writeback, clean, are taken
+        // over by the next load into them)
         // (G) pre of window p+1
         if (p + 1 < G)
             for (int k = 0; k < S; k++) {
@@ -375,16 +373,6 @@ int lc_check_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
                     if (!access(p + 1, k, j, false)) return -7;
                 if (!access(p + 1, k, D0 - 1, false)) return -7;
             }
-        // (I) loads of period p
-        staged[cmod(p, 3)].assign(o.loads.begin() + (size_t)pm * LC_LMAX,
-                                  o.loads.begin() + (size_t)(pm + 1) * LC_LMAX);
-        staged_at[cmod(p, 3)] = p;
-        for (uint32_t c : staged[cmod(p, 3)]) {
-            if (c == LC_NONE) continue;
-            if (p - last_store[line_of(c)] < 2) return -8;   // its last writeback too recent
-            for (int s = 1; s < NS; s++)                     // a dirty copy still cached: the load is stale
-                if (holds[s] == (int64_t)line_of(c) && dirty[s]) return -11;
-        }
     }
     // epilogue: every dirty slot must be in the list
     std::vector<char> flushed(NS, 0);
