@@ -133,13 +133,6 @@ int ldpc_code_coop_plan(const ldpc_code *h, int S, int R, int *first, int *count
  * apart; reads written dist+1 .. R+dist windows earlier are forwarded). */
 int ldpc_code_coop_plan_dist(const ldpc_code *h, int S, int R, int dist, int *first, int *count, int max_windows,
                              int *n_windows, int *tail, int *n_fwd);
-/* LDS line-cache plan of coop3 (kernel 8) for this code: status 0 when the
- * plan exists within max_slots 128-B cache lines and passed its self-check;
- * slots used, the most line loads / writebacks in one period, line
- * instances per iteration, lines resident at a segment start / dirty at its
- * end. */
-int ldpc_code_coop3_lc_info(const ldpc_code *h, int max_slots, int *status, int *slots, int *max_loads,
-                            int *max_wbs, int *instances, int *n_pro, int *n_epi);
 /* Layer plan of the LDS-resident kernel (kernel 7): maximal runs of
  * consecutive same-group checks sharing no variable (one block row of a
  * quasi-cyclic code).  lds_i8 / lds_f32: 1 if a codeword's state fits the

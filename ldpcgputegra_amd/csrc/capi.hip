@@ -387,17 +387,9 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     // on the same few L2 channels.  Measured (DVB-S2 r1/2, 4096 cw, 50 it,
     // coop3): pitch 4096 57.6 ms, 4160 / 4224 49.7 / 49.6 ms, 4352 50.4,
     // 4608 52.7, 5120 57.2
-    // coop3 with LDPC_COOP3_GROUPED=1: V in the grouped layout [stride / 16][N + 1][16]
-    // (a workgroup's rows contiguous) -- not with the per-iteration
-    // early-termination helpers, which address V[row][pitch]
-    // (the line cache, when coop3 has one, needs it)
-    const bool vpriv = kern == 8 && !is_float &&
-                       (c->coop3.lc_valid || getenv_int("LDPC_COOP3_GROUPED", 0) != 0) &&
-                       (!p->early_term || coop3_et_in_kernel(c->coop3, h->n));
-    const int vpad = (kern == 8 || kern == 5) && !vpriv ? std::max(0, getenv_int("LDPC_VPITCH_PAD", 64)) / 64 * 64 : 0;
+    const int vpad = (kern == 8 || kern == 5) ? std::max(0, getenv_int("LDPC_VPITCH_PAD", 64)) / 64 * 64 : 0;
     const int vpitch = stride + vpad;
-    // grouped layout: [stride / 16][n + 8][16] (the sink row n and the rest of its 128-B line)
-    const size_t v_rows = vpriv ? (size_t)h->n + 8 : (size_t)h->n + 1;
+    const size_t v_rows = (size_t)h->n + 1;   // row n: the coop kernels' sink row
     if ((rc = ensure(&sc.d_V, &sc.V_bytes, v_rows * vpitch * esz)) != LDPC_OK) return rc;
     if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_need)) != LDPC_OK) return rc;
     // early termination: live u8 | bad u32 | iterations used i32 (when the caller passed none)
@@ -415,8 +407,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         if (launch_interleave_f32((const float *)d_llr, (float *)sc.d_V, h->n, batch, vpitch, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
     } else {
-        if (vpriv ? launch_interleave_i8_grouped((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, stride, s)
-                  : launch_interleave_i8((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, vpitch, s))
+        if (launch_interleave_i8((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, vpitch, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
     }
     DecodeLaunch L{};
@@ -425,7 +416,6 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     if (kern == 8) L.P = (int8_t *)sc.d_msg + msg_zero;
     L.stride = stride;
     L.vpitch = vpitch;
-    L.vpriv = vpriv;
     L.batch = batch;
     L.iters = n_iter;
     L.is_float = is_float;
@@ -473,8 +463,6 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     if (d_hard || d_soft) {
         int r2 = is_float ? launch_deinterleave_f32((const float *)sc.d_V, d_hard, (float *)d_soft, h->n, batch,
                                                     vpitch, s)
-                 : vpriv  ? launch_deinterleave_i8_grouped((const int8_t *)sc.d_V, d_hard, (int8_t *)d_soft, h->n,
-                                                           batch, s)
                           : launch_deinterleave_i8((const int8_t *)sc.d_V, d_hard, (int8_t *)d_soft, h->n,
                                                    batch, vpitch, s);
         if (r2) return ldpc_set_error(LDPC_EDEVICE, "deinterleave: %s", hipGetErrorString(hipGetLastError()));

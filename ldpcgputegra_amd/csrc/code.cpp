@@ -356,30 +356,6 @@ extern "C" int ldpc_code_coop_plan_dist(const ldpc_code *h, int S, int R, int di
     return LDPC_OK;
 }
 
-// the LDS line-cache plan of coop3 (linecache.cpp) for this code, from the
-// coop3 schedule at its default geometry (6 slab waves): status 0 = built and
-// self-checked (replayed over three iterations), < 0 = no plan (the cache
-// would need more than max_slots lines or a period more than 48 loads)
-extern "C" int ldpc_code_coop3_lc_info(const ldpc_code *h, int max_slots, int *status, int *slots, int *max_loads,
-                                       int *max_wbs, int *instances, int *n_pro, int *n_epi)
-{
-    if (!h || !status) return ldpc_set_error(LDPC_EINVAL, "lc info args");
-    Coop3Host ho;
-    const int rc = coop3_plan_host(h, 6, 2, ho);
-    if (rc < 0) return rc;
-    *status = -100;
-    if (rc > 0) return LDPC_OK;   // no coop3 schedule
-    LcPlan lp;
-    *status = lc_build_plan(ho.pl.tab, ho.recw, ho.nw, ho.S, ho.d0, ho.pl.tail, h->n, max_slots, lp);
-    if (slots) *slots = lp.slots;
-    if (max_loads) *max_loads = lp.max_loads;
-    if (max_wbs) *max_wbs = lp.max_wbs;
-    if (instances) *instances = lp.instances;
-    if (n_pro) *n_pro = (int)lp.pro.size();
-    if (n_epi) *n_epi = (int)lp.epi.size();
-    return LDPC_OK;
-}
-
 extern "C" void ldpc_code_destroy(ldpc_code *h) { delete h; }
 
 // ---------------------------------------------------------------- channel

@@ -13,10 +13,6 @@ struct CoopCode {
     int x0;          // coop3: V row of check 0's x edge (the chain's first input)
     int m0, d1;      // coop3: checks of degree d0 (group 0), degree of the later group
     uint32_t *d_tab; // [nw][S][recw]
-    // coop3's LDS line cache (linecache.cpp): window tables [nw] (LcWin), the
-    // lines resident at a segment start / dirty at its end; lc_valid = 0: none
-    int lc_valid, lc_slots, n_pro, n_epi;
-    uint32_t *d_lctab, *d_lcpro, *d_lcepi;
 };
 
 bool coop_params_ok(const ldpc_params *p);
@@ -73,20 +69,3 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o);
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
 // early termination inside the coop3 launch (else per-iteration launches + V snapshots)
 bool coop3_et_in_kernel(const CoopCode &cc, int n);
-
-// ---- coop3's LDS line cache (linecache.cpp) ----
-constexpr int LC_LMAX = 48;                  // line loads / writebacks per period (6 slab waves x 8 lines)
-constexpr int LC_GAP = 6;                    // a line stays cached across gaps shorter than this (periods)
-constexpr uint32_t LC_NONE = 0xFFFFFFFFu;    // empty list entry
-struct LcPlan {
-    int slots = 0;                   // cache slots of 128 B (slot 0: the sink line)
-    int max_loads = 0, max_wbs = 0, instances = 0;
-    std::vector<uint16_t> rowoff;    // [nw][S][8]: cache row (slot * 8 + var % 8) of record entries 0..D0-1
-    std::vector<uint32_t> loads;     // [nw][LC_LMAX]: line | slot << 16 loaded (issued) in period u
-    std::vector<uint32_t> wbs;       // [nw][LC_LMAX]: written back in period u
-    std::vector<uint32_t> pro, epi;  // resident before period -1 / dirty after the last period
-};
-// tab: coop3's permuted slot records [nw][S][recw]; 0 = plan built and self-checked
-int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int tail, int n, int max_slots,
-                  LcPlan &o);
-int lc_check_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int tail, int n, const LcPlan &o);

@@ -962,9 +962,6 @@ int coop_upload(const ldpc_code *h, CoopCode *cc)
 void coop_free(CoopCode *cc)
 {
     (void)hipFree(cc->d_tab);
-    (void)hipFree(cc->d_lctab);
-    (void)hipFree(cc->d_lcpro);
-    (void)hipFree(cc->d_lcepi);
     *cc = CoopCode{};
 }
 

@@ -69,7 +69,22 @@ constexpr int NFW = (X + 1) / 2;    // forwarding-code dwords per record
 constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;
 constexpr int DPER = 3;             // a window table's LDS-DMA is waited for DPER periods after its issue
 constexpr int TQ = 16;              // window-table slots in LDS
-constexpr int STG_RING = 8192;      // bytes per forwarding-ring slot (power of two: see fwd_code3)
+constexpr int STG_RING = 8192;      // stage bytes per ring slot
+constexpr int RING = 16384;         // bytes per ring slot: stage [0, STG_RING), slab waves' input records after
+constexpr int RING_SH = 14;         // log2(RING): a read code + (g << RING_SH) addresses window g's ring slot
+constexpr uint32_t SEL0 = 0x010d000du;   // v_perm selector: u16 [b0 b1] -> R pair
+
+// one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot)
+struct In3 {
+    uint4 a[8][8];                    // [0..5][slot] V rows (info edges, record entry D0-1), [6..7][slot] message
+                                      // 0..31 B
+    uint4 pad[4];                     // (rows 6, 7 and b[0], b[1] in different banks)
+    uint4 b[2][8];                    // [0..1][slot] message 32..63 B
+};                                    // (entry-major: the 8 slots of one read are in different banks)
+constexpr uint32_t IN_B3 = sizeof(uint4) * (8 * 8 + 4);   // byte offset of In3::b
+// read code of info edge j of slot (w, kl) when it is not forwarded: its V row
+// piece in the window's own input record (ring slot delta 0)
+constexpr uint32_t in_code3(int w, int kl, int j) { return (uint32_t)(STG_RING + w * (int)sizeof(In3) + j * 128 + kl * 16); }
 
 template <int WS, int R>
 struct Cfg {
@@ -93,55 +108,25 @@ template <int WS, int R>
 struct alignas(16) Smem3 {
     using CF = Cfg<WS, R>;
     static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
-    uint4 stg[NR][STG_RING / 16];     // new V of a window, [record entry * (S + 1) + slot] x 16 codewords (int8,
-                                      // entries padded: the stores' reads of 8 entries are conflict-free): the
-                                      // V stores' staging and the forwarding ring (ring slot g % NR, 8 KB apart
-                                      // so that a forwarding code + (g << 13) addresses its entry)
+    // ring slot g % 4 (at LDS address 0, RING bytes apart so that a read code
+    // + (g << RING_SH) addresses it):
+    // * [0, STG_RING): the stage -- new V of window g, [record entry * (S + 1) +
+    //   slot] x 16 codewords (int8, entries padded: the stores' reads of 8
+    //   entries are conflict-free): the V stores' staging and the forwarding ring;
+    // * [STG_RING, ...): the slab waves' input records of window g (In3, LDS-DMA).
+    // Every info-edge V read of a pre is one ds_read_u16 at its read code: the
+    // own input record, or the stage of the window that wrote the value
+    uint4 ring[NR][RING / 16];
     uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
     uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post)
-    struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
-        uint4 a[8][8];                //   [0..5][slot] V rows (info edges, record entry D0-1), [6..7][slot] message
-                                      //   0..31 B
-        uint4 pad[4];                 //   (rows 6, 7 and b[0], b[1] in different banks)
-        uint4 b[2][8];                //   [0..1][slot] message 32..63 B
-    } in[WS][NI];                     // (entry-major: the 8 slots of one read are in different banks)
-    static constexpr uint32_t IN_B = sizeof(uint4) * (8 * 8 + 4);   // byte offset of In::b
+    static constexpr uint32_t IN_B = IN_B3;
     uint4 mst[WS][8][4];              // new messages of a window per slab wave, [slot] x 64 B
-    uint4 et_spare[320];              // early termination: between segments the whole struct holds the
-                                      // hard bits of every variable (u16 x 64800 for DVB-S2; one
-                                      // workgroup per CU either way)
+    // (early termination: between segments the whole struct holds the hard
+    // bits of every variable, u16 x 64800 for DVB-S2)
 };
-
-// ---- the LDS line cache (the V rows of a workgroup's codewords in whole
-// 128-B lines: linecache.cpp plans which line sits in which slot when)
-constexpr int LC_SLOTS = 800;         // cache lines (8 rows x 16 codewords each) beside the pipeline
-struct alignas(16) LcWin {            // one window's table (global [nw] array, LDS-DMA'd by the chain wave)
-    uint4 rec[48];                    // slot k: cache rows (slot * 8 + var % 8) of record entries 0..6 (u16),
-                                      // then meta16 = chain step | active << 6
-    uint16_t chk[48];                 // slot k: its check (message row; the sink row m when inactive)
-    uint32_t loads[LC_LMAX];          // lines whose load is issued in this period (line | slot << 16), entry
-    uint32_t wbs[LC_LMAX];            // li * 6 + w for lane group li of slab wave w; lines written back now
-};
-static_assert(sizeof(LcWin) % 16 == 0, "LcWin is staged in 16-B pieces");
-
-template <int WS, int R>
-struct alignas(16) Smem3LC {
-    using CF = Cfg<WS, R>;
-    static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
-    static constexpr uint32_t IN_B = 0;   // (the forwarding-ring layout's field, unused here)
-    uint4 mst[WS][8][4];              // new messages (as Smem3; first: the line loads' M0 bases, slot
-                                      // address - 128 x lane group, stay above LDS address 0)
-    uint4 cache[LC_SLOTS][8];         // the line cache (slot 0: the sink line of the inactive slots)
-    LcWin tab[TQ];                    // window tables, window g in slot g % TQ
-    uint4 cst[2][S][2][NP];           // chain constants (as Smem3)
-    uint4 xo[2][S / 8][CW];           // chain inputs (as Smem3)
-    uint4 inm[WS][NI][8][4];          // one window's old message records per slab wave ([slot] x 64 B)
-};
-static_assert(sizeof(Smem3LC<6, 2>) <= 160 * 1024, "coop3 line cache: 160 KB of LDS per workgroup");
-using Smem3LC62 = Smem3LC<6, 2>;
-static_assert(offsetof(Smem3LC62, cache) >= 7 * 128, "line loads: M0 >= 0");
+static_assert(STG_RING + 6 * sizeof(In3) <= RING && 8 * 49 * 16 <= STG_RING, "ring slot layout");
 
 struct Coop3Args {
     int8_t *V;                        // V[n + 1][pitch]; row n is the sink of inactive slots
@@ -159,9 +144,7 @@ struct Coop3Args {
     int iters, batch, m0, d1;
     int pitch, G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
     uint32_t nmsf;                    // NMS factor per half (value form)
-    size_t wgoff;                     // bytes between two codeword groups' V (see DecodeLaunch::vpriv)
-    const uint32_t *lcpro, *lcepi;    // line cache: lines resident before period -1 / dirty after the last
-    int npro, nepi;
+    size_t wgoff;                     // bytes between two codeword groups' V (16)
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
 };
 
@@ -194,10 +177,10 @@ LDPC_DEV uint32_t pk_shl5(uint32_t a) { return us(sv(a) << (short)5); }
 
 // what a period reads from LDS, issued together at its start
 struct PreIn {
-    uint32_t v[D0 - 1];               // raw V dwords (info edges, entry D0-1)
+    uint32_t v[D0 - 1];               // v[X]: the o edge's V pair (raw u16, entry D0-1)
     uint32_t ma, mb;                  // old message record of this pair
     uint4 mf;                         // record words D0 .. D0+3: meta, forwarding codes (read a period early)
-    uint32_t fv[X];                   // forwarded V pairs (raw u16) of the info edges with a forwarding code
+    unsigned short fv[X];             // V pairs (raw u16) of the info edges, at their read codes
 };
 struct StIn {                         // the stores of window p-2
     uint4 vd, md;                     // staged V row piece (16 codewords), message piece
@@ -207,9 +190,9 @@ struct PfIn {                         // the LDS-DMA gathers of window p+1+R
     uint32_t rv, chk2;
 };
 
-template <int WS, int R, bool NMS = false, bool LC = false>
+template <int WS, int R, bool NMS = false>
 struct Slab3 {
-    using SM = std::conditional_t<LC, Smem3LC<WS, R>, Smem3<WS, R>>;
+    using SM = Smem3<WS, R>;
     static constexpr int S = SM::S, NR = SM::NR;
     SM &sm;
     const Coop3Args &a;
@@ -217,133 +200,30 @@ struct Slab3 {
     uint32_t vsm;                     //   q >= X go to the parity rows' own layout P, see Coop3Args)
     i32x4 mr;                         // message rows in 16-B units
     int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
-    uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
-    uint32_t fsel;                    // ... of a forwarded u16 (0x050d040d, in a VGPR)
     PkK K;
+    PkBits mb;                        // message-code bits per edge (SGPRs)
     uint32_t fk;                      // NMS factor per half (value form)
     // per-lane constants of the LDS-DMA gathers (lane (kl, j): j < 6 a V row, j >= 6 a message piece)
     const char *g1base, *g2base;
     uint32_t g1mul, g1mask, recsel;
-    uint32_t vrd, mrd;                // byte offsets of this lane's V dword / message pair in an In record
+    uint32_t vrd, mrd;                // byte offsets of this lane's V u16 (entry 0) / message pair in an In3 record
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
-    const char *lcV = nullptr;        // LC: this group's V rows (grouped layout), lines of 128 B
-
-    // ---- line cache (LC)
-    LDPC_DEV uint4 rec(int g) const { return sm.tab[g & (TQ - 1)].rec[k]; }
-    LDPC_DEV static uint32_t row_of(const uint4 &r, int j)   // cache row of record entry j
-    {
-        const uint32_t x = j < 2 ? r.x : j < 4 ? r.y : j < 6 ? r.z : r.w;
-        return (j & 1) ? x >> 16 : x & 0xFFFFu;
-    }
-    LDPC_DEV const char *cache_b() const { return (const char *)&sm.cache[0][0]; }
-    // window g's V dwords (this pair's 2 bytes in each) and old messages; the
-    // meta word in coop3's form (active, chain step), no forwarding codes
-    LDPC_DEV void read_pre_lc(int g, int ib, PreIn &in) const
-    {
-        const uint4 rr = rec(g);
-        const char *cb = cache_b() + 4 * (q >> 1);
-#pragma unroll
-        for (int j = 0; j < X; j++) in.v[j] = *(const uint32_t *)(cb + row_of(rr, j) * 16);
-        in.v[X] = *(const uint32_t *)(cb + row_of(rr, D0 - 1) * 16);
-        const uint2 mm = *(const uint2 *)((const char *)&sm.inm[w][ib][kl][0] + 8 * q);
-        in.ma = mm.x;
-        in.mb = mm.y;
-        const uint32_t m16 = rr.w >> 16;
-        in.mf = make_uint4(((m16 & 64u) ? COOP_M_ACT : 0u) | (m16 & 63u) << STEP_SHIFT, 0u, 0u, 0u);
-    }
-    // old messages of window g: lanes 0..31 = (slot, 16-B piece) of the wave's 8 checks
-    LDPC_DEV void gathers_lc(int g, int ib) const
-    {
-        if (lane < 32) {
-            const uint32_t c = sm.tab[g & (TQ - 1)].chk[8 * w + (lane >> 2)];
-            dma16(g2base + (size_t)c * MREC + (lane & 3) * 16, (uint32_t)(uintptr_t)&sm.inm[w][ib][0][0]);
-        }
-    }
-    LDPC_DEV void read_st_lc(int g, StIn &in) const
-    {
-        in.md = sm.mst[w][kl][q & 3];
-        in.chk = sm.tab[g & (TQ - 1)].chk[k];
-    }
-    LDPC_DEV void stores_lc(const StIn &in) const
-    {
-        if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
-    }
-    // line lists: lane group li = lane >> 3 of slab wave w handles entry li * WS + w
-    // (16-B piece q of the line); the host fills entries 0..WS-1 of every list
-    // (sink line where a period has fewer), so every wave issues each line
-    // operation every period and the vmcnt counts stay exact
-    LDPC_DEV uint32_t lc_code(const uint32_t *list) const { return list[(lane >> 3) * WS + w]; }
-    LDPC_DEV void lc_wb_read(int p, uint32_t &code, uint4 &d) const
-    {
-        code = lc_code(sm.tab[p & (TQ - 1)].wbs);
-        if (code != LC_NONE) d = sm.cache[code >> 16][q];
-    }
-    LDPC_DEV void lc_wb_store(uint32_t code, const uint4 &d) const
-    {
-        if (code != LC_NONE) *(uint4 *)(lcV + (size_t)(code & 0xFFFFu) * 128 + q * 16) = d;
-    }
-    // this period's line loads, straight into their slots by LDS-DMA: lane
-    // group li (8 lanes, one 128-B line) of the wave per instruction, M0 =
-    // slot address - 128 li (the DMA writes lane l's 16 B at M0 + 16 l).  Every
-    // list entry is a line (the host pads with the sink line, slot 0), so each
-    // wave issues exactly 8 per period and the vmcnt counts stay exact; the
-    // compiler neither sees nor waits for them (no VGPR destination)
-    LDPC_DEV void lc_dma(uint32_t code) const
-    {
-        const char *ga = lcV + (size_t)(code & 0xFFFFu) * 128 + q * 16;
-        const uint32_t m0v = (uint32_t)(uintptr_t)cache_b() + (code >> 16) * 128u - (uint32_t)kl * 128u;
-#pragma unroll
-        for (int li = 0; li < 8; li++) {
-            const uint32_t m = __builtin_amdgcn_readlane(m0v, 8 * li);
-            if (kl == li) dma16(ga, m);
-        }
-    }
-    // fast periods: every table word of period p read in one batch at its
-    // start (one exposed LDS latency, shared with the chain outputs' read,
-    // instead of a dependent round trip before each line / gather operation)
-    struct LcPf {
-        uint32_t wbc, ldc, gchk, stchk;
-        uint4 rrn, rrp;   // records of windows p+1 (pre) and p-1 (post)
-    };
-    LDPC_DEV void lc_prefetch(int p, LcPf &f) const
-    {
-        f.wbc = lc_code(sm.tab[p & (TQ - 1)].wbs);
-        f.ldc = lc_code(sm.tab[p & (TQ - 1)].loads);
-        f.rrn = rec(p + 1);
-        f.rrp = rec(p - 1);
-        f.gchk = sm.tab[(p + 1 + R) & (TQ - 1)].chk[8 * w + ((lane >> 2) & 7)];
-        f.stchk = sm.tab[(p - 1) & (TQ - 1)].chk[k];
-    }
-    LDPC_DEV void lc_line_read(uint32_t code, uint4 &d) const
-    {
-        if (code != LC_NONE) d = sm.cache[code >> 16][q];
-    }
-    LDPC_DEV void read_pre_lc(const uint4 &rr, int ib, PreIn &in) const
-    {
-        const char *cb = cache_b() + 4 * (q >> 1);
-#pragma unroll
-        for (int j = 0; j < X; j++) in.v[j] = *(const uint32_t *)(cb + row_of(rr, j) * 16);
-        in.v[X] = *(const uint32_t *)(cb + row_of(rr, D0 - 1) * 16);
-        const uint2 mm = *(const uint2 *)((const char *)&sm.inm[w][ib][kl][0] + 8 * q);
-        in.ma = mm.x;
-        in.mb = mm.y;
-        const uint32_t m16 = rr.w >> 16;
-        in.mf = make_uint4(((m16 & 64u) ? COOP_M_ACT : 0u) | (m16 & 63u) << STEP_SHIFT, 0u, 0u, 0u);
-    }
-    LDPC_DEV void gathers_lc_c(uint32_t c, int ib) const
-    {
-        if (lane < 32) dma16(g2base + (size_t)c * MREC + (lane & 3) * 16, (uint32_t)(uintptr_t)&sm.inm[w][ib][0][0]);
-    }
 
     // ---- reads
-    // in.mf = mfc (window g's codes, read in the previous period); mfn <- window g+1's
-    LDPC_DEV void read_pre(int g, int ib, PreIn &in, const uint4 &mfc, uint4 &mfn) const
+    LDPC_DEV char *ringb(int g) const { return (char *)&sm.ring[g & (NR - 1)][0]; }
+    LDPC_DEV uint32_t in_lds(int g) const   // this wave's input record of window g (LDS address)
     {
-        const char *inb = (const char *)&sm.in[w][ib];
-#pragma unroll
-        for (int j = 0; j < D0 - 1; j++) in.v[j] = *(const uint32_t *)(inb + vrd + 128 * j);
+        return (uint32_t)(uintptr_t)(ringb(g) + STG_RING) + (uint32_t)w * (uint32_t)sizeof(In3);
+    }
+    // in.mf = mfc (window g's codes, read in the previous period); mfn <- window
+    // g+1's.  The o edge's row (record entry D0-1, never forwarded) and the old
+    // messages from the input record; the info edges by fwd_read
+    LDPC_DEV void read_pre(int g, int, PreIn &in, const uint4 &mfc, uint4 &mfn) const
+    {
+        const char *inb = ringb(g) + STG_RING + w * sizeof(In3);
+        in.v[X] = *(const unsigned short *)(inb + vrd + 128 * X);
         const uint2 mm = *(const uint2 *)(inb + mrd);
         in.ma = mm.x;
         in.mb = mm.y;
@@ -351,24 +231,23 @@ struct Slab3 {
         mfn = read_mf(g + 1);
     }
     LDPC_DEV uint4 read_mf(int g) const { return *(const uint4 *)&sm.tab[g & (TQ - 1)][k][D0]; }
-    // forwarded values of window g's info edges: code j (16 bits, fwd_code3)
-    // = ((-dW) mod 4) << 13 | stage offset | near << 1 | use; code + (g << 13)
-    // carries ring slot (g - dW) mod 4 in bits 13-14.  Unused codes read
-    // ring offset 0 (ignored).  Branch-free: 2 VALU + 1 ds_read_u16 per edge.
+    // V pairs (u16) of window g's info edges: read code j (16 bits, fwd_code3 /
+    // in_code3) = ((-dW) mod 4) << RING_SH | offset in the ring slot | near << 1 |
+    // forwarded; code + (g << RING_SH) carries ring slot (g - dW) mod 4 (dW = 0:
+    // the own input record).  Branch-free: 2 VALU + 1 ds_read_u16 per edge
     LDPC_DEV void fwd_read(int g, PreIn &in) const
     {
-        const char *sbase = (const char *)&sm.stg[0][0];
-        const uint32_t gs = (uint32_t)__builtin_amdgcn_readfirstlane(g << 13), q2 = 2u * (uint32_t)q;
+        const uint32_t gs = (uint32_t)__builtin_amdgcn_readfirstlane(g << RING_SH), q2 = 2u * (uint32_t)q;
         const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
 #pragma unroll
         for (int j = 0; j < X; j++) {
             const uint32_t code = (j & 1) ? fw[j >> 1] >> 16 : fw[j >> 1] & 0xFFFFu;
-            in.fv[j] = *(const unsigned short *)(sbase + (((code + gs) & 0x7FF0u) | q2));
+            in.fv[j] = *(const unsigned short *)(ringb(0) + (((code + gs) & (uint32_t)(RING * NR - 16)) | q2));
         }
     }
     LDPC_DEV void read_st(int g, StIn &in) const
     {
-        in.vd = sm.stg[g % NR][q * (S + 1) + k];
+        in.vd = ((const uint4 *)ringb(g))[q * (S + 1) + k];
         in.md = sm.mst[w][kl][q & 3];
         in.row = sm.tab[g & (TQ - 1)][k][q];
         in.chk = sm.tab[g & (TQ - 1)][k][D0] & COOP_CHK_MASK;
@@ -393,17 +272,18 @@ struct Slab3 {
         if (q < (tl ? D0 : D0 - 1)) *(uint4 *)(vsb + (size_t)in.row * vsm) = in.vd;
         if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
     }
-    LDPC_DEV void gathers(const PfIn &in, int ib) const
+    // window g's gathers into this wave's input record (ring slot g % 4)
+    LDPC_DEV void gathers(const PfIn &in, int g) const
     {
-        static_assert(offsetof(typename SM::In, b) == SM::IN_B, "In layout");
-        const uint32_t base = (uint32_t)(uintptr_t)&sm.in[w][ib];
+        static_assert(offsetof(In3, b) == IN_B3, "In layout");
+        const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane(in_lds(g));
         dma16(g1base + (size_t)in.rv * g1mul, base);
-        if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + SM::IN_B);
+        if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + IN_B3);
     }
 
-    // the first windows of the decode: a code whose source window precedes
-    // window 0 (g < dW) is not used
-    LDPC_DEV static void mask_early(int g, uint4 &mf)
+    // the first windows of the decode: a forwarded code whose source window
+    // precedes window 0 (g < dW) reads the V row from the input record instead
+    LDPC_DEV void mask_early(int g, uint4 &mf) const
     {
         uint32_t *fw = &mf.y;
 #pragma unroll
@@ -411,8 +291,9 @@ struct Slab3 {
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const uint32_t code = (fw[i] >> (16 * h)) & 0xFFFFu;
-                const int dw = (int)(((0u - (code >> 13) - 2u) & 3u) + 2u);
-                if ((code & 1u) && g < dw) fw[i] &= ~(1u << (16 * h));
+                const int dw = (int)(((0u - (code >> RING_SH) - 2u) & 3u) + 2u);
+                if (2 * i + h < X && (code & 1u) && g < dw)
+                    fw[i] = (fw[i] & ~(0xFFFFu << (16 * h))) | in_code3(w, kl, 2 * i + h) << (16 * h);
             }
     }
 
@@ -423,19 +304,10 @@ struct Slab3 {
         constexpr bool FZ = FZ_;
         const uint32_t meta = in.mf.x;
         uint32_t v[D0 - 1];
-        // V pair of edge j: this pair's two bytes of the loaded V dword, or the
-        // forwarded u16 (selector 0x050d040d: bytes 0, 1 of in.fv[j] -> R pair)
-        const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
+        // V pair of edge j: the u16 its read code addressed (SEL0: bytes 0, 1 -> R pair)
 #pragma unroll
-        for (int j = 0; j < X; j++) {
-            if constexpr (LC) {
-                v[j] = unpack_v(in.v[j], usel);
-            } else {
-                const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)fw[j >> 1], 16 * (j & 1), 1);   // 0 / -1
-                v[j] = perm(in.fv[j], in.v[j], bfi(m, fsel, usel));
-            }
-        }
-        v[X] = unpack_v(in.v[X], usel);
+        for (int j = 0; j < X; j++) v[j] = unpack_v(in.fv[j], SEL0);
+        v[X] = unpack_v(in.v[X], SEL0);
         const MsgTab t = msg_tab(in.mb);
         const uint32_t MA = in.ma, neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
@@ -446,7 +318,7 @@ struct Slab3 {
             // same edges either way, and min1 == msg_max implies cst1 == cst2)
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t, K)), neg127);
                 const uint32_t aj = abs_r(c, c510);
                 s.c[J] = c;
                 s.a[J] = aj;
@@ -456,14 +328,14 @@ struct Slab3 {
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
-            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), neg127);
+            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t, K)), neg127);
             const uint32_t ao = abs_r(cor, c510);
             s.c[X] = cor;
             s.a[X] = ao;
             s.sacc = sacc ^ cor;
             s.mn2 = pk_max(min1, pk_min(ao, min2));
             s.mn1 = pk_min(min1, ao);
-            const uint32_t mx = old_msg<X>(MA, t);
+            const uint32_t mx = old_msg<X>(MA, t, K);
             s.mx = mx;
             // chain constants in value form (R >> 8, C >> 8), both codewords at once
             COV = pk_ashr8(cor);
@@ -479,11 +351,11 @@ struct Slab3 {
                 TV = pk_ashr8(pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0));
                 EPS = EM | 0x00010001u;
                 const uint32_t base = pk_sub(COV, pk_sub(pk_ashr8(mx) ^ EM, EM));   // c_o - eps * m_x
-                A = pk_sub(base, a.offp);
-                B = pk_add(base, a.offp);
+                A = pk_sub(base, K.offp);
+                B = pk_add(base, K.offp);
             }
-            L = pk_max(pk_sub(COV, TV), VNEG127);
-            H = pk_min(pk_add(COV, TV), V127);
+            L = pk_max(pk_sub(COV, TV), K.vneg127);
+            H = pk_min(pk_add(COV, TV), K.v127);
             if constexpr (FZ) {   // converged codewords: L = H = V[p_i] as read, the step returns it
 #pragma unroll
                 for (int j = 0; j < X; j++) s.v[j] = v[j];
@@ -496,7 +368,7 @@ struct Slab3 {
             // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t, K)), neg127);
                 // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2
                 const uint32_t aj = NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510);
                 s.c[J] = c;
@@ -513,7 +385,7 @@ struct Slab3 {
             uint32_t MAn = 0;
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn, neg127);
+                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn, neg127, mb);
                 if constexpr (FZ) s.c[J] = bfi(fm, v[J], s.c[J]);   // converged codewords keep their V
             });
             s.mx = 0;
@@ -554,14 +426,13 @@ struct Slab3 {
         cp[NP] = r1;
     }
 
-    // post of window g (x inputs xr): new V pairs -> stg[g % NR], messages ->
+    // post of window g (x inputs xr): new V pairs -> the stage of ring slot g % 4, messages ->
     // mst[w]; they leave in the stores of the same period
     template <bool TL, bool FZ_ = false, int MP = -1>
-    LDPC_DEV void post(int g, uint32_t xr, const St3 &s, const uint4 &rr = uint4{}) const
+    LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
     {
         constexpr bool FZ = FZ_;
-        unsigned short *st = nullptr;                                   // [entry][..S slots..][8 pairs] u16
-        if constexpr (!LC) st = (unsigned short *)&sm.stg[g % NR][k];
+        unsigned short *st = (unsigned short *)((uint4 *)ringb(g) + k);   // [entry][..S slots..][8 pairs] u16
         constexpr int ES = (S + 1) * 8;                                 // u16 between entries
         uint32_t MA, MB;
         if constexpr (!TL) {
@@ -578,34 +449,20 @@ struct Slab3 {
             uint32_t nv[X + 1];
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
+                const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127, mb);
                 nv[J] = FZ ? perm(n, s.v[J], psel) : pack_v(n);   // FZ: pack_v of new / old per codeword
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
-            const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127);
+            const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127, mb);
             nv[X] = FZ ? perm(nx, xr, psel) : pack_v(nx);
             // the o edge: message bits only (the next check rewrites V[o] as its x edge)
-            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
+            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127, mb);
             MB = perm(k2, k1, 0x07030501u);
-            if constexpr (LC) {   // (rr: window g's record of this slot)
-                char *cb = (char *)cache_b() + 2 * q;
 #pragma unroll
-                for (int j = 0; j <= X; j++) *(unsigned short *)(cb + row_of(rr, j) * 16) = (unsigned short)nv[j];
-            } else {
-#pragma unroll
-                for (int j = 0; j <= X; j++) st[j * ES + q] = (unsigned short)nv[j];
-            }
+            for (int j = 0; j <= X; j++) st[j * ES + q] = (unsigned short)nv[j];
         } else {
-            if constexpr (LC) {
-                char *cb = (char *)cache_b() + 2 * q;
-                static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
-                    constexpr int J = decltype(jc)::value;
-                    *(unsigned short *)(cb + row_of(rr, J) * 16) = (unsigned short)pack_v(s.c[J]);
-                });
-                *(unsigned short *)(cb + row_of(rr, X) * 16) = (unsigned short)pack_v(xr);
-                *(unsigned short *)(cb + row_of(rr, D0 - 1) * 16) = (unsigned short)pack_v(s.c[X]);
-            } else {
+            {
                 static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                     constexpr int J = decltype(jc)::value;
                     st[J * ES + q] = (unsigned short)pack_v(s.c[J]);
@@ -734,14 +591,10 @@ LDPC_DEV uint32_t high_bits16(uint4 x)   // byte high bits -> 16-bit codeword ma
 // live; the snapshots are merged back at the end.  Same result as the
 // reference's per-codeword stop (oracle: syndrome after every iteration), with
 // one launch instead of one per iteration plus syndrome / snapshot kernels.
-// LC: V rows live in the LDS line cache during a segment (grouped V layout;
-// linecache.cpp's plan): no parity-row copy, no forwarding ring, the slab waves
-// move whole lines (loads, slot writes, writebacks) beside their checks.
-template <int WS, int R, bool STAMP, bool ET = false, bool NMS = false, bool LC = false>
+template <int WS, int R, bool STAMP, bool ET = false, bool NMS = false>
 __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 {
-    static_assert(!LC || WS == 6, "the line cache's window table holds 48 slots");
-    using SM = std::conditional_t<LC, Smem3LC<WS, R>, Smem3<WS, R>>;
+    using SM = Smem3<WS, R>;
     using CF = Cfg<WS, R>;
     constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U, CHW = CF::CHW, NB = CF::NB;
     __shared__ SM sm;
@@ -755,8 +608,8 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     if (!ET && a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
     // the group's parity rows -> P (consecutive checks' parity values
     // contiguous: a wave's 8 o-edge gathers / x-edge stores touch 1-2 lines,
-    // not 8), back into V at the end (LC: the grouped layout has them so)
-    if constexpr (!LC) {
+    // not 8), back into V at the end
+    {
         int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * a.wgoff;
         int8_t *ppar = a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
 #pragma unroll 8
@@ -766,7 +619,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         __syncthreads();
     }
     auto parity_out = [&]() {
-        if constexpr (LC) return;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * a.wgoff;
@@ -779,10 +631,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     __shared__ uint32_t et_sh[2];
     constexpr int NT = 64 * (WS + 1);
     const char *etV = (const char *)a.V + (size_t)wg * a.wgoff;
-    // (LC: the parity rows follow the information rows in the grouped layout, pitch 16)
-    const char *etP = LC ? etV + (size_t)a.k * 16 : (const char *)a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
+    const char *etP = (const char *)a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
     auto et_row = [&](uint32_t v) -> const uint4 * {   // V row piece of variable v (parity rows: in P)
-        return (LC || (int)v < a.k) ? (const uint4 *)(etV + (size_t)v * (size_t)a.pitch)
+        return ((int)v < a.k) ? (const uint4 *)(etV + (size_t)v * (size_t)a.pitch)
                             : (const uint4 *)(etP + (size_t)(v - (uint32_t)a.k) * 16);
     };
     if constexpr (ET) {
@@ -953,7 +804,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     if (wave == CHW) {
         // ------------------------------------------------------------ chain wave
         if (a.prio) __builtin_amdgcn_s_setprio(3);
-        constexpr int TABW = LC ? (int)(sizeof(LcWin) / 4) : S * RECW;   // words per window table
+        constexpr int TABW = S * RECW;   // words per window table
         constexpr int NCH = TABW / 4;   // 16-B chunks per window table
         constexpr int CPL = (NCH + 63) / 64;
         static_assert(CPL * DPER <= 63, "table staging");
@@ -974,7 +825,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             w4[0] = (uint32_t)(int)((const int8_t *)et_row((uint32_t)a.x0))[c] & 0xFFFFu;
             int un = KAHEAD % a.nw;
             __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 in LDS
-            if constexpr (LC) __syncthreads();   // LC: the resident lines are in the cache
             __syncthreads();   // prologue 2: constants of window 0 in LDS
             if (STAMP) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
@@ -987,7 +837,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 if (STAMP) sA += stamp3() - tx;
                 __syncthreads();
             }
-            if constexpr (LC) __syncthreads();   // LC: the slab waves write the dirty lines back
             if (!ET || !et_after(it)) break;
         }
         write_stamps();
@@ -1000,13 +849,15 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     // the second-dispatched half of the slab waves loses VALU arbitration to
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
+    // (fair issue by phase in the fast periods, below; LDPC_COOP3_SLAB_PRIO=1:
+    // static priority for the second-dispatched waves instead)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
     const int kl = lane >> 3, q = lane & 7;
     const char *Vb = (const char *)a.V + (size_t)wg * a.wgoff;
     const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
     // parity rows k + j of this group at Pb + 16 j: row r at Pb - 16 k + 16 r
     char *Pr = (char *)a.P + ((size_t)wg * (size_t)(a.m + 1) - (size_t)a.k) * 16;
-    Slab3<WS, R, NMS, LC> sl{sm,
+    Slab3<WS, R, NMS> sl{sm,
                     a,
                     q >= X ? Pr : (char *)Vb,
                     q >= X ? 16u : (uint32_t)a.pitch,
@@ -1017,22 +868,24 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     sw,
                     lane,
                     a.tail,
-                    0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
-                    opaque(0x050d040du),
-                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
+                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff), opaque(0x03000300u),
+                        opaque(0x040c000cu), opaque(V127), opaque(VNEG127), opaque(a.offp)},
+                    PkBits{{sopaque(0x00010001u), sopaque(0x00040004u), sopaque(0x00100010u), sopaque(0x00400040u),
+                            sopaque(0x01000100u), sopaque(0x04000400u), sopaque(0x10001000u), 0u},
+                           {sopaque(0x00020002u), sopaque(0x00080008u), sopaque(0x00200020u), sopaque(0x00800080u),
+                            sopaque(0x02000200u), sopaque(0x08000800u), sopaque(0x20002000u), 0u}},
                     opaque(a.nmsf),
                     // DMA lane 8e + slot: entry e < 6 a V row (record entry e, the
                     // o edge's D0-1 for e = X), e >= 6 message piece e - 6
                     kl < X ? Vb : kl == X ? Pr : Mb + (kl - 6) * 16,
-                    LC ? Mb : Mb + (2 + (kl & 1)) * 16,
+                    Mb + (2 + (kl & 1)) * 16,
                     kl < X ? (uint32_t)a.pitch : kl == X ? 16u : (uint32_t)MREC,
                     kl < 6 ? 0xFFFFFFFFu : COOP_CHK_MASK,
                     (uint32_t)(kl < X ? kl : (kl == X ? D0 - 1 : D0)),
-                    (uint32_t)(kl * 16 + 4 * (q >> 1)),
+                    (uint32_t)(kl * 16 + 2 * q),
                     (uint32_t)(q < 4 ? (6 + (q >> 1)) * 128 + kl * 16 + (q & 1) * 8
                                      : SM::IN_B + ((q >> 1) - 2) * 128 + kl * 16 +
                                            (q & 1) * 8)};
-    sl.lcV = Vb;
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     constexpr int NI = CF::NI, NS = CF::NS;
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
@@ -1045,39 +898,21 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         }
         St3 st[NS];
         uint4 mfc;   // records D0 .. D0+3 of the next pre's window
-        if constexpr (LC) {
-            // lines resident before period -1 -> their slots (a lane group per line)
-            for (int i = kl * WS + sw; i < a.npro; i += 8 * WS) {
-                const uint32_t code = a.lcpro[i];
-                sm.cache[code >> 16][q] = *(const uint4 *)(Vb + (size_t)(code & 0xFFFFu) * 128 + q * 16);
-            }
+        PfIn pi;
 #pragma unroll
-            for (int i = 0; i <= R; i++) sl.gathers_lc(i, i);   // old messages of windows 0 .. R
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();   // the resident lines are in the cache
-            PreIn in;
-            sl.read_pre_lc(0, 0, in);
-            if (a.tail == 0)
-                sl.template pre<true, ET>(0, in, st[0]);
-            else
-                sl.template pre<false, ET>(0, in, st[0]);
-        } else {
-            PfIn pi;
-#pragma unroll
-            for (int i = 0; i <= R; i++) {   // window i -> in[w][i]   (nw > R + 3)
-                sl.read_pf(i, pi);
-                sl.gathers(pi, i);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            PreIn in;
-            sl.read_pre(0, 0, in, sl.read_mf(0), mfc);
-            sl.mask_early(0, in.mf);
-            sl.fwd_read(0, in);
-            if (a.tail == 0)
-                sl.template pre<true, ET>(0, in, st[0]);
-            else
-                sl.template pre<false, ET>(0, in, st[0]);
+        for (int i = 0; i <= R; i++) {   // window i -> in[w][i]   (nw > R + 3)
+            sl.read_pf(i, pi);
+            sl.gathers(pi, i);   // (window i)
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PreIn in;
+        sl.read_pre(0, 0, in, sl.read_mf(0), mfc);
+        sl.mask_early(0, in.mf);
+        sl.fwd_read(0, in);
+        if (a.tail == 0)
+            sl.template pre<true, ET>(0, in, st[0]);
+        else
+            sl.template pre<false, ET>(0, in, st[0]);
         __syncthreads();   // prologue 2
         if (STAMP) t0 = stamp3();
         int uA = a.nw - 1;   // local index of window p-1 (post)
@@ -1103,7 +938,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         // period p-R, followed by 4 in each later period: in the main loop (every
         // period does everything, no tail window) vmcnt(4(R-1)) covers them.
         constexpr int MP1 = -1, MP2 = -1;   // mid-phase priorities (none: quarter-period levels measured the same)
-        const bool fair = a.slab_prio == 2;
+        // fair issue: a compile-time choice (a runtime one branches around the
+        // s_setprio, and values live across that join get re-masked)
+        constexpr bool fair = true;
         auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
             constexpr bool GU = decltype(guarded)::value;
@@ -1113,69 +950,8 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             PreIn in;
             PfIn pi;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
-            unsigned long long t1 = 0, t2 = 0, t3 = 0, ta = 0, tb = 0;
-            if constexpr (LC) {
-                // line cache: (A) read the lines written back now, (B) message
-                // stores of window p-2, post of window p-1 into the cache rows,
-                // (D) the writeback stores, (G) pre of window p+1 from the
-                // cache, (H) message gathers of window p+1+R, (I) this
-                // period's 8 line loads (LDS-DMA into their slots).  Vector
-                // memory per fast period and wave: B, D, H, 8 x I = 11
-                // operations; vmcnt(11) before the barrier leaves the previous
-                // period's complete: its line loads are in the cache for the
-                // next period (first read two periods after the issue) and
-                // the gathers of window p+R, read in period p+R-1, have landed
-                uint32_t wbc;
-                uint4 wbd = make_uint4(0, 0, 0, 0);
-                if (fast) {
-                    if (fair) __builtin_amdgcn_s_setprio(1);
-                    typename decltype(sl)::LcPf f;
-                    sl.lc_prefetch(p, f);
-                    sl.stores_lc(sc);
-                    const uint32_t xr = sl.read_x(p - 1, sp);
-                    sl.lc_line_read(f.wbc, wbd);
-                    sl.template post<false, ET, MP1>(p - 1, xr, sp, f.rrp);
-                    if (STAMP) ta = stampL();
-                    sl.lc_wb_store(f.wbc, wbd);
-                    if (STAMP) tb = stampL();
-                    sl.read_pre_lc(f.rrn, (s + 1) % NI, in);
-                    sl.gathers_lc_c(f.gchk, (s + R + 1) % NI);
-                    sl.lc_dma(f.ldc);
-                    sc.md = sm.mst[sw][kl][q & 3];
-                    sc.chk = f.stchk;
-                    if (STAMP) t1 = t2 = stampL();
-                    if (fair) __builtin_amdgcn_s_setprio(0);
-                    sl.template pre<false, ET, MP2>(p + 1, in, sn);
-                    if (STAMP) t3 = stampL();
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    sl.lc_wb_read(p, wbc, wbd);
-                    if (dst) sl.stores_lc(sc);
-                    if (dpo) {
-                        const uint32_t xr = sl.read_x(p - 1, sp);
-                        if (uA == a.tail)
-                            sl.template post<true, ET>(p - 1, xr, sp, sl.rec(p - 1));
-                        else
-                            sl.template post<false, ET>(p - 1, xr, sp, sl.rec(p - 1));
-                    }
-                    sl.lc_wb_store(wbc, wbd);
-                    if (STAMP) t1 = t2 = t3 = stampL();
-                    if (dpr) {
-                        sl.read_pre_lc(p + 1, (s + 1) % NI, in);
-                        if (uB == a.tail)
-                            sl.template pre<true, ET>(p + 1, in, sn);
-                        else
-                            sl.template pre<false, ET>(p + 1, in, sn);
-                        sl.gathers_lc(p + 1 + R, (s + R + 1) % NI);
-                    }
-                    sl.lc_dma(sl.lc_code(sm.tab[p & (TQ - 1)].loads));
-                    if (dpo) {
-                        sl.read_st_lc(p - 1, sc);
-                        sc_tl = uA == a.tail;
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-            } else if (fast) {
+            unsigned long long t1 = 0, t2 = 0, t3 = 0;
+            if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs, nothing from memory) and waits for its window
                 // p+1 gathers only before its pre, half a period later than at
@@ -1187,12 +963,15 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 sl.read_pf(p + 1 + R, pi);
                 constexpr int VMW = 4 * (R - 1) + 2;
                 sl.template post<false, ET, MP1>(p - 1, xr, sp);
+                if (STAMP) t1 = stamp3();
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMW) : "memory");
+                if (STAMP) t2 = stampL();
+                // the gathers before the pre's LDS reads: their lane < 16 branch
+                // would otherwise sit between those u16 loads and their use
+                sl.gathers(pi, p + 1 + R);
                 sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
                 sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values (wave 0)
-                sl.gathers(pi, (s + R + 1) % NI);
                 sl.read_st(p - 1, sc);
-                if (STAMP) t1 = t2 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(0);
                 sl.template pre<false, ET, MP2>(p + 1, in, sn);
                 if (STAMP) t3 = stampL();
@@ -1219,21 +998,13 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                         sl.template pre<true, ET>(p + 1, in, sn);
                     else
                         sl.template pre<false, ET>(p + 1, in, sn);
-                    sl.gathers(pi, (s + R + 1) % NI);
+                    sl.gathers(pi, p + 1 + R);
                 }
-            }
-            if constexpr (LC) {   // the previous period's line loads and gathers have landed (see above)
-                if (fast) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
             }
             if (STAMP) {
                 const unsigned long long t5 = stampL();
                 sA += t5 - tx;
-                if (fast && LC) {   // post | writeback store | LDS reads, issue | pre (the rest: the end wait)
-                    sP[0] += ta - tx;
-                    sP[1] += tb - ta;
-                    sP[2] += t1 - tb;
-                    sP[3] += t3 - t1;
-                } else if (fast) {
+                if (fast) {
                     sP[0] += t1 - tx;
                     sP[1] += t2 - t1;
                     sP[2] += t3 - t2;
@@ -1261,18 +1032,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)
                 period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
         });
-        if constexpr (LC) {
-            sl.stores_lc(sc);   // window G-1
-            // the dirty lines still in the cache go back to V
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            for (int i = kl * WS + sw; i < a.nepi; i += 8 * WS) {
-                const uint32_t code = a.lcepi[i];
-                *(uint4 *)(Vb + (size_t)(code & 0xFFFFu) * 128 + q * 16) = sm.cache[code >> 16][q];
-            }
-        } else {
-            sl.stores(sc, sc_tl);   // window G-1
-        }
+        sl.stores(sc, sc_tl);   // window G-1
         if (!ET || !et_after(it)) break;
     }
     write_stamps();
@@ -1293,7 +1053,7 @@ int env_int3(const char *name, int def)
 
 // diagnostic build (LDPC_COOP3_STAMP=1): per-period cycles of each wave
 template <int WS>
-void report_stamps3(const unsigned long long *d, int grid, hipStream_t s, bool lc = false)
+void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
 {
     constexpr int nwaves = WS + 1, CHW = WS >= 3 ? 3 : WS;
     std::vector<unsigned long long> h((size_t)grid * nwaves * 8);
@@ -1314,12 +1074,9 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s, bool l
         const double *x = &v[w * 8];
         if (w == CHW)
             fprintf(stderr, "  chain %d: busy %.0f steps %.0f\n", w, x[0], x[1]);
-        else if (lc)
-            fprintf(stderr, "  slab %d: busy %.0f | post %.0f wb %.0f lds+issue %.0f pre %.0f end-wait %.0f\n", w, x[0],
-                    x[1], x[2], x[3], x[4], x[0] - x[1] - x[2] - x[3] - x[4]);
         else
-            fprintf(stderr, "  slab %d: busy %.0f | vmcnt %.0f %s %.0f %s %.0f mem %.0f\n", w, x[0], x[1],
-                    w == 0 ? "post" : "pre", x[2], w == 0 ? "pre" : "post", x[3], x[0] - x[1] - x[2] - x[3]);
+            fprintf(stderr, "  slab %d: busy %.0f | stores+post %.0f vmcnt-wait %.0f reads+pre %.0f rest %.0f\n", w,
+                    x[0], x[1], x[2], x[3], x[0] - x[1] - x[2] - x[3]);
     }
 }
 
@@ -1336,12 +1093,12 @@ int launch_wsr(const Coop3Args &a, int grid, bool stamped, hipStream_t s)
 
 }  // namespace
 
-// forwarding code of a value written dW windows before the reading window,
-// by slot `slot`, record entry e (Slab3::fwd_read): ring slot (g - dW) mod 4 is
-// ((-dW) mod 4 + g) mod 4, entry offset (e * (S + 1) + slot) * 16 < 8192
+// read code of a value written dW windows before the reading window, by slot
+// `slot`, record entry e (Slab3::fwd_read): ring slot (g - dW) mod 4 is
+// ((-dW) mod 4 + g) mod 4, stage offset (e * (S + 1) + slot) * 16 < STG_RING
 static uint32_t fwd_code3(int dW, int slot, int e, int S)
 {
-    return ((uint32_t)(-dW) & 3u) << 13 | (uint32_t)(e * (S + 1) + slot) * 16u | (dW == 2 ? 2u : 0u) | 1u;
+    return ((uint32_t)(-dW) & 3u) << RING_SH | (uint32_t)(e * (S + 1) + slot) * 16u | (dW == 2 ? 2u : 0u) | 1u;
 }
 
 // OMS / MS as coop (coop_params_ok); NMS with factor <= 64 (msg_max <= 63: the
@@ -1411,9 +1168,9 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
             const uint32_t *src = rec_at(u, k);
             uint32_t *rec = &tab[((size_t)u * S + kn) * RECW];
             std::copy(src, src + RECW, rec);
-            for (int j = 0; j < 2 * NFW; j++) {   // plan codes -> fwd_code3 (the unused last half: 0)
+            for (int j = 0; j < 2 * NFW; j++) {   // plan codes -> read codes (the unused last half: 0)
                 const uint32_t f = j < X ? code_at(src, j) : COOP_FWD_NONE;
-                uint32_t c = 0;
+                uint32_t c = j < X ? in_code3(kn / 8, kn % 8, j) : 0u;   // not forwarded: the own input record
                 if (f != COOP_FWD_NONE) {
                     const int dw = (int)(f >> 9), uw = (u + nw - dw) % nw;
                     c = fwd_code3(dw, slot_of[(size_t)uw * S + ((f >> 3) & 63)], (int)(f & 7), S);
@@ -1457,49 +1214,6 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
     cc->S = S;
     cc->R = r;
     cc->nw = nw;
-    // the LDS line cache (LDPC_COOP3_LC=1): plan, window tables, prologue /
-    // epilogue lists; without a plan coop3 runs its forwarding-ring path
-    if (S == 48 && env_int3("LDPC_COOP3_LC", 0) != 0 && h->m < 65536 && h->n % 8 == 0) {
-        LcPlan lp;
-        if (lc_build_plan(pl.tab, RECW, nw, S, D0, pl.tail, h->n, LC_SLOTS, lp) == 0) {
-            std::vector<LcWin> wt((size_t)nw);
-            const uint32_t sink = (uint32_t)(h->n / 8);   // slot 0
-            for (int u = 0; u < nw; u++) {
-                LcWin &W = wt[(size_t)u];
-                for (int k = 0; k < S; k++) {
-                    const uint32_t *rec = &pl.tab[((size_t)u * S + k) * RECW];
-                    const uint16_t *ro = &lp.rowoff[((size_t)u * S + k) * 8];
-                    const uint32_t act = (rec[D0] & COOP_M_ACT) ? 1u : 0u, step = (rec[D0] >> STEP_SHIFT) & 63u;
-                    W.rec[k] = make_uint4(ro[0] | (uint32_t)ro[1] << 16, ro[2] | (uint32_t)ro[3] << 16,
-                                          ro[4] | (uint32_t)ro[5] << 16, ro[6] | (step | act << 6) << 16);
-                    W.chk[k] = (uint16_t)(rec[D0] & COOP_CHK_MASK);
-                }
-                for (int i = 0; i < LC_LMAX; i++) {
-                    // entries 0 .. 5 always present (one per slab wave: every wave
-                    // issues each line operation every period, for the vmcnt counts)
-                    const uint32_t l = lp.loads[(size_t)u * LC_LMAX + i], b = lp.wbs[(size_t)u * LC_LMAX + i];
-                    W.loads[i] = l == LC_NONE ? sink : l;   // every entry: 8 line loads per wave and period
-                    W.wbs[i] = (b == LC_NONE && i < 6) ? sink : b;
-                }
-            }
-            const size_t tb = wt.size() * sizeof(LcWin);
-            if (hipMalloc(&cc->d_lctab, tb) != hipSuccess ||
-                hipMalloc(&cc->d_lcpro, 4 * std::max<size_t>(1, lp.pro.size())) != hipSuccess ||
-                hipMalloc(&cc->d_lcepi, 4 * std::max<size_t>(1, lp.epi.size())) != hipSuccess ||
-                hipMemcpy(cc->d_lctab, wt.data(), tb, hipMemcpyHostToDevice) != hipSuccess ||
-                (lp.pro.size() && hipMemcpy(cc->d_lcpro, lp.pro.data(), 4 * lp.pro.size(), hipMemcpyHostToDevice) !=
-                                      hipSuccess) ||
-                (lp.epi.size() && hipMemcpy(cc->d_lcepi, lp.epi.data(), 4 * lp.epi.size(), hipMemcpyHostToDevice) !=
-                                      hipSuccess)) {
-                coop_free(cc);
-                return ldpc_set_error(LDPC_EDEVICE, "coop3 line-cache tables");
-            }
-            cc->lc_valid = 1;
-            cc->lc_slots = lp.slots;
-            cc->n_pro = (int)lp.pro.size();
-            cc->n_epi = (int)lp.epi.size();
-        }
-    }
     cc->tail = pl.tail;
     cc->n_fwd = pl.n_fwd;
     cc->x0 = (int)h->edge_var[h->check_start[0] + X];
@@ -1521,7 +1235,6 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     if (L.early && coop3_et_in_kernel(cc, L.n)) {
         // in-kernel early termination (one launch, coop3_decode<.., ET>)
         if (!L.iters_used) return -1;
-        if (L.vpriv && cc.lc_valid && (size_t)L.n * 2 > sizeof(Smem3LC<6, 2>)) return -1;
         if (L.iters == 0) {
             hipLaunchKernelGGL(fill_iters3_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used, 0);
             return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1551,18 +1264,9 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.V = (int8_t *)L.V;
     a.Mc = (uint8_t *)L.msg;
     a.tab = cc.d_tab;
-    // V layout: rows of L.vpitch codewords, a group's 16 B at wg * 16 in each;
-    // or (L.vpriv) every group's rows contiguous, [stride / 16][n + 1][16]
-    a.pitch = L.vpriv ? CW : L.vpitch;
-    a.wgoff = L.vpriv ? (size_t)(L.n + 8) * CW : (size_t)CW;
-    const bool lc = L.vpriv && cc.lc_valid;   // the line cache needs the grouped layout
-    if (lc) {
-        a.tab = cc.d_lctab;
-        a.lcpro = cc.d_lcpro;
-        a.lcepi = cc.d_lcepi;
-        a.npro = cc.n_pro;
-        a.nepi = cc.n_epi;
-    }
+    // V layout: rows of L.vpitch codewords, a group's 16 B at wg * 16 in each
+    a.pitch = L.vpitch;
+    a.wgoff = (size_t)CW;
     a.G = cc.nw * iters;
     a.nw = cc.nw;
     a.tail = cc.tail;
@@ -1586,7 +1290,7 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.offp = nms ? 0u : (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
     a.nmsf = nms ? (uint32_t)(L.param & 0xFFFF) * 0x00010001u : 0u;
     a.prio = env_int3("LDPC_COOP3_PRIO", 1);
-    a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 0 none, 1 static (second waves), 2 fair by phase
+    a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 1: static (second waves) on top of the fair phases
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups
     const int ws = cc.S / 8;
@@ -1597,30 +1301,6 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
     int rc;
-    if (lc) {
-        if (ws != 6) return -1;
-        if (stamped && !et && L.algo != LDPC_ALGO_NMS) {
-            hipLaunchKernelGGL((coop3_decode<6, 2, true, false, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
-            rc = hipGetLastError() == hipSuccess ? 0 : -1;
-            if (rc == 0) report_stamps3<6>(a.stamps, grid, s, true);
-            (void)hipFree(a.stamps);
-            return rc;
-        }
-        if (stamped) (void)hipFree(a.stamps);
-        if (et) {
-            if (L.algo == LDPC_ALGO_NMS)
-                hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true, true>), dim3(grid), dim3(64 * 7), 0, s, a);
-            else
-                hipLaunchKernelGGL((coop3_decode<6, 2, false, true, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
-        } else {
-            if (L.algo == LDPC_ALGO_NMS)
-                hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true, true>), dim3(grid), dim3(64 * 7), 0, s, a);
-            else
-                hipLaunchKernelGGL((coop3_decode<6, 2, false, false, false, true>), dim3(grid), dim3(64 * 7), 0, s,
-                                   a);
-        }
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
     if (et) {
         if (stamped) (void)hipFree(a.stamps);
         if (L.algo == LDPC_ALGO_NMS)

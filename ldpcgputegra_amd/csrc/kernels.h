@@ -9,8 +9,6 @@ struct DecodeLaunch {
     void *msg;
     int stride;          // codeword slots (multiple of 64): the batch padded
     int vpitch;          // V row pitch in codewords (>= stride; coop3 may pad it)
-    int vpriv;           // coop3 only: V is [stride / 16][N + 8][16] (each 16-codeword group's rows
-                         // contiguous) instead of [N + 1][vpitch]
     int batch;
     int iters;
     int is_float;
@@ -45,9 +43,6 @@ int launch_generic(const DecodeLaunch &L, hipStream_t s);
 int launch_quantize_f32_i8(const float *y, int8_t *q, long count, int factor, int sat_neg, int sat_pos,
                            hipStream_t s);
 int launch_interleave_i8(const int8_t *llr, int8_t *V, int n, int batch, int stride, hipStream_t s);
-// the same into / out of the grouped layout V[stride / 16][n + 8][16] (DecodeLaunch::vpriv)
-int launch_interleave_i8_grouped(const int8_t *llr, int8_t *V, int n, int batch, int stride, hipStream_t s);
-int launch_deinterleave_i8_grouped(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, hipStream_t s);
 int launch_interleave_f32(const float *llr, float *V, int n, int batch, int stride, hipStream_t s);
 int launch_deinterleave_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, int stride,
                            hipStream_t s);

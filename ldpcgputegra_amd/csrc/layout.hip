@@ -15,16 +15,7 @@
 
 namespace {
 
-// V element (node i, codeword b): row-major V[i][stride], or (GROUPED) the
-// 16-codeword-group layout V[b / 16][n + 8][16] (rows n .. n+7: the sink line)
-template <bool GROUPED>
-__device__ __forceinline__ size_t vidx(int i, int b, int n, int stride)
-{
-    return GROUPED ? ((size_t)(b >> 4) * (size_t)(n + 8) + (size_t)i) * 16 + (size_t)(b & 15)
-                   : (size_t)i * stride + b;
-}
-
-template <typename T, bool GROUPED = false>
+template <typename T>
 __global__ void __launch_bounds__(256) interleave_k(const T *__restrict__ src, T *__restrict__ dst, int n,
                                                     int batch, int stride)
 {
@@ -40,11 +31,11 @@ __global__ void __launch_bounds__(256) interleave_k(const T *__restrict__ src, T
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         const int i = n0 + ty + 4 * r, b = b0 + tx;
-        if (i < n && b < stride) dst[vidx<GROUPED>(i, b, n, stride)] = tile[tx][ty + 4 * r];
+        if (i < n && b < stride) dst[(size_t)i * stride + b] = tile[tx][ty + 4 * r];
     }
 }
 
-template <typename T, bool GROUPED = false>
+template <typename T>
 __global__ void __launch_bounds__(256) deinterleave_k(const T *__restrict__ V, uint8_t *__restrict__ hard,
                                                       T *__restrict__ soft, int n, int batch, int stride)
 {
@@ -54,7 +45,7 @@ __global__ void __launch_bounds__(256) deinterleave_k(const T *__restrict__ V, u
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         const int i = n0 + ty + 4 * r, b = b0 + tx;
-        tile[ty + 4 * r][tx] = (i < n && b < batch) ? V[vidx<GROUPED>(i, b, n, stride)] : (T)0;
+        tile[ty + 4 * r][tx] = (i < n && b < batch) ? V[(size_t)i * stride + b] : (T)0;
     }
     __syncthreads();
 #pragma unroll
@@ -169,18 +160,6 @@ int launch_interleave_f32(const float *llr, float *V, int n, int batch, int stri
 {
     dim3 g((n + 63) / 64, (stride + 63) / 64);
     hipLaunchKernelGGL(interleave_k<float>, g, dim3(256), 0, s, llr, V, n, batch, stride);
-    return ok();
-}
-int launch_interleave_i8_grouped(const int8_t *llr, int8_t *V, int n, int batch, int stride, hipStream_t s)
-{
-    dim3 g((n + 63) / 64, (stride + 63) / 64);
-    hipLaunchKernelGGL((interleave_k<int8_t, true>), g, dim3(256), 0, s, llr, V, n, batch, stride);
-    return ok();
-}
-int launch_deinterleave_i8_grouped(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, hipStream_t s)
-{
-    dim3 g((n + 63) / 64, (batch + 63) / 64);
-    hipLaunchKernelGGL((deinterleave_k<int8_t, true>), g, dim3(256), 0, s, V, hard, soft, n, batch, 0);
     return ok();
 }
 int launch_deinterleave_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, int stride,

@@ -170,22 +170,3 @@ def test_dvbs2_shaped_tables(name, k, q, profile):
     cw = code.encode(info)
     assert np.array_equal(cw[:, :k], info)
     assert (t.syndrome(cw) == 0).all()
-
-
-def test_coop3_line_cache_plan():
-    """The LDS line-cache plan of coop3 for DVB-S2 r1/2 (linecache.cpp) builds
-    and passes its replay self-check within the kernel's 800 cache lines and
-    48 line loads / writebacks per period; codes without a coop3 schedule have
-    none."""
-    import ctypes as C
-    from ldpcgputegra_amd import Code, _lib
-    def info(name, max_slots=800):
-        v = [C.c_int() for _ in range(7)]
-        code = Code(name)                             # keep the handle alive over the call
-        _lib.check(_lib.lib().ldpc_code_coop3_lc_info(code.handle, max_slots, *[C.byref(x) for x in v]))
-        return [x.value for x in v]
-    st, slots, ml, mw, inst, npro, nepi = info("dvbs2_r1_2")
-    assert st == 0 and 400 < slots <= 800 and ml <= 48 and mw <= 48 and inst > 8100
-    assert 0 < nepi <= npro <= slots
-    assert info("dvbs2_r1_2", 300)[0] < 0            # too few lines: no plan
-    assert info("576x288")[0] == -100                 # no coop3 schedule

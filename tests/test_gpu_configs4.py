@@ -144,35 +144,6 @@ def test_per_iteration_early_termination_padded_pitch(kernel, env):
     dec.close()
 
 
-@pytest.mark.parametrize("early,batch", [(False, 200), (True, 200), (False, 1024)])
-def test_coop3_grouped_layout_vs_oracle(early, batch):
-    """coop3 with V in the grouped layout (LDPC_COOP3_GROUPED=1: each
-    16-codeword group's rows contiguous, [stride/16][N+1][16]) -- ragged and
-    whole-workgroup batches, fixed iterations and in-kernel early termination:
-    soft output, hard decisions and iterations used equal the oracle's."""
-    torch = _torch()
-    t = load_table("dvbs2_r1_2")
-    iters = 20
-    llr = channel.awgn_i8_host(t.n, batch, seed=29, table=channel.i8_table(channel.sigma_from_ebn0(1.1, 0.5)))
-    eh, es, eit = O.decode_i8(t, llr, iters, early_term=early, return_soft=True, threads=O.host_threads())
-    os.environ["LDPC_COOP3_GROUPED"] = "1"
-    try:
-        dec = Decoder(Code("dvbs2_r1_2"), max_batch=batch, kernel=8)
-        d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
-        d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
-        d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
-        dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=default_params(early_term=int(early)),
-                             soft=d_soft, iters_used=d_its)
-        torch.cuda.synchronize()
-    finally:
-        del os.environ["LDPC_COOP3_GROUPED"]
-    assert dec.last_kernel == "coop3"
-    assert np.array_equal(d_its.cpu().numpy(), eit)
-    assert np.array_equal(d_soft.cpu().numpy(), es)
-    assert np.array_equal(d_hard.cpu().numpy(), eh)
-    dec.close()
-
-
 @pytest.mark.parametrize("factor,early", [(29, False), (24, True), (32, False)])
 def test_coop3_nms_vs_oracle(factor, early):
     """NMS (CDecoder_NMS_fixed_SSE.cpp:188-240: cst = (min * factor) >> 5) on
@@ -197,68 +168,4 @@ def test_coop3_nms_vs_oracle(factor, early):
     assert np.array_equal(d_its.cpu().numpy(), eit)
     assert np.array_equal(d_soft.cpu().numpy(), es)
     assert np.array_equal(d_hard.cpu().numpy(), eh)
-    dec.close()
-
-
-def _lc_decoder(batch):
-    """A coop3 context built with the LDS line cache (LDPC_COOP3_LC=1 at
-    context creation)."""
-    os.environ["LDPC_COOP3_LC"] = "1"
-    try:
-        return Decoder(Code("dvbs2_r1_2"), max_batch=batch, kernel=8)
-    finally:
-        del os.environ["LDPC_COOP3_LC"]
-
-
-@pytest.mark.parametrize("algo,early,batch,iters", [("oms", False, 200, 20), ("oms", True, 200, 30),
-                                                    ("nms", False, 64, 12), ("nms", True, 100, 25),
-                                                    ("oms", False, 16, 3)])
-def test_coop3_line_cache_vs_oracle(algo, early, batch, iters):
-    """coop3 with its V rows in the LDS line cache (grouped V layout, lines
-    loaded / written back by the plan of linecache.cpp): soft output, hard
-    decisions and iterations used equal the oracle's -- OMS and NMS, fixed
-    iterations and in-kernel early termination, ragged and single-workgroup
-    batches."""
-    from ldpcgputegra_amd import ALGO_NMS
-    torch = _torch()
-    t = load_table("dvbs2_r1_2")
-    llr = channel.awgn_i8_host(t.n, batch, seed=41 + batch, table=channel.i8_table(channel.sigma_from_ebn0(1.1, 0.5)))
-    o_algo, o_param = (O.NMS, 29) if algo == "nms" else (O.OMS, 1)
-    eh, es, eit = O.decode_i8(t, llr, iters, o_algo, o_param, early_term=early, return_soft=True,
-                              threads=O.host_threads())
-    dec = _lc_decoder(batch)
-    p = default_params(algo=ALGO_NMS, factor=29, early_term=int(early)) if algo == "nms" else \
-        default_params(early_term=int(early))
-    d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
-    d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
-    d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
-    for rep in range(2):
-        dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=p, soft=d_soft, iters_used=d_its)
-        torch.cuda.synchronize()
-        assert dec.last_kernel == "coop3"
-        assert np.array_equal(d_its.cpu().numpy(), eit), rep
-        assert np.array_equal(d_soft.cpu().numpy(), es), (rep, int((d_soft.cpu().numpy() != es).sum()))
-        assert np.array_equal(d_hard.cpu().numpy(), eh), rep
-    dec.close()
-
-
-def test_coop3_line_cache_full_batch_vs_reference():
-    """configs[2] in full on the line-cache coop3: 4096 codewords, 50 it, every
-    hard decision equal to the reference SSE decoder's (oracle/_ref)."""
-    torch = _torch()
-    t = load_table("dvbs2_r1_2")
-    B = 4096
-    dec = _lc_decoder(B)
-    llr = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
-    dec.awgn_i8_device(llr, 0, 77, channel.i8_table(channel.sigma_from_ebn0(1.0, 0.5)))
-    h = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
-    dec.decode_i8_device(llr, h, 50)
-    torch.cuda.synchronize()
-    assert dec.last_kernel == "coop3"
-    got, host = h.cpu().numpy(), llr.cpu().numpy()
-    thr = O.host_threads()
-    exp = O.ref_decode_mt("dvbs2_r1_2", host, 50, 1, thr) if O.ref_available("dvbs2_r1_2") else \
-        O.decode_i8(t, host, 50, threads=thr)
-    diff = np.nonzero((got != exp).any(axis=1))[0]
-    assert diff.size == 0, "codewords differing from the reference: %s" % diff[:16]
     dec.close()

@@ -29,8 +29,6 @@ for s in ${STEPS//,/ }; do
     vmem) step ubench_vmem 120 ./tools/ubench_vmem ldpcgputegra_amd/codes/dvbs2_r1_2.txt ;;
     lc) step ubench_lc 120 ./tools/ubench_lc ;;
     bench) step bench 300 python3 bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
-    benchg) LDPC_COOP3_GROUPED=1 step bench_grouped 300 python3 bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
-    benchlc) LDPC_COOP3_LC=1 step bench_lc 300 python3 bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
     mixed) step bench_mixed 300 python3 bench.py --mixed ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} ;;
     tests) step tests 900 python3 -u -m pytest ${TESTS:-tests} -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "${TESTK:-not nothing}" ;;
     prof) PROF_OUT=$OUT/prof bash tools/profile.sh || exit $? ;;
