@@ -69,22 +69,7 @@ constexpr int NFW = (X + 1) / 2;    // forwarding-code dwords per record
 constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;
 constexpr int DPER = 3;             // a window table's LDS-DMA is waited for DPER periods after its issue
 constexpr int TQ = 16;              // window-table slots in LDS
-constexpr int STG_RING = 8192;      // stage bytes per ring slot
-constexpr int RING = 16384;         // bytes per ring slot: stage [0, STG_RING), slab waves' input records after
-constexpr int RING_SH = 14;         // log2(RING): a read code + (g << RING_SH) addresses window g's ring slot
-constexpr uint32_t SEL0 = 0x010d000du;   // v_perm selector: u16 [b0 b1] -> R pair
-
-// one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot)
-struct In3 {
-    uint4 a[8][8];                    // [0..5][slot] V rows (info edges, record entry D0-1), [6..7][slot] message
-                                      // 0..31 B
-    uint4 pad[4];                     // (rows 6, 7 and b[0], b[1] in different banks)
-    uint4 b[2][8];                    // [0..1][slot] message 32..63 B
-};                                    // (entry-major: the 8 slots of one read are in different banks)
-constexpr uint32_t IN_B3 = sizeof(uint4) * (8 * 8 + 4);   // byte offset of In3::b
-// read code of info edge j of slot (w, kl) when it is not forwarded: its V row
-// piece in the window's own input record (ring slot delta 0)
-constexpr uint32_t in_code3(int w, int kl, int j) { return (uint32_t)(STG_RING + w * (int)sizeof(In3) + j * 128 + kl * 16); }
+constexpr int STG_RING = 8192;      // bytes per forwarding-ring slot (power of two: see fwd_code3)
 
 template <int WS, int R>
 struct Cfg {
@@ -108,25 +93,26 @@ template <int WS, int R>
 struct alignas(16) Smem3 {
     using CF = Cfg<WS, R>;
     static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
-    // ring slot g % 4 (at LDS address 0, RING bytes apart so that a read code
-    // + (g << RING_SH) addresses it):
-    // * [0, STG_RING): the stage -- new V of window g, [record entry * (S + 1) +
-    //   slot] x 16 codewords (int8, entries padded: the stores' reads of 8
-    //   entries are conflict-free): the V stores' staging and the forwarding ring;
-    // * [STG_RING, ...): the slab waves' input records of window g (In3, LDS-DMA).
-    // Every info-edge V read of a pre is one ds_read_u16 at its read code: the
-    // own input record, or the stage of the window that wrote the value
-    uint4 ring[NR][RING / 16];
+    uint4 stg[NR][STG_RING / 16];     // new V of a window, [record entry * (S + 1) + slot] x 16 codewords (int8,
+                                      // entries padded: the stores' reads of 8 entries are conflict-free): the
+                                      // V stores' staging and the forwarding ring (ring slot g % NR, 8 KB apart
+                                      // so that a forwarding code + (g << 13) addresses its entry)
     uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
     uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post)
-    static constexpr uint32_t IN_B = IN_B3;
+    struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
+        uint4 a[8][8];                //   [0..5][slot] V rows (info edges, record entry D0-1), [6..7][slot] message
+                                      //   0..31 B
+        uint4 pad[4];                 //   (rows 6, 7 and b[0], b[1] in different banks)
+        uint4 b[2][8];                //   [0..1][slot] message 32..63 B
+    } in[WS][NI];                     // (entry-major: the 8 slots of one read are in different banks)
+    static constexpr uint32_t IN_B = sizeof(uint4) * (8 * 8 + 4);   // byte offset of In::b
     uint4 mst[WS][8][4];              // new messages of a window per slab wave, [slot] x 64 B
-    // (early termination: between segments the whole struct holds the hard
-    // bits of every variable, u16 x 64800 for DVB-S2)
+    uint4 et_spare[320];              // early termination: between segments the whole struct holds the
+                                      // hard bits of every variable (u16 x 64800 for DVB-S2; one
+                                      // workgroup per CU either way)
 };
-static_assert(STG_RING + 6 * sizeof(In3) <= RING && 8 * 49 * 16 <= STG_RING, "ring slot layout");
 
 struct Coop3Args {
     int8_t *V;                        // V[n + 1][pitch]; row n is the sink of inactive slots
@@ -177,10 +163,10 @@ LDPC_DEV uint32_t pk_shl5(uint32_t a) { return us(sv(a) << (short)5); }
 
 // what a period reads from LDS, issued together at its start
 struct PreIn {
-    uint32_t v[D0 - 1];               // v[X]: the o edge's V pair (raw u16, entry D0-1)
+    uint32_t v[D0 - 1];               // raw V dwords (info edges, entry D0-1)
     uint32_t ma, mb;                  // old message record of this pair
     uint4 mf;                         // record words D0 .. D0+3: meta, forwarding codes (read a period early)
-    unsigned short fv[X];             // V pairs (raw u16) of the info edges, at their read codes
+    uint32_t fv[X];                   // forwarded V pairs (raw u16) of the info edges with a forwarding code
 };
 struct StIn {                         // the stores of window p-2
     uint4 vd, md;                     // staged V row piece (16 codewords), message piece
@@ -200,30 +186,25 @@ struct Slab3 {
     uint32_t vsm;                     //   q >= X go to the parity rows' own layout P, see Coop3Args)
     i32x4 mr;                         // message rows in 16-B units
     int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
+    uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
+    uint32_t fsel;                    // ... of a forwarded u16 (0x050d040d, in a VGPR)
     PkK K;
-    PkBits mb;                        // message-code bits per edge (SGPRs)
     uint32_t fk;                      // NMS factor per half (value form)
     // per-lane constants of the LDS-DMA gathers (lane (kl, j): j < 6 a V row, j >= 6 a message piece)
     const char *g1base, *g2base;
     uint32_t g1mul, g1mask, recsel;
-    uint32_t vrd, mrd;                // byte offsets of this lane's V u16 (entry 0) / message pair in an In3 record
+    uint32_t vrd, mrd;                // byte offsets of this lane's V dword / message pair in an In record
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
 
     // ---- reads
-    LDPC_DEV char *ringb(int g) const { return (char *)&sm.ring[g & (NR - 1)][0]; }
-    LDPC_DEV uint32_t in_lds(int g) const   // this wave's input record of window g (LDS address)
+    // in.mf = mfc (window g's codes, read in the previous period); mfn <- window g+1's
+    LDPC_DEV void read_pre(int g, int ib, PreIn &in, const uint4 &mfc, uint4 &mfn) const
     {
-        return (uint32_t)(uintptr_t)(ringb(g) + STG_RING) + (uint32_t)w * (uint32_t)sizeof(In3);
-    }
-    // in.mf = mfc (window g's codes, read in the previous period); mfn <- window
-    // g+1's.  The o edge's row (record entry D0-1, never forwarded) and the old
-    // messages from the input record; the info edges by fwd_read
-    LDPC_DEV void read_pre(int g, int, PreIn &in, const uint4 &mfc, uint4 &mfn) const
-    {
-        const char *inb = ringb(g) + STG_RING + w * sizeof(In3);
-        in.v[X] = *(const unsigned short *)(inb + vrd + 128 * X);
+        const char *inb = (const char *)&sm.in[w][ib];
+#pragma unroll
+        for (int j = 0; j < D0 - 1; j++) in.v[j] = *(const uint32_t *)(inb + vrd + 128 * j);
         const uint2 mm = *(const uint2 *)(inb + mrd);
         in.ma = mm.x;
         in.mb = mm.y;
@@ -231,23 +212,24 @@ struct Slab3 {
         mfn = read_mf(g + 1);
     }
     LDPC_DEV uint4 read_mf(int g) const { return *(const uint4 *)&sm.tab[g & (TQ - 1)][k][D0]; }
-    // V pairs (u16) of window g's info edges: read code j (16 bits, fwd_code3 /
-    // in_code3) = ((-dW) mod 4) << RING_SH | offset in the ring slot | near << 1 |
-    // forwarded; code + (g << RING_SH) carries ring slot (g - dW) mod 4 (dW = 0:
-    // the own input record).  Branch-free: 2 VALU + 1 ds_read_u16 per edge
+    // forwarded values of window g's info edges: code j (16 bits, fwd_code3)
+    // = ((-dW) mod 4) << 13 | stage offset | near << 1 | use; code + (g << 13)
+    // carries ring slot (g - dW) mod 4 in bits 13-14.  Unused codes read
+    // ring offset 0 (ignored).  Branch-free: 2 VALU + 1 ds_read_u16 per edge.
     LDPC_DEV void fwd_read(int g, PreIn &in) const
     {
-        const uint32_t gs = (uint32_t)__builtin_amdgcn_readfirstlane(g << RING_SH), q2 = 2u * (uint32_t)q;
+        const char *sbase = (const char *)&sm.stg[0][0];
+        const uint32_t gs = (uint32_t)__builtin_amdgcn_readfirstlane(g << 13), q2 = 2u * (uint32_t)q;
         const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
 #pragma unroll
         for (int j = 0; j < X; j++) {
             const uint32_t code = (j & 1) ? fw[j >> 1] >> 16 : fw[j >> 1] & 0xFFFFu;
-            in.fv[j] = *(const unsigned short *)(ringb(0) + (((code + gs) & (uint32_t)(RING * NR - 16)) | q2));
+            in.fv[j] = *(const unsigned short *)(sbase + (((code + gs) & 0x7FF0u) | q2));
         }
     }
     LDPC_DEV void read_st(int g, StIn &in) const
     {
-        in.vd = ((const uint4 *)ringb(g))[q * (S + 1) + k];
+        in.vd = sm.stg[g % NR][q * (S + 1) + k];
         in.md = sm.mst[w][kl][q & 3];
         in.row = sm.tab[g & (TQ - 1)][k][q];
         in.chk = sm.tab[g & (TQ - 1)][k][D0] & COOP_CHK_MASK;
@@ -272,18 +254,17 @@ struct Slab3 {
         if (q < (tl ? D0 : D0 - 1)) *(uint4 *)(vsb + (size_t)in.row * vsm) = in.vd;
         if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
     }
-    // window g's gathers into this wave's input record (ring slot g % 4)
-    LDPC_DEV void gathers(const PfIn &in, int g) const
+    LDPC_DEV void gathers(const PfIn &in, int ib) const
     {
-        static_assert(offsetof(In3, b) == IN_B3, "In layout");
-        const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane(in_lds(g));
+        static_assert(offsetof(typename SM::In, b) == SM::IN_B, "In layout");
+        const uint32_t base = (uint32_t)(uintptr_t)&sm.in[w][ib];
         dma16(g1base + (size_t)in.rv * g1mul, base);
-        if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + IN_B3);
+        if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + SM::IN_B);
     }
 
-    // the first windows of the decode: a forwarded code whose source window
-    // precedes window 0 (g < dW) reads the V row from the input record instead
-    LDPC_DEV void mask_early(int g, uint4 &mf) const
+    // the first windows of the decode: a code whose source window precedes
+    // window 0 (g < dW) is not used
+    LDPC_DEV static void mask_early(int g, uint4 &mf)
     {
         uint32_t *fw = &mf.y;
 #pragma unroll
@@ -291,9 +272,8 @@ struct Slab3 {
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const uint32_t code = (fw[i] >> (16 * h)) & 0xFFFFu;
-                const int dw = (int)(((0u - (code >> RING_SH) - 2u) & 3u) + 2u);
-                if (2 * i + h < X && (code & 1u) && g < dw)
-                    fw[i] = (fw[i] & ~(0xFFFFu << (16 * h))) | in_code3(w, kl, 2 * i + h) << (16 * h);
+                const int dw = (int)(((0u - (code >> 13) - 2u) & 3u) + 2u);
+                if ((code & 1u) && g < dw) fw[i] &= ~(1u << (16 * h));
             }
     }
 
@@ -304,10 +284,15 @@ struct Slab3 {
         constexpr bool FZ = FZ_;
         const uint32_t meta = in.mf.x;
         uint32_t v[D0 - 1];
-        // V pair of edge j: the u16 its read code addressed (SEL0: bytes 0, 1 -> R pair)
+        // V pair of edge j: this pair's two bytes of the loaded V dword, or the
+        // forwarded u16 (selector 0x050d040d: bytes 0, 1 of in.fv[j] -> R pair)
+        const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
 #pragma unroll
-        for (int j = 0; j < X; j++) v[j] = unpack_v(in.fv[j], SEL0);
-        v[X] = unpack_v(in.v[X], SEL0);
+        for (int j = 0; j < X; j++) {
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)fw[j >> 1], 16 * (j & 1), 1);   // 0 / -1
+            v[j] = perm(in.fv[j], in.v[j], bfi(m, fsel, usel));
+        }
+        v[X] = unpack_v(in.v[X], usel);
         const MsgTab t = msg_tab(in.mb);
         const uint32_t MA = in.ma, neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
@@ -318,7 +303,7 @@ struct Slab3 {
             // same edges either way, and min1 == msg_max implies cst1 == cst2)
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t, K)), neg127);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
                 const uint32_t aj = abs_r(c, c510);
                 s.c[J] = c;
                 s.a[J] = aj;
@@ -328,14 +313,14 @@ struct Slab3 {
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
-            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t, K)), neg127);
+            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), neg127);
             const uint32_t ao = abs_r(cor, c510);
             s.c[X] = cor;
             s.a[X] = ao;
             s.sacc = sacc ^ cor;
             s.mn2 = pk_max(min1, pk_min(ao, min2));
             s.mn1 = pk_min(min1, ao);
-            const uint32_t mx = old_msg<X>(MA, t, K);
+            const uint32_t mx = old_msg<X>(MA, t);
             s.mx = mx;
             // chain constants in value form (R >> 8, C >> 8), both codewords at once
             COV = pk_ashr8(cor);
@@ -351,11 +336,11 @@ struct Slab3 {
                 TV = pk_ashr8(pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0));
                 EPS = EM | 0x00010001u;
                 const uint32_t base = pk_sub(COV, pk_sub(pk_ashr8(mx) ^ EM, EM));   // c_o - eps * m_x
-                A = pk_sub(base, K.offp);
-                B = pk_add(base, K.offp);
+                A = pk_sub(base, a.offp);
+                B = pk_add(base, a.offp);
             }
-            L = pk_max(pk_sub(COV, TV), K.vneg127);
-            H = pk_min(pk_add(COV, TV), K.v127);
+            L = pk_max(pk_sub(COV, TV), VNEG127);
+            H = pk_min(pk_add(COV, TV), V127);
             if constexpr (FZ) {   // converged codewords: L = H = V[p_i] as read, the step returns it
 #pragma unroll
                 for (int j = 0; j < X; j++) s.v[j] = v[j];
@@ -368,7 +353,7 @@ struct Slab3 {
             // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t, K)), neg127);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
                 // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2
                 const uint32_t aj = NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510);
                 s.c[J] = c;
@@ -385,7 +370,7 @@ struct Slab3 {
             uint32_t MAn = 0;
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn, neg127, mb);
+                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn, neg127);
                 if constexpr (FZ) s.c[J] = bfi(fm, v[J], s.c[J]);   // converged codewords keep their V
             });
             s.mx = 0;
@@ -426,13 +411,13 @@ struct Slab3 {
         cp[NP] = r1;
     }
 
-    // post of window g (x inputs xr): new V pairs -> the stage of ring slot g % 4, messages ->
+    // post of window g (x inputs xr): new V pairs -> stg[g % NR], messages ->
     // mst[w]; they leave in the stores of the same period
     template <bool TL, bool FZ_ = false, int MP = -1>
     LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
     {
         constexpr bool FZ = FZ_;
-        unsigned short *st = (unsigned short *)((uint4 *)ringb(g) + k);   // [entry][..S slots..][8 pairs] u16
+        unsigned short *st = (unsigned short *)&sm.stg[g % NR][k];   // [entry][..S slots..][8 pairs] u16
         constexpr int ES = (S + 1) * 8;                                 // u16 between entries
         uint32_t MA, MB;
         if constexpr (!TL) {
@@ -449,15 +434,15 @@ struct Slab3 {
             uint32_t nv[X + 1];
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127, mb);
+                const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
                 nv[J] = FZ ? perm(n, s.v[J], psel) : pack_v(n);   // FZ: pack_v of new / old per codeword
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
-            const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127, mb);
+            const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127);
             nv[X] = FZ ? perm(nx, xr, psel) : pack_v(nx);
             // the o edge: message bits only (the next check rewrites V[o] as its x edge)
-            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127, mb);
+            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
             MB = perm(k2, k1, 0x07030501u);
 #pragma unroll
             for (int j = 0; j <= X; j++) st[j * ES + q] = (unsigned short)nv[j];
@@ -849,8 +834,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     // the second-dispatched half of the slab waves loses VALU arbitration to
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
-    // (fair issue by phase in the fast periods, below; LDPC_COOP3_SLAB_PRIO=1:
-    // static priority for the second-dispatched waves instead)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
     const int kl = lane >> 3, q = lane & 7;
     const char *Vb = (const char *)a.V + (size_t)wg * a.wgoff;
@@ -868,12 +851,9 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     sw,
                     lane,
                     a.tail,
-                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff), opaque(0x03000300u),
-                        opaque(0x040c000cu), opaque(V127), opaque(VNEG127), opaque(a.offp)},
-                    PkBits{{sopaque(0x00010001u), sopaque(0x00040004u), sopaque(0x00100010u), sopaque(0x00400040u),
-                            sopaque(0x01000100u), sopaque(0x04000400u), sopaque(0x10001000u), 0u},
-                           {sopaque(0x00020002u), sopaque(0x00080008u), sopaque(0x00200020u), sopaque(0x00800080u),
-                            sopaque(0x02000200u), sopaque(0x08000800u), sopaque(0x20002000u), 0u}},
+                    0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
+                    opaque(0x050d040du),
+                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
                     opaque(a.nmsf),
                     // DMA lane 8e + slot: entry e < 6 a V row (record entry e, the
                     // o edge's D0-1 for e = X), e >= 6 message piece e - 6
@@ -882,7 +862,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     kl < X ? (uint32_t)a.pitch : kl == X ? 16u : (uint32_t)MREC,
                     kl < 6 ? 0xFFFFFFFFu : COOP_CHK_MASK,
                     (uint32_t)(kl < X ? kl : (kl == X ? D0 - 1 : D0)),
-                    (uint32_t)(kl * 16 + 2 * q),
+                    (uint32_t)(kl * 16 + 4 * (q >> 1)),
                     (uint32_t)(q < 4 ? (6 + (q >> 1)) * 128 + kl * 16 + (q & 1) * 8
                                      : SM::IN_B + ((q >> 1) - 2) * 128 + kl * 16 +
                                            (q & 1) * 8)};
@@ -902,7 +882,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 #pragma unroll
         for (int i = 0; i <= R; i++) {   // window i -> in[w][i]   (nw > R + 3)
             sl.read_pf(i, pi);
-            sl.gathers(pi, i);   // (window i)
+            sl.gathers(pi, i);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         PreIn in;
@@ -938,9 +918,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         // period p-R, followed by 4 in each later period: in the main loop (every
         // period does everything, no tail window) vmcnt(4(R-1)) covers them.
         constexpr int MP1 = -1, MP2 = -1;   // mid-phase priorities (none: quarter-period levels measured the same)
-        // fair issue: a compile-time choice (a runtime one branches around the
-        // s_setprio, and values live across that join get re-masked)
-        constexpr bool fair = true;
+        const bool fair = a.slab_prio == 2;
         auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
             constexpr bool GU = decltype(guarded)::value;
@@ -963,15 +941,12 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 sl.read_pf(p + 1 + R, pi);
                 constexpr int VMW = 4 * (R - 1) + 2;
                 sl.template post<false, ET, MP1>(p - 1, xr, sp);
-                if (STAMP) t1 = stamp3();
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMW) : "memory");
-                if (STAMP) t2 = stampL();
-                // the gathers before the pre's LDS reads: their lane < 16 branch
-                // would otherwise sit between those u16 loads and their use
-                sl.gathers(pi, p + 1 + R);
                 sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
                 sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values (wave 0)
+                sl.gathers(pi, (s + R + 1) % NI);
                 sl.read_st(p - 1, sc);
+                if (STAMP) t1 = t2 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(0);
                 sl.template pre<false, ET, MP2>(p + 1, in, sn);
                 if (STAMP) t3 = stampL();
@@ -998,7 +973,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                         sl.template pre<true, ET>(p + 1, in, sn);
                     else
                         sl.template pre<false, ET>(p + 1, in, sn);
-                    sl.gathers(pi, p + 1 + R);
+                    sl.gathers(pi, (s + R + 1) % NI);
                 }
             }
             if (STAMP) {
@@ -1075,8 +1050,8 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
         if (w == CHW)
             fprintf(stderr, "  chain %d: busy %.0f steps %.0f\n", w, x[0], x[1]);
         else
-            fprintf(stderr, "  slab %d: busy %.0f | stores+post %.0f vmcnt-wait %.0f reads+pre %.0f rest %.0f\n", w,
-                    x[0], x[1], x[2], x[3], x[0] - x[1] - x[2] - x[3]);
+            fprintf(stderr, "  slab %d: busy %.0f | vmcnt %.0f %s %.0f %s %.0f mem %.0f\n", w, x[0], x[1],
+                    w == 0 ? "post" : "pre", x[2], w == 0 ? "pre" : "post", x[3], x[0] - x[1] - x[2] - x[3]);
     }
 }
 
@@ -1093,12 +1068,12 @@ int launch_wsr(const Coop3Args &a, int grid, bool stamped, hipStream_t s)
 
 }  // namespace
 
-// read code of a value written dW windows before the reading window, by slot
-// `slot`, record entry e (Slab3::fwd_read): ring slot (g - dW) mod 4 is
-// ((-dW) mod 4 + g) mod 4, stage offset (e * (S + 1) + slot) * 16 < STG_RING
+// forwarding code of a value written dW windows before the reading window,
+// by slot `slot`, record entry e (Slab3::fwd_read): ring slot (g - dW) mod 4 is
+// ((-dW) mod 4 + g) mod 4, entry offset (e * (S + 1) + slot) * 16 < 8192
 static uint32_t fwd_code3(int dW, int slot, int e, int S)
 {
-    return ((uint32_t)(-dW) & 3u) << RING_SH | (uint32_t)(e * (S + 1) + slot) * 16u | (dW == 2 ? 2u : 0u) | 1u;
+    return ((uint32_t)(-dW) & 3u) << 13 | (uint32_t)(e * (S + 1) + slot) * 16u | (dW == 2 ? 2u : 0u) | 1u;
 }
 
 // OMS / MS as coop (coop_params_ok); NMS with factor <= 64 (msg_max <= 63: the
@@ -1168,9 +1143,9 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
             const uint32_t *src = rec_at(u, k);
             uint32_t *rec = &tab[((size_t)u * S + kn) * RECW];
             std::copy(src, src + RECW, rec);
-            for (int j = 0; j < 2 * NFW; j++) {   // plan codes -> read codes (the unused last half: 0)
+            for (int j = 0; j < 2 * NFW; j++) {   // plan codes -> fwd_code3 (the unused last half: 0)
                 const uint32_t f = j < X ? code_at(src, j) : COOP_FWD_NONE;
-                uint32_t c = j < X ? in_code3(kn / 8, kn % 8, j) : 0u;   // not forwarded: the own input record
+                uint32_t c = 0;
                 if (f != COOP_FWD_NONE) {
                     const int dw = (int)(f >> 9), uw = (u + nw - dw) % nw;
                     c = fwd_code3(dw, slot_of[(size_t)uw * S + ((f >> 3) & 63)], (int)(f & 7), S);
@@ -1290,7 +1265,7 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.offp = nms ? 0u : (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
     a.nmsf = nms ? (uint32_t)(L.param & 0xFFFF) * 0x00010001u : 0u;
     a.prio = env_int3("LDPC_COOP3_PRIO", 1);
-    a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 1: static (second waves) on top of the fair phases
+    a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 0 none, 1 static (second waves), 2 fair by phase
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups
     const int ws = cc.S / 8;

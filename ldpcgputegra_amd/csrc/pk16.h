@@ -81,19 +81,6 @@ LDPC_DEV uint32_t abs_r(uint32_t r, uint32_t c510) { return pk_max(r, pk_sub(c51
 // is read
 struct PkK {
     uint32_t neg127, r0, c510, rmm, coff;   // R(-127), R(0), 510, R(msg_max), C(offset) per half
-    uint32_t msk, mor;                      // old_msg's selector mask / fixed bytes (one v_and_or_b32)
-    uint32_t v127, vneg127, offp;           // +-127 and the offset per half (value form)
-};
-// a constant the optimiser cannot see, held in an SGPR (a VOP3 operand that
-// is neither a literal nor a VGPR: v_and_or_b32 v, v, s, v)
-LDPC_DEV uint32_t sopaque(uint32_t x)
-{
-    asm volatile("" : "+s"(x));
-    return x;
-}
-// message-code bits of edge J per half (new_msg): sign at bit 2J, "got cst2" at 2J + 1
-struct PkBits {
-    uint32_t s[8], n[8];
 };
 
 // byte tables [+cst1, -cst1, +cst2, -cst2] of the two codewords of a pair
@@ -108,26 +95,25 @@ LDPC_DEV MsgTab msg_tab(uint32_t MB)
 
 // old message of edge J (C pair): byte 1 = t0[code0], byte 3 = t1[code1]
 template <int J>
-LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t, const PkK &K)
+LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t)
 {
     uint32_t sh;
     if constexpr (J <= 4)
         sh = MA << (8 - 2 * J);
     else
         sh = MA >> (2 * J - 8);
-    return perm(t.t1, t.t0, (sh & K.msk) | K.mor);   // (msk, mor = 0x03000300, 0x040c000c)
+    return perm(t.t1, t.t0, (sh & 0x03000300u) | 0x040c000cu);
 }
 
 // new message of edge J: its code into MA, the new V (R pair) returned
 template <int J>
 LDPC_DEV uint32_t new_msg(uint32_t c, uint32_t a, uint32_t min1, uint32_t k1, uint32_t k2, uint32_t P, uint32_t &MA,
-                          uint32_t neg127, const PkBits &mb)
+                          uint32_t neg127)
 {
     const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));   // -1: a > min1, the edge gets cst2
     const uint32_t rr = bfi(neq, k2, k1);
     const uint32_t sgn = pk_sra15(c ^ P);             // -1: the message is negative
-    MA = opaque((sgn & mb.s[J]) | MA);                // (SGPR bit masks: one v_and_or_b32 each; opaque
-    MA = opaque((neq & mb.n[J]) | MA);                // keeps the OR chain from being reassociated)
+    MA |= (sgn & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
     return pk_max(pk_add_sat(c, pk_sub(rr ^ sgn, sgn)), neg127);
 }
 
