@@ -133,6 +133,15 @@ int ldpc_code_coop_plan(const ldpc_code *h, int S, int R, int *first, int *count
  * apart; reads written dist+1 .. R+dist windows earlier are forwarded). */
 int ldpc_code_coop_plan_dist(const ldpc_code *h, int S, int R, int dist, int *first, int *count, int max_windows,
                              int *n_windows, int *tail, int *n_fwd);
+/* Line cache of the DVB-S2 r1/2 kernel (kernel 8, coop3): the information
+ * rows move between HBM and LDS as 128-B lines (8 rows x 16 codewords) on a
+ * static plan checked by replaying it.  slots: LDS line slots the plan uses
+ * (0 when the code has no coop3 schedule), max_slots: what the kernel has,
+ * residencies: line loads per iteration, prologue / epilogue: lines filled /
+ * written back at a segment start / end.  (Introspection for tests; replaces
+ * no reference interface.) */
+int ldpc_code_coop3_lc_info(const ldpc_code *h, int *slots, int *max_slots, int *residencies, int *prologue,
+                            int *epilogue);
 /* Layer plan of the LDS-resident kernel (kernel 7): maximal runs of
  * consecutive same-group checks sharing no variable (one block row of a
  * quasi-cyclic code).  lds_i8 / lds_f32: 1 if a codeword's state fits the

@@ -224,6 +224,16 @@ class Code:
                                               C.byref(n), C.byref(t), C.byref(f)))
         return dict(windows=list(zip(first.tolist(), count.tolist())), tail=t.value, n_fwd=f.value)
 
+    def coop3_line_cache(self):
+        """Line-cache plan of the coop3 kernel (kernel 8): dict(slots,
+        max_slots, residencies, prologue, epilogue); None when the code has no
+        coop3 schedule."""
+        v = [C.c_int() for _ in range(5)]
+        _lib.check(_lib.lib().ldpc_code_coop3_lc_info(self._h, *[C.byref(x) for x in v]))
+        if v[0].value == 0:
+            return None
+        return dict(zip(("slots", "max_slots", "residencies", "prologue", "epilogue"), (x.value for x in v)))
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and _lib._lib is not None:

@@ -35,14 +35,11 @@ struct Scratch {
     size_t msg_bytes = 0;
     void *d_early = nullptr;        // coop early termination: live[stride] u8, bad[stride] u32, iters[stride]
     size_t early_bytes = 0;
-    void *d_Vs = nullptr;           // coop3 per-iteration early termination: V snapshot [N+1][vpitch]
-    size_t Vs_bytes = 0;
     void release()
     {
         (void)hipFree(d_V);
         (void)hipFree(d_msg);
         (void)hipFree(d_early);
-        (void)hipFree(d_Vs);
         *this = Scratch{};
     }
 };
@@ -306,7 +303,8 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
     const bool w2 = windowed2_params_ok(p);
     const bool co = c->coop.valid && coop_params_ok(p);
-    const bool co3 = c->coop3.valid && coop3_params_ok(p, c->coop3) && coop3_stride_ok(stride);
+    const bool co3 = c->coop3.valid && coop3_params_ok(p, c->coop3) && coop3_stride_ok(stride) &&
+                     (!p->early_term || coop3_et_in_kernel(c->coop3, c->code->n));
     switch (c->kernel) {
     case 1: return 1;
     case 2: return w1 ? 2 : -1;
@@ -378,33 +376,33 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
                              : win    ? windowed_msg_bytes(h, stride)
                                       : (size_t)h->e * stride * esz) +
                             4096;
-    // coop3: its parity-row layout follows the messages (DecodeLaunch::P)
-    const size_t msg_need = msg_zero + (kern == 8 ? (size_t)(h->m + 1) * stride : 0);
-    // V row pitch (codewords): the coop kernels pad it by LDPC_VPITCH_PAD (default
-    // 64; multiple of 64) codewords.  A workgroup touches its 16-B piece of
-    // every row and the XCD remap gives each XCD a fixed 512-B window of a row:
-    // with a power-of-two pitch (batch 4096) every row's window of an XCD falls
-    // on the same few L2 channels.  Measured (DVB-S2 r1/2, 4096 cw, 50 it,
-    // coop3): pitch 4096 57.6 ms, 4160 / 4224 49.7 / 49.6 ms, 4352 50.4,
-    // 4608 52.7, 5120 57.2
-    const int vpad = (kern == 8 || kern == 5) ? std::max(0, getenv_int("LDPC_VPITCH_PAD", 64)) / 64 * 64 : 0;
+    // V row pitch (codewords): the coop kernel pads it by LDPC_VPITCH_PAD
+    // (default 64; multiple of 64) codewords.  A workgroup touches its 16-B
+    // piece of every row and the XCD remap gives each XCD a fixed 512-B window
+    // of a row: with a power-of-two pitch (batch 4096) every row's window of an
+    // XCD falls on the same few L2 channels.  Measured (DVB-S2 r1/2, 4096 cw,
+    // 50 it, the row-layout coop3 of r02): pitch 4096 57.6 ms, 4160 / 4224
+    // 49.7 / 49.6 ms, 4352 50.4, 4608 52.7, 5120 57.2.  coop3
+    // keeps V grouped per 16 codewords instead (coop3_group_bytes per group).
+    const int vpad = kern == 5 ? std::max(0, getenv_int("LDPC_VPITCH_PAD", 64)) / 64 * 64 : 0;
     const int vpitch = stride + vpad;
-    const size_t v_rows = (size_t)h->n + 1;   // row n: the coop kernels' sink row
-    if ((rc = ensure(&sc.d_V, &sc.V_bytes, v_rows * vpitch * esz)) != LDPC_OK) return rc;
-    if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_need)) != LDPC_OK) return rc;
+    const size_t vgroup = kern == 8 ? coop3_group_bytes(h) : 0;
+    const size_t v_bytes = kern == 8 ? (size_t)(stride / 16) * vgroup
+                                     : ((size_t)h->n + 1) * vpitch * esz;   // row n: the coop kernel's sink row
+    if ((rc = ensure(&sc.d_V, &sc.V_bytes, v_bytes)) != LDPC_OK) return rc;
+    if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_zero)) != LDPC_OK) return rc;
     // early termination: live u8 | bad u32 | iterations used i32 (when the caller passed none)
     const bool et_state = (kern == 5 || kern == 8) && p->early_term;
-    // V snapshots: only coop3's per-iteration launches need them (where its
-    // in-kernel early termination does not apply)
-    const bool et_vs = et_state && kern == 8 && !coop3_et_in_kernel(c->coop3, h->n);
     if (et_state && (rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
-    if (et_vs && (rc = ensure(&sc.d_Vs, &sc.Vs_bytes, (size_t)(h->n + 1) * vpitch)) != LDPC_OK) return rc;
     if (alloc_only) return LDPC_OK;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
     HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));
     if (is_float) {
         if (launch_interleave_f32((const float *)d_llr, (float *)sc.d_V, h->n, batch, vpitch, s))
+            return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
+    } else if (kern == 8) {
+        if (launch_interleave_grp_i8((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, stride, vgroup, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
     } else {
         if (launch_interleave_i8((const int8_t *)d_llr, (int8_t *)sc.d_V, h->n, batch, vpitch, s))
@@ -413,7 +411,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     DecodeLaunch L{};
     L.V = sc.d_V;
     L.msg = sc.d_msg;
-    if (kern == 8) L.P = (int8_t *)sc.d_msg + msg_zero;
+    L.vgroup = vgroup;
     L.stride = stride;
     L.vpitch = vpitch;
     L.batch = batch;
@@ -438,7 +436,6 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         L.bad = (uint32_t *)sc.d_early;
         if (!L.iters_used) L.iters_used = (int32_t *)((char *)sc.d_early + (size_t)stride * 4);
         L.live = (uint8_t *)sc.d_early + (size_t)stride * 8;
-        if (et_vs) L.Vs = (int8_t *)sc.d_Vs;
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (c->profile) {
@@ -461,10 +458,12 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
                               e != hipSuccess ? hipGetErrorString(e) : "launch configuration rejected by the host side");
     }
     if (d_hard || d_soft) {
-        int r2 = is_float ? launch_deinterleave_f32((const float *)sc.d_V, d_hard, (float *)d_soft, h->n, batch,
-                                                    vpitch, s)
-                          : launch_deinterleave_i8((const int8_t *)sc.d_V, d_hard, (int8_t *)d_soft, h->n,
-                                                   batch, vpitch, s);
+        int r2 = is_float    ? launch_deinterleave_f32((const float *)sc.d_V, d_hard, (float *)d_soft, h->n, batch,
+                                                       vpitch, s)
+                 : kern == 8 ? launch_deinterleave_grp_i8((const int8_t *)sc.d_V, d_hard, (int8_t *)d_soft, h->n,
+                                                          batch, vgroup, s)
+                             : launch_deinterleave_i8((const int8_t *)sc.d_V, d_hard, (int8_t *)d_soft, h->n,
+                                                      batch, vpitch, s);
         if (r2) return ldpc_set_error(LDPC_EDEVICE, "deinterleave: %s", hipGetErrorString(hipGetLastError()));
     }
     return LDPC_OK;

@@ -13,13 +13,16 @@ struct CoopCode {
     int x0;          // coop3: V row of check 0's x edge (the chain's first input)
     int m0, d1;      // coop3: checks of degree d0 (group 0), degree of the later group
     uint32_t *d_tab; // [nw][S][recw]
+    // coop3 line cache (LcPlan): slots used, lines resident at a segment start / written back at its end
+    int lc_slots, n_lc_pro, n_lc_epi;
+    uint32_t *d_lc_pro, *d_lc_epi;
 };
 
 bool coop_params_ok(const ldpc_params *p);
 int coop_upload(const ldpc_code *h, CoopCode *cc);
 void coop_free(CoopCode *cc);
 int launch_coop(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
-// early termination around per-iteration launches (coop, coop3 at WS != 6): init,
+// early termination around per-iteration launches (coop with LDPC_COOP_ET_KERNEL=0): init,
 // syndrome after iteration `it` (0-based; with L.Vs, snapshot of the codewords
 // converging now), and the final merge of the snapshots into V (L.Vs only)
 int coop_early_begin(const DecodeLaunch &L, hipStream_t s);
@@ -57,6 +60,8 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPl
 // ---- coop3.hip: slab waves doing pre + post, i16 chain (D0 = 7) ----
 bool coop3_params_ok(const ldpc_params *p, const CoopCode &cc);
 bool coop3_stride_ok(int stride);
+// bytes between two codeword groups of coop3's grouped V (DecodeLaunch::vgroup)
+size_t coop3_group_bytes(const ldpc_code *h);
 // compressed messages: [stride / 16][m + 1][8 pairs][2] u32 (4 B per codeword and check; row m is the sink)
 size_t coop3_msg_bytes(const ldpc_code *h, int stride);
 int coop3_upload(const ldpc_code *h, CoopCode *cc);
@@ -66,6 +71,28 @@ struct Coop3Host {
     int S = 0, nw = 0, recw = 0, d0 = 0;
 };
 int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o);
+struct LcPlan;
+// the schedule and its line-cache plan (linecache.cpp): 0 ok, 1 none for this code, < 0 error
+int coop3_plan_lc(const ldpc_code *h, Coop3Host &ho, LcPlan &lp);
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
-// early termination inside the coop3 launch (else per-iteration launches + V snapshots)
+
+// ---- linecache.cpp: coop3's LDS line cache (info rows as 128-B lines) ----
+constexpr int LC_GAP = 8;    // accesses of a line >= LC_GAP periods apart: separate residencies
+constexpr int LC_LEAD = 3;   // a line is loaded (into VGPRs) >= 3 periods before its first access
+constexpr int LC_OPS = 48;   // line loads / writebacks per period: 6 slab waves x 8 lane groups
+struct LcPlan {
+    int slots = 0;                 // LDS line slots used, the sink (slot 0) included
+    int residencies = 0;           // line residencies per iteration
+    std::vector<uint32_t> ops;     // [nw][LC_OPS][2]: load line | writeback line << 16,
+                                   //   slot written (the load of 2 periods earlier) | writeback slot << 16
+    std::vector<uint32_t> piece;   // [nw][S][D0 - 2]: LDS byte offset (from the cache) of each info entry's piece
+    std::vector<uint32_t> pro;     // slot << 16 | line: lines resident at a segment start
+    std::vector<uint32_t> epi;     // slot << 16 | line: dirty lines written back at a segment end
+};
+// tab: coop3's permuted slot records (Coop3Host::pl.tab); 0 = ok (plan self-checked), -1 = no plan
+int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int n, int k, int max_slots,
+                  LcPlan &o);
+int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int n, int k,
+                  int iters);
+// early termination inside the coop3 launch (the only form coop3 has)
 bool coop3_et_in_kernel(const CoopCode &cc, int n);

@@ -962,6 +962,8 @@ int coop_upload(const ldpc_code *h, CoopCode *cc)
 void coop_free(CoopCode *cc)
 {
     (void)hipFree(cc->d_tab);
+    (void)hipFree(cc->d_lc_pro);
+    (void)hipFree(cc->d_lc_epi);
     *cc = CoopCode{};
 }
 

@@ -23,19 +23,28 @@
 //   3 with the highest priority;
 // * a window's checks are permuted over its slots (coop3_upload): the chain
 //   still runs them in check order (each record carries its chain step), and
-//   every distance-2 forwarding source and reader sits in slab wave 0, so no
-//   wave ever waits for another inside a period (one s_barrier per period);
-// * vector memory -- the bound on MI355X: each check moves 6 scattered 16-B
-//   V row pieces each way per 16 codewords, and the CU's texture path stalls
-//   on the scattered stores -- is issued at the start and middle of a
-//   period, never at its end: stores one barrier after their post, LDS-DMA
-//   gathers R = 2 windows ahead.
+//   every check that reads a value written two windows earlier sits in slab
+//   wave 0 with the check that wrote it, so no wave ever waits for another
+//   inside a period (one s_barrier per period);
+// * V lives in the grouped layout Vg[group][row][16 codewords] and the
+//   information rows move between HBM and the workgroup's LDS as whole 128-B
+//   lines (8 rows x 16 codewords) through a line cache planned on the host
+//   (linecache.cpp: each line is loaded ~3 periods before its first use and
+//   written back after its last, one residency serving ~8 checks): a period's
+//   vector memory is one 64-lane store (messages + parity rows), one 64-lane
+//   line writeback, one 64-lane LDS-DMA gather (messages + o-edge parity rows)
+//   and one 64-lane line load per slab wave -- whole lines, no scattered 16-B
+//   V pieces (on MI355X the CU's texture path stalled on those: 47 ms per
+//   launch, 18 % of it on the info-row stores alone);
+// * the pre / post of a check read / write its info rows in the line cache,
+//   so a value written by the post of window u-1 .. u-2 is simply there for
+//   the pre of window u (the host keeps distance-2 writers and readers in slab
+//   wave 0, which posts before its pre).
 //
 // Period p (one s_barrier): chain = steps of window p; slab waves = post of
 // window p-1, pre of window p+1, stores of window p-2, gathers of window
-// p+1+R.  The plan (dist 1) keeps neighbouring windows free of shared
-// information variables; values written 2 .. R+3 windows before a pre are
-// forwarded through a 4-window LDS stage ring.
+// p+1+R, the line cache's writebacks / loads of period p and the slot writes
+// of the lines loaded in period p-2.
 //
 // The chain recurrence (check i, x edge input Y = V[p_{i-1}]):
 //   V[p_i] = clamp(c_o + eps * sign(c_x) * min(max(|c_x| - off, 0), T), +-127)
@@ -59,17 +68,21 @@
 
 #include "pk16.h"
 
-__device__ void sbuf_store_v4(i32x4 v, i32x4 rsrc, int index, int offset, int soffset, int aux)
-    __asm("llvm.amdgcn.struct.buffer.store.v4i32");
-
 namespace {
 
 constexpr int D0 = 7, X = D0 - 2;   // first-group check degree, information edges per check
-constexpr int NFW = (X + 1) / 2;    // forwarding-code dwords per record
-constexpr int RECW = (D0 + 1 + NFW + 3) / 4 * 4;
-constexpr int DPER = 3;             // a window table's LDS-DMA is waited for DPER periods after its issue
-constexpr int TQ = 16;              // window-table slots in LDS
-constexpr int STG_RING = 8192;      // bytes per forwarding-ring slot (power of two: see fwd_code3)
+constexpr int RECW = 12;            // slot record words (coop3_upload)
+constexpr int DPER = 2;             // a window table's LDS-DMA is waited for DPER periods after its issue
+constexpr int TQ = 8;               // window-table slots in LDS
+constexpr int LC_SLOTS = 776;       // line-cache slots (128 B each; slot 0 is the sink)
+
+// slot record (coop3_upload): words 0..4 the LDS byte offsets (from the line
+// cache) of the info entries' 16-B pieces, 5 / 6 the x / o edge parity rows
+// (row - k), 7 meta = check | COOP_M_ACT | chain step << STEP_SHIFT, 8 the
+// period's line load / writeback (line | line << 16) and 9 its slot write /
+// writeback slot (slot | slot << 16) of lane group (slot & 7) of the slot's
+// slab wave (LcPlan::ops), 10 .. 11 zero
+constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
 
 template <int WS, int R>
 struct Cfg {
@@ -77,60 +90,49 @@ struct Cfg {
     static constexpr int KAHEAD = R + 2 + DPER;        // tables staged KAHEAD windows ahead of the chain
     static constexpr int NI = R + 1;                   // LDS-DMA input windows in flight per slab wave
     static constexpr int NS = R + 1 < 3 ? 3 : R + 1;   // window states in VGPRs (pre at p-1, post at p+1)
-    static constexpr int U = NS;                       // periods unrolled (multiple of NI and NS)
-    static constexpr int NR = 4;                       // staged-output windows: window g's entries are read in
-                                                       // periods g+1 .. g+R+2 (stores, forwards)
+    static constexpr int U = NS;                       // periods unrolled (multiple of NI, NS and 3: line loads
+                                                       // are written to their slots two periods later)
+    static constexpr int NR = 2;                       // staged-output windows: window g's parity V is staged in
+                                                       // period g+1 and read for its stores at that period's end
     static constexpr int CHW = WS >= 3 ? 3 : WS;       // the chain wave (waves go to SIMDs 0,2,1,3,0,2,1: wave 3
                                                        // has a SIMD of its own for WS = 3 and WS = 6)
     static constexpr int NB = S / 8;                   // chain blocks of 8 steps
     static_assert(TQ >= KAHEAD + 2, "table ring: a window's records are read until its stores");
-    static_assert(NR == 4 && R + 2 <= NR && 8 * (S + 1) * 16 <= STG_RING,
-                  "forwarding ring: codes carry (g - dW) mod 4 for dW = 2 .. R+3");
-    static_assert(U % NI == 0 && U % NS == 0, "unroll");
+    static_assert(U % NI == 0 && U % NS == 0 && U % 3 == 0, "unroll");
 };
 
 template <int WS, int R>
 struct alignas(16) Smem3 {
     using CF = Cfg<WS, R>;
     static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
-    uint4 stg[NR][STG_RING / 16];     // new V of a window, [record entry * (S + 1) + slot] x 16 codewords (int8,
-                                      // entries padded: the stores' reads of 8 entries are conflict-free): the
-                                      // V stores' staging and the forwarding ring (ring slot g % NR, 8 KB apart
-                                      // so that a forwarding code + (g << 13) addresses its entry)
+    uint4 lc[LC_SLOTS][8];            // line cache: slot = 8 V rows x 16 codewords (LcPlan; slot 0: the sink)
+    uint4 stg[NR][2][S + 1];          // parity V of a window, [x edge / the tail's last edge][slot] x 16
+                                      // codewords (int8): the stores' staging
     uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
     uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post)
     struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
-        uint4 a[8][8];                //   [0..5][slot] V rows (info edges, record entry D0-1), [6..7][slot] message
-                                      //   0..31 B
-        uint4 pad[4];                 //   (rows 6, 7 and b[0], b[1] in different banks)
-        uint4 b[2][8];                //   [0..1][slot] message 32..63 B
-    } in[WS][NI];                     // (entry-major: the 8 slots of one read are in different banks)
-    static constexpr uint32_t IN_B = sizeof(uint4) * (8 * 8 + 4);   // byte offset of In::b
+        uint4 d[5][8];                //   e < 4: message bytes 16e .. 16e+15, e = 4: the o-edge parity row
+    } in[WS][NI];
     uint4 mst[WS][8][4];              // new messages of a window per slab wave, [slot] x 64 B
-    uint4 et_spare[320];              // early termination: between segments the whole struct holds the
-                                      // hard bits of every variable (u16 x 64800 for DVB-S2; one
-                                      // workgroup per CU either way)
 };
 
 struct Coop3Args {
-    int8_t *V;                        // V[n + 1][pitch]; row n is the sink of inactive slots
+    int8_t *V;                        // grouped V: Vg[group][row][16], groups gstride bytes apart; row n (and the
+                                      // sink line n / 8) is the sink of inactive slots and unused line ops
     uint8_t *Mc;                      // [pitch / 16][mrows][8 pairs][2] u32; row m is the sink
     const uint32_t *tab;              // [nw][S][RECW] slot records
+    const uint32_t *lc_pro, *lc_epi;  // line cache: resident lines at a segment start / written back at its end
     unsigned long long *stamps;       // diagnostic build: [grid][waves][4]
-    const uint8_t *live;              // early termination: [pitch] 0 = converged (NULL: all live)
-    int8_t *P;                        // parity rows k + j at P[group][j], j <= m (DecodeLaunch::P)
     // in-kernel early termination (ET kernels): layered edge list (group 0:
-    // checks [0, m0) of degree D0, then degree d1), snapshot V [n][pitch],
-    // iterations used per codeword
+    // checks [0, m0) of degree D0, then degree d1), iterations used per codeword
     const uint32_t *ev;
-    int8_t *Vs;
     int32_t *iters_used;
-    int iters, batch, m0, d1;
-    int pitch, G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
+    int iters, batch, m0, d1, n_pro, n_epi;
+    int G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
     uint32_t nmsf;                    // NMS factor per half (value form)
-    size_t wgoff;                     // bytes between two codeword groups' V (16)
+    size_t gstride;                   // bytes between two codeword groups' V
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
 };
 
@@ -145,9 +147,10 @@ struct St3 {                          // one window's state from pre to post (R 
 
 // record meta (word D0): check | COOP_M_ACT | chain step << STEP_SHIFT.  The
 // host permutes a window's checks over its slots (coop3_upload: every
-// distance-2 forwarding source and reader in slab wave 0); the chain runs the
-// steps in check order, so a slot's constants / x input sit at its step
+// distance-2 writer and reader in slab wave 0); the chain runs the steps in
+// check order, so a slot's constants / x input sit at its step
 constexpr int STEP_SHIFT = 22;
+static_assert(W_META == D0, "meta word");
 
 LDPC_DEV uint32_t pk_ashr8(uint32_t a) { return us(sv(a) >> (short)8); }
 LDPC_DEV uint32_t pk_add(uint32_t a, uint32_t b) { return us(sv(a) + sv(b)); }
@@ -161,19 +164,20 @@ LDPC_DEV uint32_t nms_v(uint32_t r, uint32_t f) { return us(__builtin_bit_cast(s
 LDPC_DEV uint32_t nms_c(uint32_t r, uint32_t f) { return (pk_mul_lo(pk_ashr8(r), f) << 3) & HIBYTES; }   // (<= 4032 << 3: no carry between halves)
 LDPC_DEV uint32_t pk_shl5(uint32_t a) { return us(sv(a) << (short)5); }
 
-// what a period reads from LDS, issued together at its start
+// a window's records of one slot as a pre reads them: info pieces 0..3, and
+// (piece 4, x row, o row, meta)
+struct Rec {
+    uint4 pc, pm;
+};
+// what a pre reads from LDS
 struct PreIn {
-    uint32_t v[D0 - 1];               // raw V dwords (info edges, entry D0-1)
+    uint32_t v[D0 - 1];               // raw V dwords (info edges from the line cache, the o edge from In)
     uint32_t ma, mb;                  // old message record of this pair
-    uint4 mf;                         // record words D0 .. D0+3: meta, forwarding codes (read a period early)
-    uint32_t fv[X];                   // forwarded V pairs (raw u16) of the info edges with a forwarding code
+    uint32_t meta;
 };
-struct StIn {                         // the stores of window p-2
-    uint4 vd, md;                     // staged V row piece (16 codewords), message piece
-    uint32_t row, chk;                // record entry q of the slot, its meta
-};
-struct PfIn {                         // the LDS-DMA gathers of window p+1+R
-    uint32_t rv, chk2;
+struct StIn {                         // the store of window p-2: one 16-B piece per lane
+    uint4 d;
+    char *addr;
 };
 
 template <int WS, int R, bool NMS = false>
@@ -182,62 +186,65 @@ struct Slab3 {
     static constexpr int S = SM::S, NR = SM::NR;
     SM &sm;
     const Coop3Args &a;
-    char *vsb;                        // V row store of record entry q: vsb + row * vsm (the parity entries
-    uint32_t vsm;                     //   q >= X go to the parity rows' own layout P, see Coop3Args)
-    i32x4 mr;                         // message rows in 16-B units
     int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
     uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
-    uint32_t fsel;                    // ... of a forwarded u16 (0x050d040d, in a VGPR)
     PkK K;
     uint32_t fk;                      // NMS factor per half (value form)
-    // per-lane constants of the LDS-DMA gathers (lane (kl, j): j < 6 a V row, j >= 6 a message piece)
-    const char *g1base, *g2base;
-    uint32_t g1mul, g1mask, recsel;
-    uint32_t vrd, mrd;                // byte offsets of this lane's V dword / message pair in an In record
+    char *Vg;                         // the group's V rows (16 B each; parity row k + j at Pr + 16 j)
+    // LDS byte offsets of this lane inside a line-cache piece: the pre's V
+    // dword (4 (q >> 1)), the post's u16 (2 q), and a line op's 16-B piece (16 q)
+    uint32_t lrd, lwr, lq;
+    // gathers, lane (e, slot) = (lane >> 3, lane & 7): e < 4 message piece e of
+    // the slot's check, e = 4 its o-edge parity row, e > 4 idle
+    const char *gbase;
+    uint32_t gmul, gmask, gsel;
+    // stores, lane (kl, q): q < 4 message piece q, q = 4 the x-edge parity
+    // row, q = 5 the tail's last edge (else the sink row)
+    char *sbase;
+    uint32_t smul;
+    uint32_t mrd, prd;                // byte offsets in an In record: this lane's message pair / o-edge V dword
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
 
+    LDPC_DEV const char *lcb() const { return (const char *)&sm.lc[0][0]; }
+    LDPC_DEV char *lcw() const { return (char *)&sm.lc[0][0]; }
+
     // ---- reads
-    // in.mf = mfc (window g's codes, read in the previous period); mfn <- window g+1's
-    LDPC_DEV void read_pre(int g, int ib, PreIn &in, const uint4 &mfc, uint4 &mfn) const
+    LDPC_DEV Rec read_rec(int g) const
+    {
+        const uint4 *r = (const uint4 *)&sm.tab[g & (TQ - 1)][k][0];
+        return {r[0], r[1]};
+    }
+    LDPC_DEV uint2 read_lop(int g) const { return *(const uint2 *)&sm.tab[g & (TQ - 1)][k][W_LOP]; }
+    // pre inputs of the window whose records are rc (its gathers landed in in[w][ib])
+    LDPC_DEV void read_pre(int ib, const Rec &rc, PreIn &in) const
     {
         const char *inb = (const char *)&sm.in[w][ib];
-#pragma unroll
-        for (int j = 0; j < D0 - 1; j++) in.v[j] = *(const uint32_t *)(inb + vrd + 128 * j);
+        in.v[0] = *(const uint32_t *)(lcb() + rc.pc.x + lrd);
+        in.v[1] = *(const uint32_t *)(lcb() + rc.pc.y + lrd);
+        in.v[2] = *(const uint32_t *)(lcb() + rc.pc.z + lrd);
+        in.v[3] = *(const uint32_t *)(lcb() + rc.pc.w + lrd);
+        in.v[4] = *(const uint32_t *)(lcb() + rc.pm.x + lrd);
+        in.v[X] = *(const uint32_t *)(inb + prd);
         const uint2 mm = *(const uint2 *)(inb + mrd);
         in.ma = mm.x;
         in.mb = mm.y;
-        in.mf = mfc;
-        mfn = read_mf(g + 1);
+        in.meta = rc.pm.w;
     }
-    LDPC_DEV uint4 read_mf(int g) const { return *(const uint4 *)&sm.tab[g & (TQ - 1)][k][D0]; }
-    // forwarded values of window g's info edges: code j (16 bits, fwd_code3)
-    // = ((-dW) mod 4) << 13 | stage offset | near << 1 | use; code + (g << 13)
-    // carries ring slot (g - dW) mod 4 in bits 13-14.  Unused codes read
-    // ring offset 0 (ignored).  Branch-free: 2 VALU + 1 ds_read_u16 per edge.
-    LDPC_DEV void fwd_read(int g, PreIn &in) const
+    // the store of window g (tl: the tail window): address and 16-B piece of this lane
+    LDPC_DEV void read_st(int g, bool tl, StIn &in) const
     {
-        const char *sbase = (const char *)&sm.stg[0][0];
-        const uint32_t gs = (uint32_t)__builtin_amdgcn_readfirstlane(g << 13), q2 = 2u * (uint32_t)q;
-        const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
-#pragma unroll
-        for (int j = 0; j < X; j++) {
-            const uint32_t code = (j & 1) ? fw[j >> 1] >> 16 : fw[j >> 1] & 0xFFFFu;
-            in.fv[j] = *(const unsigned short *)(sbase + (((code + gs) & 0x7FF0u) | q2));
-        }
+        const uint32_t *r = &sm.tab[g & (TQ - 1)][k][0];
+        const uint32_t idx = q < 4 ? (r[W_META] & COOP_CHK_MASK) : q == 4 ? r[W_X] : (q == 5 && tl) ? r[W_O]
+                                                                                                : (uint32_t)a.m;
+        in.addr = sbase + (size_t)idx * smul;
+        const char *src = q < 4 ? (const char *)&sm.mst[w][kl][q] : (const char *)&sm.stg[g % NR][q == 4 ? 0 : 1][k];
+        in.d = *(const uint4 *)src;
     }
-    LDPC_DEV void read_st(int g, StIn &in) const
+    LDPC_DEV uint32_t read_gidx(int g) const   // the gather's row / check of window g (lane (e, slot))
     {
-        in.vd = sm.stg[g % NR][q * (S + 1) + k];
-        in.md = sm.mst[w][kl][q & 3];
-        in.row = sm.tab[g & (TQ - 1)][k][q];
-        in.chk = sm.tab[g & (TQ - 1)][k][D0] & COOP_CHK_MASK;
-    }
-    LDPC_DEV void read_pf(int g, PfIn &in) const
-    {
-        in.rv = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][recsel] & g1mask;
-        in.chk2 = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][D0] & COOP_CHK_MASK;
+        return sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
     }
     LDPC_DEV uint32_t read_x(int g, const St3 &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
@@ -246,53 +253,31 @@ struct Slab3 {
         return perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127]
     }
 
-    // ---- memory operations at the end of a period
-    // lane (kl, c): record entry c's 16 codewords (c < 6, the tail 7) and
-    // message piece c (c < 4) of its wave's slot kl
-    LDPC_DEV void stores(const StIn &in, bool tl) const
+    // ---- vector memory (every op unconditional and 64 lanes wide: unused
+    // lanes go to the sink row / line / slot, so the per-period vmcnt counts
+    // are static)
+    LDPC_DEV void stores(const StIn &in) const { *(uint4 *)in.addr = in.d; }
+    LDPC_DEV void gathers(uint32_t idx, int ib) const
     {
-        if (q < (tl ? D0 : D0 - 1)) *(uint4 *)(vsb + (size_t)in.row * vsm) = in.vd;
-        if (q < 4) sbuf_store_v4(__builtin_bit_cast(i32x4, in.md), mr, (int)(in.chk * 4 + q), 0, 0, 0);
-    }
-    LDPC_DEV void gathers(const PfIn &in, int ib) const
-    {
-        static_assert(offsetof(typename SM::In, b) == SM::IN_B, "In layout");
         const uint32_t base = (uint32_t)(uintptr_t)&sm.in[w][ib];
-        dma16(g1base + (size_t)in.rv * g1mul, base);
-        if (lane < 16) dma16(g2base + (size_t)in.chk2 * MREC, base + SM::IN_B);
+        if (lane < 40) dma16(gbase + (size_t)idx * gmul, base);
     }
-
-    // the first windows of the decode: a code whose source window precedes
-    // window 0 (g < dW) is not used
-    LDPC_DEV static void mask_early(int g, uint4 &mf)
-    {
-        uint32_t *fw = &mf.y;
-#pragma unroll
-        for (int i = 0; i < 3; i++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t code = (fw[i] >> (16 * h)) & 0xFFFFu;
-                const int dw = (int)(((0u - (code >> 13) - 2u) & 3u) + 2u);
-                if ((code & 1u) && g < dw) fw[i] &= ~(1u << (16 * h));
-            }
-    }
+    // line cache: writeback of period p (slot -> VGPRs, then HBM), load of
+    // period p (HBM -> VGPRs), slot write of the load of period p-2
+    LDPC_DEV uint4 wb_read(uint2 lop) const { return *(const uint4 *)(lcb() + (lop.y >> 16) * 128u + lq); }
+    LDPC_DEV void wb_store(uint2 lop, const uint4 &d) const { *(uint4 *)(Vg + (size_t)(lop.x >> 16) * 128 + lq) = d; }
+    LDPC_DEV uint4 line_load(uint2 lop) const { return *(const uint4 *)(Vg + (size_t)(lop.x & 0xFFFFu) * 128 + lq); }
+    LDPC_DEV void line_put(uint2 lop, const uint4 &d) const { *(uint4 *)(lcw() + (lop.y & 0xFFFFu) * 128u + lq) = d; }
 
     // pre of window g: chain constants -> cst[g & 1], state -> s
     template <bool TL, bool FZ_ = false, int MP = -1>
     LDPC_DEV void pre(int g, const PreIn &in, St3 &s) const
     {
         constexpr bool FZ = FZ_;
-        const uint32_t meta = in.mf.x;
+        const uint32_t meta = in.meta;
         uint32_t v[D0 - 1];
-        // V pair of edge j: this pair's two bytes of the loaded V dword, or the
-        // forwarded u16 (selector 0x050d040d: bytes 0, 1 of in.fv[j] -> R pair)
-        const uint32_t fw[3] = {in.mf.y, in.mf.z, in.mf.w};
 #pragma unroll
-        for (int j = 0; j < X; j++) {
-            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)fw[j >> 1], 16 * (j & 1), 1);   // 0 / -1
-            v[j] = perm(in.fv[j], in.v[j], bfi(m, fsel, usel));
-        }
-        v[X] = unpack_v(in.v[X], usel);
+        for (int j = 0; j <= X; j++) v[j] = unpack_v(in.v[j], usel);
         const MsgTab t = msg_tab(in.mb);
         const uint32_t MA = in.ma, neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
@@ -411,14 +396,18 @@ struct Slab3 {
         cp[NP] = r1;
     }
 
-    // post of window g (x inputs xr): new V pairs -> stg[g % NR], messages ->
-    // mst[w]; they leave in the stores of the same period
+    // post of window g (x inputs xr, records rc): new info V pairs -> the line
+    // cache, parity V -> stg[g % NR], messages -> mst[w]; the last two leave
+    // in the store of period g + 2
     template <bool TL, bool FZ_ = false, int MP = -1>
-    LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
+    LDPC_DEV void post(int g, uint32_t xr, const St3 &s, const Rec &rc) const
     {
         constexpr bool FZ = FZ_;
-        unsigned short *st = (unsigned short *)&sm.stg[g % NR][k];   // [entry][..S slots..][8 pairs] u16
-        constexpr int ES = (S + 1) * 8;                                 // u16 between entries
+        unsigned short *sx = (unsigned short *)&sm.stg[g % NR][0][k] + q, *so = (unsigned short *)&sm.stg[g % NR][1][k] + q;
+        const uint32_t pcs[X] = {rc.pc.x, rc.pc.y, rc.pc.z, rc.pc.w, rc.pm.x};
+        auto put = [&](int j, uint32_t v) __attribute__((always_inline)) {
+            *(unsigned short *)(lcw() + pcs[j] + lwr) = (unsigned short)v;
+        };
         uint32_t MA, MB;
         if constexpr (!TL) {
             const uint32_t cx = pk_max(pk_sub_sat(xr, s.mx), K.neg127);
@@ -431,30 +420,25 @@ struct Slab3 {
                                     : pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0) & HIBYTES;
             const uint32_t P = (sacc ^ ((D0 & 1) ? SIGNS : 0u)) & SIGNS;
             MA = 0;
-            uint32_t nv[X + 1];
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
                 const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
-                nv[J] = FZ ? perm(n, s.v[J], psel) : pack_v(n);   // FZ: pack_v of new / old per codeword
+                put(J, FZ ? perm(n, s.v[J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
             const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127);
-            nv[X] = FZ ? perm(nx, xr, psel) : pack_v(nx);
+            *sx = (unsigned short)(FZ ? perm(nx, xr, psel) : pack_v(nx));
             // the o edge: message bits only (the next check rewrites V[o] as its x edge)
             (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
             MB = perm(k2, k1, 0x07030501u);
-#pragma unroll
-            for (int j = 0; j <= X; j++) st[j * ES + q] = (unsigned short)nv[j];
         } else {
-            {
-                static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
-                    constexpr int J = decltype(jc)::value;
-                    st[J * ES + q] = (unsigned short)pack_v(s.c[J]);
-                });
-                st[X * ES + q] = (unsigned short)pack_v(xr);               // V of the last group-0 check's o edge
-                st[(D0 - 1) * ES + q] = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
-            }
+            static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int J = decltype(jc)::value;
+                put(J, pack_v(s.c[J]));
+            });
+            *sx = (unsigned short)pack_v(xr);       // V of the last group-0 check's o edge
+            *so = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
             MA = s.mn1;
             MB = s.mn2;
         }
@@ -570,12 +554,12 @@ LDPC_DEV uint32_t high_bits16(uint4 x)   // byte high bits -> 16-bit codeword ma
 }
 // Wave CHW: the chain; the others: slab waves (slab index w: slots 8w .. 8w+7).
 // ET: in-kernel early termination -- the decode runs one iteration per
-// segment (pipeline drained at its end), then the whole workgroup checks the
-// syndrome of its live codewords (stopping once each has a failing check),
-// snapshots the V of the codewords converging now, and leaves when none is
-// live; the snapshots are merged back at the end.  Same result as the
-// reference's per-codeword stop (oracle: syndrome after every iteration), with
-// one launch instead of one per iteration plus syndrome / snapshot kernels.
+// segment (pipeline drained and the line cache written back at its end), then
+// the whole workgroup checks the syndrome of its live codewords (stopping once
+// each has a failing check), records the iterations of the codewords
+// converging now and freezes them, and leaves when none is live.  Same result
+// as the reference's per-codeword stop (oracle: syndrome after every
+// iteration), in one launch.
 template <int WS, int R, bool STAMP, bool ET = false, bool NMS = false>
 __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
 {
@@ -590,37 +574,11 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
     const int G = ET ? a.nw : a.G;   // periods per segment (ET: one iteration)
     if (G == 0) return;
-    if (!ET && a.live && !__syncthreads_or(threadIdx.x < CW && a.live[wg * CW + threadIdx.x])) return;
-    // the group's parity rows -> P (consecutive checks' parity values
-    // contiguous: a wave's 8 o-edge gathers / x-edge stores touch 1-2 lines,
-    // not 8), back into V at the end
-    {
-        int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * a.wgoff;
-        int8_t *ppar = a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
-#pragma unroll 8
-        for (int j = threadIdx.x; j < a.m; j += blockDim.x)
-            *(uint4 *)(ppar + 16 * (size_t)j) = *(const uint4 *)(vpar + (size_t)j * (size_t)a.pitch);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    auto parity_out = [&]() {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int8_t *vpar = a.V + (size_t)a.k * (size_t)a.pitch + (size_t)wg * a.wgoff;
-        const int8_t *ppar = a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
-#pragma unroll 8
-        for (int j = threadIdx.x; j < a.m; j += blockDim.x)
-            *(uint4 *)(vpar + (size_t)j * (size_t)a.pitch) = *(const uint4 *)(ppar + 16 * (size_t)j);
-    };
+    char *Vg = (char *)a.V + (size_t)wg * a.gstride;
     // ---- ET state: [0] live codewords, [1] failing codewords (syndrome)
     __shared__ uint32_t et_sh[2];
     constexpr int NT = 64 * (WS + 1);
-    const char *etV = (const char *)a.V + (size_t)wg * a.wgoff;
-    const char *etP = (const char *)a.P + (size_t)wg * (size_t)(a.m + 1) * 16;
-    auto et_row = [&](uint32_t v) -> const uint4 * {   // V row piece of variable v (parity rows: in P)
-        return ((int)v < a.k) ? (const uint4 *)(etV + (size_t)v * (size_t)a.pitch)
-                            : (const uint4 *)(etP + (size_t)(v - (uint32_t)a.k) * 16);
-    };
+    auto et_row = [&](uint32_t v) -> const uint4 * { return (const uint4 *)(Vg + (size_t)v * 16); };
     if constexpr (ET) {
         if (threadIdx.x == 0) {
             const int valid = min(CW, max(0, a.batch - wg * CW));
@@ -682,7 +640,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         return (fail & live) == live;
     };
     auto et_after = [&](int it) -> bool {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the iteration's stores and table DMAs
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the iteration's stores, writebacks and table DMAs
         __syncthreads();
         const uint32_t live = et_sh[0];
         // round 0: one check per thread, gathered directly -- threads 0..63
@@ -700,30 +658,19 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             // the full syndrome: every variable's hard bits staged in LDS (the
             // pipeline's LDS is idle between segments; the launch checks n
             // fits), then the checks, 8 per thread and round with an exit
-            // test after each; loads unconditional (clamped check index) so a
-            // round's index loads are in flight together
+            // test after each; loads unconditional (clamped index) so a
+            // round's loads are in flight together
             uint16_t *hb = reinterpret_cast<uint16_t *>(&sm);
-            // (16 unconditional loads in flight per thread: clamped rows)
             auto hbits = [](uint4 y) {
                 return (uint16_t)high_bits16(make_uint4(pos_bits(y.x), pos_bits(y.y), pos_bits(y.z), pos_bits(y.w)));
             };
-            for (int r0 = 0; r0 < a.k; r0 += NT * 16) {   // information rows: V
+            for (int r0 = 0; r0 < a.n; r0 += NT * 16) {
                 uint4 y[16];
 #pragma unroll
-                for (int i = 0; i < 16; i++)
-                    y[i] = *(const uint4 *)(etV + (size_t)min(r0 + i * NT + (int)threadIdx.x, a.k - 1) * (size_t)a.pitch);
+                for (int i = 0; i < 16; i++) y[i] = *et_row((uint32_t)min(r0 + i * NT + (int)threadIdx.x, a.n - 1));
 #pragma unroll
                 for (int i = 0; i < 16; i++)
-                    if (r0 + i * NT + (int)threadIdx.x < a.k) hb[r0 + i * NT + threadIdx.x] = hbits(y[i]);
-            }
-            for (int r0 = 0; r0 < a.m; r0 += NT * 16) {   // parity rows: P
-                uint4 y[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++)
-                    y[i] = *(const uint4 *)(etP + (size_t)min(r0 + i * NT + (int)threadIdx.x, a.m - 1) * 16);
-#pragma unroll
-                for (int i = 0; i < 16; i++)
-                    if (r0 + i * NT + (int)threadIdx.x < a.m) hb[a.k + r0 + i * NT + threadIdx.x] = hbits(y[i]);
+                    if (r0 + i * NT + (int)threadIdx.x < a.n) hb[r0 + i * NT + threadIdx.x] = hbits(y[i]);
             }
             __syncthreads();
             bool done = false;
@@ -806,10 +753,10 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             for (int w = 0; w < KAHEAD; w++) stage(w % a.nw, w);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             uint32_t w4[4] = {0, 0, 0, 0};
-            // the chain's first input V[x0] (a parity row: in P during the decode)
+            // the chain's first input V[x0] (a parity row)
             w4[0] = (uint32_t)(int)((const int8_t *)et_row((uint32_t)a.x0))[c] & 0xFFFFu;
             int un = KAHEAD % a.nw;
-            __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 in LDS
+            __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 and the resident lines in LDS
             __syncthreads();   // prologue 2: constants of window 0 in LDS
             if (STAMP) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
@@ -822,29 +769,26 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 if (STAMP) sA += stamp3() - tx;
                 __syncthreads();
             }
+            __syncthreads();   // epilogue: the slab waves' line writebacks read the cache
             if (!ET || !et_after(it)) break;
         }
         write_stamps();
-        parity_out();
         return;
     }
 
     // ------------------------------------------------------------ slab waves
     const int sw = wave - (wave > CHW ? 1 : 0);   // slab index
+    constexpr int NSL = 64 * WS;                  // slab threads
+    const int st_id = sw * 64 + lane;
     // the second-dispatched half of the slab waves loses VALU arbitration to
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
     const int kl = lane >> 3, q = lane & 7;
-    const char *Vb = (const char *)a.V + (size_t)wg * a.wgoff;
     const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
-    // parity rows k + j of this group at Pb + 16 j: row r at Pb - 16 k + 16 r
-    char *Pr = (char *)a.P + ((size_t)wg * (size_t)(a.m + 1) - (size_t)a.k) * 16;
+    char *Pr = Vg + (size_t)a.k * 16;   // parity row k + j at Pr + 16 j (row n: the sink)
     Slab3<WS, R, NMS> sl{sm,
                     a,
-                    q >= X ? Pr : (char *)Vb,
-                    q >= X ? 16u : (uint32_t)a.pitch,
-                    buffer_rsrc(Mb, 16u, (uint32_t)a.mrows * 4u),
                     8 * sw + kl,
                     kl,
                     q,
@@ -852,24 +796,33 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     lane,
                     a.tail,
                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
-                    opaque(0x050d040du),
                     PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
                     opaque(a.nmsf),
-                    // DMA lane 8e + slot: entry e < 6 a V row (record entry e, the
-                    // o edge's D0-1 for e = X), e >= 6 message piece e - 6
-                    kl < X ? Vb : kl == X ? Pr : Mb + (kl - 6) * 16,
-                    Mb + (2 + (kl & 1)) * 16,
-                    kl < X ? (uint32_t)a.pitch : kl == X ? 16u : (uint32_t)MREC,
-                    kl < 6 ? 0xFFFFFFFFu : COOP_CHK_MASK,
-                    (uint32_t)(kl < X ? kl : (kl == X ? D0 - 1 : D0)),
-                    (uint32_t)(kl * 16 + 4 * (q >> 1)),
-                    (uint32_t)(q < 4 ? (6 + (q >> 1)) * 128 + kl * 16 + (q & 1) * 8
-                                     : SM::IN_B + ((q >> 1) - 2) * 128 + kl * 16 +
-                                           (q & 1) * 8)};
+                    Vg,
+                    (uint32_t)(4 * (q >> 1)),
+                    (uint32_t)(2 * q),
+                    (uint32_t)(16 * q),
+                    // gathers: lane (e, slot) = (kl, q) here
+                    kl < 4 ? Mb + kl * 16 : (const char *)Pr,
+                    kl < 4 ? (uint32_t)MREC : 16u,
+                    kl < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu,
+                    (uint32_t)(kl < 4 ? W_META : W_O),
+                    // stores
+                    q < 4 ? (char *)Mb + q * 16 : Pr,
+                    q < 4 ? (uint32_t)MREC : 16u,
+                    (uint32_t)(((q >> 1) * 8 + kl) * 16 + (q & 1) * 8),
+                    (uint32_t)((32 + kl) * 16 + 4 * (q >> 1))};
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     constexpr int NI = CF::NI, NS = CF::NS;
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
-        __syncthreads();   // prologue 1: tables in LDS
+        // line cache prologue: the lines resident at a segment start (LcPlan::pro)
+        for (int i = st_id; i < 8 * a.n_pro; i += NSL) {
+            const uint32_t pw = a.lc_pro[i >> 3];
+            const uint32_t piece = (uint32_t)(i & 7) * 16u;
+            *(uint4 *)((char *)&sm.lc[0][0] + (pw >> 16) * 128u + piece) =
+                *(const uint4 *)(Vg + (size_t)(pw & 0xFFFFu) * 128 + piece);
+        }
+        __syncthreads();   // prologue 1: tables and resident lines in LDS
         if constexpr (ET) {   // codewords 2q (low half) and 2q+1 (high half) of this lane: converged?
             const int valid = min(CW, max(0, a.batch - wg * CW));
             const uint32_t conv = (((1u << valid) - 1u) & ~et_sh[0]) >> (2 * q);
@@ -877,103 +830,108 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             sl.psel = 0x0c0c0000u | ((conv & 2u) ? 0x0300u : 0x0700u) | ((conv & 1u) ? 0x01u : 0x05u);
         }
         St3 st[NS];
-        uint4 mfc;   // records D0 .. D0+3 of the next pre's window
-        PfIn pi;
+        uint4 pend[3];   // line loads of periods p-2, p-1, p (written to their slots in period p+2)
 #pragma unroll
-        for (int i = 0; i <= R; i++) {   // window i -> in[w][i]   (nw > R + 3)
-            sl.read_pf(i, pi);
-            sl.gathers(pi, i);
-        }
+        for (int i = 0; i < 3; i++) pend[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i <= R; i++) sl.gathers(sl.read_gidx(i), i);   // window i -> in[w][i]   (nw > R + 3)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         PreIn in;
-        sl.read_pre(0, 0, in, sl.read_mf(0), mfc);
-        sl.mask_early(0, in.mf);
-        sl.fwd_read(0, in);
+        Rec rcn = sl.read_rec(1 % a.nw);   // records of the next pre's window
+        sl.read_pre(0, sl.read_rec(0), in);
         if (a.tail == 0)
             sl.template pre<true, ET>(0, in, st[0]);
         else
             sl.template pre<false, ET>(0, in, st[0]);
+        uint2 lop = sl.read_lop(0);   // line ops of the next period
         __syncthreads();   // prologue 2
         if (STAMP) t0 = stamp3();
         int uA = a.nw - 1;   // local index of window p-1 (post)
         int uB = 1 % a.nw;   // local index of window p+1 (pre)
-        StIn sc;             // the stores of window p-2 (read from the stage at the end of period p-1)
+        StIn sc;             // the store of window p-2 (read from the stage at the end of period p-1)
+        sc.addr = Pr + (size_t)a.m * 16;
         bool sc_tl = false;  // ... window p-2 is the tail
         // Period p: post of window p-1 (state st[(p-1) % NS], x inputs from the
-        // chain's window p-1) -> staged outputs; pre of window p+1 (inputs
-        // in[w][(p+1) % NI], -> st[(p+1) % NS]).  Vector memory: the two stores of
-        // window p-2 go first, the two LDS-DMA gathers of window p+1+R into
-        // in[w][(p+1+R) % NI] follow the first half, so no wave ends a period
-        // queueing behind the workgroup's stores (the CU's vector-memory issue is
-        // what bounds this kernel at the end of a period).
-        // The plan only keeps neighbouring windows free of shared information
-        // variables (dist 1): a value window p+1 reads may have been written by
-        // the post of window p-1 in this same period.  The host puts every such
-        // source and reader in slab wave 0, which posts before its pre and reads
-        // those values back from its own stage (LDS keeps a wave's order); the
-        // other waves run their pre first, so their x inputs arrive behind it.
-        // A value is stored at the start of the second period after its window's
-        // chain, so reads 2 .. R+3 windows later are forwarded (plan depth R + 2).
-        // The gathers of window p+1 were the last vector memory operations of
-        // period p-R, followed by 4 in each later period: in the main loop (every
-        // period does everything, no tail window) vmcnt(4(R-1)) covers them.
+        // chain's window p-1, info V into the line cache); pre of window p+1
+        // (inputs from the line cache and in[w][(p+1) % NI], -> st[(p+1) % NS]).
+        // Vector memory, in this order every period (the counts are static, so
+        // that vmcnt(6) before the pre is the gathers of window p+1 and the
+        // line loads of period p-2): the store of window p-2 (messages + parity
+        // rows), the line writeback of period p, the LDS-DMA gathers of window
+        // p+1+R, the line load of period p.  The plan only keeps neighbouring
+        // windows free of shared information variables (dist 1): a value window
+        // p+1 reads may have been written by the post of window p-1 in this same
+        // period; the host puts every such writer and reader in slab wave 0,
+        // which posts before its pre (LDS keeps a wave's order).
         constexpr int MP1 = -1, MP2 = -1;   // mid-phase priorities (none: quarter-period levels measured the same)
         const bool fair = a.slab_prio == 2;
         auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
             constexpr bool GU = decltype(guarded)::value;
             if (STAMP) tx = stampL();
-            const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G, dst = p >= 2 && p <= G + 1;
+            const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
             const bool fast = !GU && uA != a.tail && uB != a.tail && !sc_tl;
             PreIn in;
-            PfIn pi;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
+            const Rec rcp = sl.read_rec(p - 1);     // the post's records
+            const uint4 wbd = sl.wb_read(lop);      // the writeback's line piece (posts up to p-1 wrote it)
+            // every period issues the same four vector memory operations in
+            // the same order, guarded or not (unused ones on the sinks), so
+            // both vmcnt(6) here and the compiler's own waits for the line
+            // loads count exactly
+            uint32_t gi = (uint32_t)a.m;            // gathers of window p+1+R (sink rows when there is none)
+            uint32_t xr = 0;
             if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
-                // state in VGPRs, nothing from memory) and waits for its window
-                // p+1 gathers only before its pre, half a period later than at
-                // the period start (the stores of this period are 2 more
-                // operations in flight): 47.6 -> 46.9 ms
+                // state in VGPRs) and waits for its window p+1 gathers and line
+                // loads only before its pre
                 if (fair) __builtin_amdgcn_s_setprio(1);
-                sl.stores(sc, false);
-                const uint32_t xr = sl.read_x(p - 1, sp);
-                sl.read_pf(p + 1 + R, pi);
-                constexpr int VMW = 4 * (R - 1) + 2;
-                sl.template post<false, ET, MP1>(p - 1, xr, sp);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMW) : "memory");
-                sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
-                sl.fwd_read(p + 1, in);   // after the stage writes: distance-2 values (wave 0)
-                sl.gathers(pi, (s + R + 1) % NI);
-                sl.read_st(p - 1, sc);
+                sl.stores(sc);
+                xr = sl.read_x(p - 1, sp);
+                gi = sl.read_gidx(p + 1 + R);
+                sl.template post<false, ET, MP1>(p - 1, xr, sp, rcp);
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                sl.stores(sc);   // (the sink before period 2)
+                if (dpo) {
+                    xr = sl.read_x(p - 1, sp);
+                    if (uA == a.tail)
+                        sl.template post<true, ET>(p - 1, xr, sp, rcp);
+                    else
+                        sl.template post<false, ET>(p - 1, xr, sp, rcp);
+                }
+                if (dpr) gi = sl.read_gidx(p + 1 + R);
+            }
+            sl.wb_store(lop, wbd);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // gathers of window p+1, line loads of period p-2
+            sl.line_put(lop, pend[(s + 1) % 3]);
+            if (fast || dpr) sl.read_pre((s + 1) % NI, rcn, in);
+            sl.gathers(gi, (s + R + 1) % NI);
+            pend[s] = sl.line_load(lop);
+            if (fast) {
+                sl.read_st(p - 1, false, sc);
+                rcn = sl.read_rec(p + 2);
+                lop = sl.read_lop(p + 1);
                 if (STAMP) t1 = t2 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(0);
                 sl.template pre<false, ET, MP2>(p + 1, in, sn);
                 if (STAMP) t3 = stampL();
             } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (dst) sl.stores(sc, sc_tl);
-                if (dpo) {
-                    if (uA == a.tail)
-                        sl.template post<true, ET>(p - 1, sl.read_x(p - 1, sp), sp);
-                    else
-                        sl.template post<false, ET>(p - 1, sl.read_x(p - 1, sp), sp);
-                }
                 if (STAMP) t1 = t2 = t3 = stampL();
                 if (dpo) {
-                    sl.read_st(p - 1, sc);
+                    sl.read_st(p - 1, uA == a.tail, sc);
                     sc_tl = uA == a.tail;
+                } else {
+                    sc.addr = Pr + (size_t)a.m * 16;
                 }
+                rcn = sl.read_rec(p + 2);
+                lop = sl.read_lop(p + 1);
                 if (dpr) {
-                    sl.read_pre(p + 1, (s + 1) % NI, in, mfc, mfc);
-                    if (p + 1 < R + 3) sl.mask_early(p + 1, in.mf);
-                    sl.fwd_read(p + 1, in);
-                    sl.read_pf(p + 1 + R, pi);
                     if (uB == a.tail)
                         sl.template pre<true, ET>(p + 1, in, sn);
                     else
                         sl.template pre<false, ET>(p + 1, in, sn);
-                    sl.gathers(pi, (s + R + 1) % NI);
                 }
             }
             if (STAMP) {
@@ -991,8 +949,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         };
         using T = std::true_type;
         using F = std::false_type;
-        // periods 0 .. U guarded (their pres drop codes whose source window
-        // precedes window 0: U + 2 >= R + 3, the largest forwarding distance)
+        // periods 0 .. U guarded
         static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
             if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, T{}, decltype(jc)::value);
         });
@@ -1007,11 +964,18 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)
                 period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
         });
-        sl.stores(sc, sc_tl);   // window G-1
+        sl.stores(sc);   // window G-1
+        // line cache epilogue: the dirty lines still resident (LcPlan::epi)
+        __syncthreads();
+        for (int i = st_id; i < 8 * a.n_epi; i += NSL) {
+            const uint32_t pw = a.lc_epi[i >> 3];
+            const uint32_t piece = (uint32_t)(i & 7) * 16u;
+            *(uint4 *)(Vg + (size_t)(pw & 0xFFFFu) * 128 + piece) =
+                *(const uint4 *)((const char *)&sm.lc[0][0] + (pw >> 16) * 128u + piece);
+        }
         if (!ET || !et_after(it)) break;
     }
     write_stamps();
-    parity_out();
 }
 
 __global__ void fill_iters3_k(int batch, int32_t *iters_used, int iters)
@@ -1068,14 +1032,6 @@ int launch_wsr(const Coop3Args &a, int grid, bool stamped, hipStream_t s)
 
 }  // namespace
 
-// forwarding code of a value written dW windows before the reading window,
-// by slot `slot`, record entry e (Slab3::fwd_read): ring slot (g - dW) mod 4 is
-// ((-dW) mod 4 + g) mod 4, entry offset (e * (S + 1) + slot) * 16 < 8192
-static uint32_t fwd_code3(int dW, int slot, int e, int S)
-{
-    return ((uint32_t)(-dW) & 3u) << 13 | (uint32_t)(e * (S + 1) + slot) * 16u | (dW == 2 ? 2u : 0u) | 1u;
-}
-
 // OMS / MS as coop (coop_params_ok); NMS with factor <= 64 (msg_max <= 63: the
 // products fit the i16 halves) at the default WS = 6
 bool coop3_params_ok(const ldpc_params *p, const CoopCode &cc)
@@ -1099,19 +1055,18 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
 {
     o = Coop3Host{};
     if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return 1;
-    if ((ws != 3 && ws != 4 && ws != 6) || r != 2)
-        return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 3 | 4 | 6 and LDPC_COOP3_R 2");
+    if (ws != 6 || r != 2) return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 6 and LDPC_COOP3_R 2");
     const int S = 8 * ws;
     CoopPlan &pl = o.pl;
-    // dist 1 (distance-2 sources and readers share slab wave 0); a value is
-    // stored at the start of the second period after its window's chain, so
-    // reads 2 .. r+3 windows later are forwarded from the LDS stage (plan
-    // prefetch depth r + 2)
+    // dist 1: neighbouring windows share no information variable; the plan's
+    // forwarding codes mark the reads of values written 2 .. r+3 windows
+    // earlier, of which distance 2 (writer's post and reader's pre in the same
+    // period) puts writer and reader in slab wave 0
     if (coop_build_plan(h, S, r + 2, 1, RECW, pl, true) != 0) return 1;
     const int nw = (int)pl.first.size();
     auto rec_at = [&](int u, int k) { return &pl.tab[((size_t)u * S + k) * RECW]; };
     auto code_at = [&](const uint32_t *rec, int j) { return (rec[D0 + 1 + j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
-    // distance-2 forwarding sources and readers -> slab wave 0 (slots 0..7);
+    // distance-2 writers and readers -> slab wave 0 (slots 0..7);
     // the other checks keep their order, the inactive slots come last
     std::vector<char> special((size_t)nw * S, 0);
     for (int u = 0; u < nw; u++)
@@ -1122,7 +1077,7 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
                 special[(size_t)u * S + k] = 1;
                 special[(size_t)((u + nw - 2) % nw) * S + ((f >> 3) & 63)] = 1;
             }
-    std::vector<int> slot_of((size_t)nw * S), check_at((size_t)nw * S);   // plan slot (= chain step) <-> slot
+    std::vector<int> check_at((size_t)nw * S);   // slot -> plan slot (= chain step)
     for (int u = 0; u < nw; u++) {
         int n = 0;
         for (int pass = 0; pass < 3; pass++)
@@ -1130,7 +1085,6 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
                 const bool act = k < pl.count[u], sp = special[(size_t)u * S + k] != 0;
                 if ((pass == 0 && sp) || (pass == 1 && act && !sp) || (pass == 2 && !act)) {
                     if (pass == 0 && n >= 8) return 1;   // more than wave 0 holds: no coop3 schedule
-                    slot_of[(size_t)u * S + k] = n;
                     check_at[(size_t)u * S + n] = k;
                     n++;
                 }
@@ -1142,17 +1096,7 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
             const int k = check_at[(size_t)u * S + kn];
             const uint32_t *src = rec_at(u, k);
             uint32_t *rec = &tab[((size_t)u * S + kn) * RECW];
-            std::copy(src, src + RECW, rec);
-            for (int j = 0; j < 2 * NFW; j++) {   // plan codes -> fwd_code3 (the unused last half: 0)
-                const uint32_t f = j < X ? code_at(src, j) : COOP_FWD_NONE;
-                uint32_t c = 0;
-                if (f != COOP_FWD_NONE) {
-                    const int dw = (int)(f >> 9), uw = (u + nw - dw) % nw;
-                    c = fwd_code3(dw, slot_of[(size_t)uw * S + ((f >> 3) & 63)], (int)(f & 7), S);
-                }
-                uint32_t &d = rec[D0 + 1 + j / 2];
-                d = (d & ~(0xFFFFu << (16 * (j & 1)))) | (c << (16 * (j & 1)));
-            }
+            std::copy(src, src + D0 + 1, rec);   // entries and meta (the forwarding codes are not used)
             if (k >= pl.count[u]) {   // inactive slot: sink V row n, sink message row m, no flags
                 for (int j = 0; j < D0; j++) rec[j] = (uint32_t)h->n;
                 rec[D0] = (uint32_t)h->m;
@@ -1170,79 +1114,110 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
     return 0;
 }
 
+// slot records as coop3_decode reads them (see RECW): the info entries
+// become the LDS offsets of their pieces in the line cache (LcPlan::piece),
+// the parity entries rows of the group's parity part, and each record carries
+// the line ops of its lane group (LcPlan::ops)
+static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vector<uint32_t> &out)
+{
+    const int S = ho.S, nw = ho.nw;
+    out.assign((size_t)nw * S * RECW, 0);
+    for (int u = 0; u < nw; u++)
+        for (int kk = 0; kk < S; kk++) {
+            const uint32_t *src = &ho.pl.tab[((size_t)u * S + kk) * RECW];
+            uint32_t *rec = &out[((size_t)u * S + kk) * RECW];
+            for (int j = 0; j < X; j++) rec[j] = lp.piece[((size_t)u * S + kk) * X + j];
+            rec[W_X] = src[X] - (uint32_t)k;
+            rec[W_O] = src[D0 - 1] - (uint32_t)k;
+            rec[W_META] = src[D0];
+            rec[W_LOP] = lp.ops[((size_t)u * LC_OPS + kk) * 2];
+            rec[W_LOP + 1] = lp.ops[((size_t)u * LC_OPS + kk) * 2 + 1];
+        }
+}
+
+int coop3_plan_lc(const ldpc_code *h, Coop3Host &ho, LcPlan &lp)
+{
+    const int ws = env_int3("LDPC_COOP3_WS", 6), r = env_int3("LDPC_COOP3_R", 2);
+    const int rc = coop3_plan_host(h, ws, r, ho);
+    if (rc != 0) return rc;
+    const int k = h->n - h->m;
+    if (lc_build_plan(ho.pl.tab, RECW, ho.nw, ho.S, D0, h->n, k, LC_SLOTS, lp) != 0) return 1;
+    return 0;
+}
+
 int coop3_upload(const ldpc_code *h, CoopCode *cc)
 {
     *cc = CoopCode{};
     Coop3Host ho;
-    const int ws = env_int3("LDPC_COOP3_WS", 6), r = env_int3("LDPC_COOP3_R", 2);
-    const int rc = coop3_plan_host(h, ws, r, ho);
+    LcPlan lp;
+    const int rc = coop3_plan_lc(h, ho, lp);
     if (rc != 0) return rc > 0 ? LDPC_OK : rc;
-    CoopPlan &pl = ho.pl;
-    const int S = ho.S, nw = ho.nw;
-    if (hipMalloc(&cc->d_tab, pl.tab.size() * 4) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop3 tables");
-    if (hipMemcpy(cc->d_tab, pl.tab.data(), pl.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    std::vector<uint32_t> tab;
+    coop3_records(ho, lp, h->n - h->m, tab);
+    auto up = [&](uint32_t **d, const std::vector<uint32_t> &v) -> int {
+        const size_t bytes = std::max<size_t>(v.size(), 1) * 4;
+        if (hipMalloc(d, bytes) != hipSuccess) return ldpc_set_error(LDPC_ENOMEM, "coop3 tables");
+        if (!v.empty() && hipMemcpy(*d, v.data(), v.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return ldpc_set_error(LDPC_EDEVICE, "coop3 table upload");
+        return LDPC_OK;
+    };
+    int e;
+    if ((e = up(&cc->d_tab, tab)) != LDPC_OK || (e = up(&cc->d_lc_pro, lp.pro)) != LDPC_OK ||
+        (e = up(&cc->d_lc_epi, lp.epi)) != LDPC_OK) {
         coop_free(cc);
-        return ldpc_set_error(LDPC_EDEVICE, "coop3 table upload");
+        return e;
     }
     cc->valid = 1;
     cc->d0 = D0;
-    cc->S = S;
-    cc->R = r;
-    cc->nw = nw;
-    cc->tail = pl.tail;
-    cc->n_fwd = pl.n_fwd;
+    cc->S = ho.S;
+    cc->R = 2;
+    cc->nw = ho.nw;
+    cc->tail = ho.pl.tail;
+    cc->n_fwd = ho.pl.n_fwd;
     cc->x0 = (int)h->edge_var[h->check_start[0] + X];
     cc->m0 = h->group_cnt[0];
     cc->d1 = h->group_deg[1];
+    cc->lc_slots = lp.slots;
+    cc->n_lc_pro = (int)lp.pro.size();
+    cc->n_lc_epi = (int)lp.epi.size();
     return LDPC_OK;
 }
 
-static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
-                              hipStream_t s);
+// the group stride of coop3's V: rows 0 .. n+7 (row n and the line n / 8:
+// the sinks) of 16 B, an odd number of 128-B lines (groups spread over the L2
+// channels)
+size_t coop3_group_bytes(const ldpc_code *h)
+{
+    size_t lines = ((size_t)h->n + 8 + 7) / 8;
+    if (lines % 2 == 0) lines++;
+    return lines * 128;
+}
 
-// the ET kernel is instantiated for WS = 6 only, and et_after stages the hard
-// bits of all n variables (u16 each) in the workgroup's LDS
+// the workgroup's LDS (the ET kernel stages the hard bits of all n variables,
+// u16 each, in it between segments)
 bool coop3_et_in_kernel(const CoopCode &cc, int n) { return cc.S == 48 && (size_t)n * 2 <= sizeof(Smem3<6, 2>); }
 
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
 {
-    if (!cc.valid || !coop3_stride_ok(L.stride)) return -1;
-    if (L.early && coop3_et_in_kernel(cc, L.n)) {
-        // in-kernel early termination (one launch, coop3_decode<.., ET>)
-        if (!L.iters_used) return -1;
-        if (L.iters == 0) {
-            hipLaunchKernelGGL(fill_iters3_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used, 0);
-            return hipGetLastError() == hipSuccess ? 0 : -1;
-        }
-        return launch_coop3_iters(L, cc, L.iters, nullptr, s);
-    }
-    if (L.early) {
-        // one launch per iteration; converged codewords keep iterating inside
-        // live workgroups, so their V is snapshot when they converge and
-        // merged back at the end (L.Vs)
-        if (!L.Vs || coop_early_begin(L, s)) return -1;
-        for (int it = 0; it < L.iters; it++)
-            if (launch_coop3_iters(L, cc, 1, L.live, s) || coop_early_after_iter(L, it, s)) return -1;
-        return coop_early_end(L, s);
-    }
-    if (L.iters_used)
+    if (!cc.valid || !coop3_stride_ok(L.stride) || L.vgroup == 0) return -1;
+    if (L.iters_used && (!L.early || L.iters == 0)) {
         hipLaunchKernelGGL(fill_iters3_k, dim3((L.batch + 255) / 256), dim3(256), 0, s, L.batch, L.iters_used,
-                           L.iters);
-    return launch_coop3_iters(L, cc, L.iters, nullptr, s);
-}
-
-static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int iters, const uint8_t *live,
-                              hipStream_t s)
-{
+                           L.early ? 0 : L.iters);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (L.iters == 0) return 0;
+    const bool et = L.early != 0;
+    if (et && (!L.iters_used || !coop3_et_in_kernel(cc, L.n))) return -1;
     Coop3Args a{};
-    a.live = live;
     a.V = (int8_t *)L.V;
+    a.gstride = L.vgroup;
     a.Mc = (uint8_t *)L.msg;
     a.tab = cc.d_tab;
-    // V layout: rows of L.vpitch codewords, a group's 16 B at wg * 16 in each
-    a.pitch = L.vpitch;
-    a.wgoff = (size_t)CW;
-    a.G = cc.nw * iters;
+    a.lc_pro = cc.d_lc_pro;
+    a.lc_epi = cc.d_lc_epi;
+    a.n_pro = cc.n_lc_pro;
+    a.n_epi = cc.n_lc_epi;
+    a.G = cc.nw * L.iters;
     a.nw = cc.nw;
     a.tail = cc.tail;
     a.mrows = L.m + 1;
@@ -1250,12 +1225,9 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.m = L.m;
     a.k = L.n - L.m;
     a.x0 = cc.x0;
-    a.P = L.P;
-    const bool et = L.early && live == nullptr;   // in-kernel early termination
     a.ev = L.d_edge_var;
-    a.Vs = L.Vs;
     a.iters_used = L.iters_used;
-    a.iters = iters;
+    a.iters = L.iters;
     a.batch = L.batch;
     a.m0 = cc.m0;
     a.d1 = cc.d1;
@@ -1268,39 +1240,44 @@ static int launch_coop3_iters(const DecodeLaunch &L, const CoopCode &cc, int ite
     a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 0 none, 1 static (second waves), 2 fair by phase
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups
-    const int ws = cc.S / 8;
-    const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0;
-    if (stamped) {
-        const size_t bytes = (size_t)grid * (ws + 1) * 8 * sizeof(unsigned long long);
-        if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
-        (void)hipMemsetAsync(a.stamps, 0, bytes, s);
-    }
-    int rc;
     if (et) {
-        if (stamped) (void)hipFree(a.stamps);
-        if (L.algo == LDPC_ALGO_NMS)
+        if (nms)
             hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 7), 0, s, a);
         else
             hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    if (L.algo == LDPC_ALGO_NMS) {
-        if (ws != 6 || stamped) return -1;
+    if (nms) {
         hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    if (ws == 6)
-        rc = launch_wsr<6, 2>(a, grid, stamped, s);
-    else if (ws == 4)
-        rc = launch_wsr<4, 2>(a, grid, stamped, s);
-    else
-        rc = launch_wsr<3, 2>(a, grid, stamped, s);
+    const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0;
     if (stamped) {
-        if (rc == 0)
-            (ws == 6   ? report_stamps3<6>(a.stamps, grid, s)
-             : ws == 4 ? report_stamps3<4>(a.stamps, grid, s)
-                       : report_stamps3<3>(a.stamps, grid, s));
+        const size_t bytes = (size_t)grid * 7 * 8 * sizeof(unsigned long long);
+        if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
+        (void)hipMemsetAsync(a.stamps, 0, bytes, s);
+    }
+    const int rc = launch_wsr<6, 2>(a, grid, stamped, s);
+    if (stamped) {
+        if (rc == 0) report_stamps3<6>(a.stamps, grid, s);
         (void)hipFree(a.stamps);
     }
     return rc;
+}
+
+// line-cache statistics of a code's coop3 schedule (tests, tools)
+extern "C" int ldpc_code_coop3_lc_info(const ldpc_code *h, int *slots, int *max_slots, int *residencies,
+                                       int *prologue, int *epilogue)
+{
+    if (!h || !slots) return ldpc_set_error(LDPC_EINVAL, "coop3 lc info args");
+    Coop3Host ho;
+    LcPlan lp;
+    const int rc = coop3_plan_lc(h, ho, lp);
+    if (rc < 0) return rc;
+    *slots = rc == 0 ? lp.slots : 0;
+    if (max_slots) *max_slots = LC_SLOTS;
+    if (residencies) *residencies = rc == 0 ? lp.residencies : 0;
+    if (prologue) *prologue = rc == 0 ? (int)lp.pro.size() : 0;
+    if (epilogue) *epilogue = rc == 0 ? (int)lp.epi.size() : 0;
+    return LDPC_OK;
 }

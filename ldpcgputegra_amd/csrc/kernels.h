@@ -28,10 +28,9 @@ struct DecodeLaunch {
     // (coop2 keeps iterating converged codewords that share a workgroup with
     // live ones; the snapshot is merged back before the hard decisions)
     int8_t *Vs;
-    // coop3: the parity rows k .. n-1 (+ a sink row) in their own layout,
-    // [stride / 16][m + 1][16 codewords]: consecutive checks' parity values
-    // are contiguous per codeword group (the kernel copies them in and out)
-    int8_t *P;
+    // coop3: V in the grouped layout Vg[stride / 16][rows][16 codewords],
+    // vgroup bytes between groups (0: the row layout V[N][vpitch])
+    size_t vgroup;
     // dynamic LDS bytes added to the windowed2 launch (mixed batches: keeps its
     // waves off the CUs of a concurrent coop3 decode, see ldpc_ctx_set_lds_pad)
     int lds_pad;
@@ -48,6 +47,11 @@ int launch_deinterleave_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, 
                            hipStream_t s);
 int launch_deinterleave_f32(const float *V, uint8_t *hard, float *soft, int n, int batch, int stride,
                             hipStream_t s);
+// frame-major [batch][N] <-> grouped Vg[group][row][16] (group = 16 codewords, groups `gbytes` apart)
+int launch_interleave_grp_i8(const int8_t *llr, int8_t *V, int n, int batch, int stride, size_t gbytes,
+                             hipStream_t s);
+int launch_deinterleave_grp_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, size_t gbytes,
+                               hipStream_t s);
 
 // rows of `row_bytes` bytes: dst[i] = src[idx[i]] (gather) / dst[idx[i]] = src[i] (scatter)
 int launch_gather_rows(const void *src, void *dst, const int32_t *idx, int rows, int row_bytes, hipStream_t s);

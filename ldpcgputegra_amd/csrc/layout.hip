@@ -59,6 +59,61 @@ __global__ void __launch_bounds__(256) deinterleave_k(const T *__restrict__ V, u
     }
 }
 
+// grouped layout (coop3): Vg[group][row][16 codewords], groups `gbytes` apart.
+// A 64x64 tile is 4 groups x 64 rows: one 16-B row piece per thread, so the
+// node-major side moves whole contiguous runs of 64 pieces per group.
+__global__ void __launch_bounds__(256) interleave_grp_k(const int8_t *__restrict__ src, int8_t *__restrict__ dst,
+                                                        int n, int batch, size_t gbytes)
+{
+    __shared__ int8_t tile[64][65];   // [codeword][node]
+    const int n0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int b = b0 + ty + 4 * r, i = n0 + tx;
+        tile[ty + 4 * r][tx] = (b < batch && i < n) ? src[(size_t)b * n + i] : (int8_t)0;
+    }
+    __syncthreads();
+    const int gq = threadIdx.x >> 6, ni = threadIdx.x & 63;   // group of the tile, node
+    if (n0 + ni < n) {
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            w[d] = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[d] |= (uint32_t)(uint8_t)tile[16 * gq + 4 * d + j][ni] << (8 * j);
+        }
+        *(uint4 *)(dst + (size_t)(b0 / 16 + gq) * gbytes + (size_t)(n0 + ni) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+__global__ void __launch_bounds__(256) deinterleave_grp_k(const int8_t *__restrict__ V, uint8_t *__restrict__ hard,
+                                                          int8_t *__restrict__ soft, int n, int batch, size_t gbytes)
+{
+    __shared__ int8_t tile[64][65];   // [codeword][node]
+    const int n0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+    const int gq = threadIdx.x >> 6, ni = threadIdx.x & 63;
+    if (n0 + ni < n) {
+        const uint4 y = *(const uint4 *)(V + (size_t)(b0 / 16 + gq) * gbytes + (size_t)(n0 + ni) * 16);
+        const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) tile[16 * gq + 4 * d + j][ni] = (int8_t)(w[d] >> (8 * j));
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int b = b0 + ty + 4 * r, i = n0 + tx;
+        if (b < batch && i < n) {
+            const int8_t x = tile[ty + 4 * r][tx];
+            if (hard) hard[(size_t)b * n + i] = x > 0 ? 1 : 0;
+            if (soft) soft[(size_t)b * n + i] = x;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) awgn_i8_k(int8_t *__restrict__ llr, int n, int batch, uint64_t first_cw,
                                                  uint64_t seed, AwgnTable t, const uint8_t *__restrict__ cw)
 {
@@ -174,6 +229,20 @@ int launch_deinterleave_f32(const float *V, uint8_t *hard, float *soft, int n, i
 {
     dim3 g((n + 63) / 64, (batch + 63) / 64);
     hipLaunchKernelGGL(deinterleave_k<float>, g, dim3(256), 0, s, V, hard, soft, n, batch, stride);
+    return ok();
+}
+int launch_interleave_grp_i8(const int8_t *llr, int8_t *V, int n, int batch, int stride, size_t gbytes,
+                             hipStream_t s)
+{
+    dim3 g((n + 63) / 64, (stride + 63) / 64);
+    hipLaunchKernelGGL(interleave_grp_k, g, dim3(256), 0, s, llr, V, n, batch, gbytes);
+    return ok();
+}
+int launch_deinterleave_grp_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, size_t gbytes,
+                               hipStream_t s)
+{
+    dim3 g((n + 63) / 64, (batch + 63) / 64);
+    hipLaunchKernelGGL(deinterleave_grp_k, g, dim3(256), 0, s, V, hard, soft, n, batch, gbytes);
     return ok();
 }
 int launch_awgn_i8(int8_t *llr, int n, int batch, uint64_t first_cw, uint64_t seed, const AwgnTable &t,

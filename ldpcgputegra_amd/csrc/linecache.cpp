@@ -1,0 +1,440 @@
+// linecache.cpp -- host planner of coop3's LDS line cache.
+//
+// coop3 keeps V (the int8 LLRs of a workgroup's 16 codewords) in the grouped
+// layout Vg[group][row][16 B] and moves the information rows between HBM and
+// the workgroup's LDS as whole 128-B lines (8 consecutive rows x 16
+// codewords), instead of one scattered 16-B piece per edge and check each way.
+// DVB-S2 is what makes lines pay: information bit m of a 360-bit group is
+// touched by checks x + m q (ETSI EN 302 307 Annex B, the reference's tables
+// code/x86/Constantes/64800x32400.dvb-s2/constantes_sse.h), so the layered
+// schedule walks each address of a group through consecutive bits, one bit
+// per q = 90 checks (two coop3 windows): one line load serves ~8 uses.
+//
+// The plan is static (per code, from the coop3 window schedule), periodic
+// with the nw windows of one iteration, and self-checked by replaying it:
+//   * window u's pre reads its info entries in period u - 1, its post writes
+//     them in period u + 1 (coop3_decode's period p: post of window p-1, pre
+//     of window p+1);
+//   * a residency (a line's accesses, split where two are >= LC_GAP periods
+//     apart) is loaded into VGPRs in period tl <= f - 3 (f = first access) by
+//     lane group i of slab wave w, written into its LDS slot by the same lanes
+//     in period tl + 2, and -- if written to -- written back (slot -> VGPRs ->
+//     HBM, whole line) in period tw >= e + 1 (e = last access); the slot is
+//     held over [tl + 2, tw];
+//   * a line written back is loaded again >= 3 periods after its store (the
+//     kernel's per-period vmcnt waits complete a store by then);
+//   * at most LC_OPS loads and LC_OPS writebacks per period (6 slab waves x 8
+//     lane groups: one 64-lane global load and one 64-lane global store per
+//     wave and period, unused lane groups on the sink line / sink slot);
+//   * no load in the last two periods of an iteration, so that a segment start
+//     has no load in flight: the lines resident at a segment start are filled
+//     by its prologue (LcPlan::pro) and the dirty ones left at its end are
+//     written back by its epilogue (LcPlan::epi);
+//   * slot 0 is the sink (the inactive slots' info entries), HBM line n / 8
+//     the sink line (rows n .. n+7: row n is the parity sink as well).
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "coop.h"
+
+namespace {
+
+struct Res {
+    uint32_t line;
+    int f, e;            // first / last access period (f in [0, nw), e >= f, may exceed nw)
+    int tl, tw;          // load period, writeback period (tw = e when clean), unrolled around f
+    bool dirty, whole;   // written to; resident for the whole iteration
+    int fw = 1 << 30;    // first write period (unrolled like e)
+    int slot = -1;
+    int li = -1, wi = -1;   // index of its load / writeback in the period's op list
+};
+
+inline int cmod(int a, int m) { return ((a % m) + m) % m; }
+
+// no plan: -1 (LDPC_LC_DEBUG=1 names the planner line that gave up)
+int lc_fail(int line)
+{
+    const char *e = getenv("LDPC_LC_DEBUG");
+    if (e && *e == '1') fprintf(stderr, "coop3 line cache plan: none (linecache.cpp:%d)\n", line);
+    return -1;
+}
+
+}  // namespace
+
+int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int n, int k, int max_slots,
+                  LcPlan &o)
+{
+    o = LcPlan{};
+    const int X = D0 - 2;
+    if (S != LC_OPS || nw < 4 * LC_GAP || n % 8 != 0 || k % 8 != 0 || k <= 0 || max_slots < 2 || n / 8 + 1 >= 65536)
+        return lc_fail(__LINE__);
+    const uint32_t nlines = (uint32_t)(k / 8), sink_line = (uint32_t)(n / 8);
+    auto rec_at = [&](int u, int kk) { return &tab[((size_t)u * S + kk) * recw]; };
+    // accesses per line: period << 1 | write
+    std::vector<std::vector<uint32_t>> acc(nlines);
+    for (int u = 0; u < nw; u++)
+        for (int kk = 0; kk < S; kk++) {
+            const uint32_t *r = rec_at(u, kk);
+            if (!(r[D0] & COOP_M_ACT)) continue;
+            for (int j = 0; j < X; j++) {
+                if (r[j] >= (uint32_t)k) return lc_fail(__LINE__);   // info entries must be information rows
+                acc[r[j] / 8].push_back((uint32_t)cmod(u - 1, nw) << 1);
+                acc[r[j] / 8].push_back((uint32_t)cmod(u + 1, nw) << 1 | 1u);
+            }
+            for (int j = X; j < D0; j++)
+                if (r[j] < (uint32_t)k) return lc_fail(__LINE__);   // x / o entries: parity rows
+        }
+    // residencies
+    std::vector<Res> rs;
+    std::vector<std::vector<int>> res_of(nlines);   // per line, in cyclic order of f
+    for (uint32_t L = 0; L < nlines; L++) {
+        auto &a = acc[L];
+        if (a.empty()) continue;
+        std::sort(a.begin(), a.end());
+        std::vector<int> per;
+        std::vector<char> wr;
+        for (uint32_t x : a) {
+            const int p = (int)(x >> 1);
+            if (per.empty() || per.back() != p) {
+                per.push_back(p);
+                wr.push_back(0);
+            }
+            wr.back() |= (char)(x & 1u);
+        }
+        const int m = (int)per.size();
+        std::vector<int> cut;   // i: a cut between access i and i + 1 (cyclic)
+        for (int i = 0; i < m; i++) {
+            const int gap = i + 1 < m ? per[i + 1] - per[i] : per[0] + nw - per[i];
+            if (gap >= LC_GAP) cut.push_back(i);
+        }
+        if (cut.empty()) {
+            Res R{L, per[0], per[0] + nw - 1, 0, 0, false, true};
+            for (int i = 0; i < m; i++) R.dirty |= wr[i] != 0;
+            res_of[L].push_back((int)rs.size());
+            rs.push_back(R);
+            continue;
+        }
+        // start at the access after the last cut so that the residencies come out in cyclic order
+        for (size_t c = 0; c < cut.size(); c++) {
+            const int s = (cut[c] + 1) % m, t = cut[(c + 1) % cut.size()];
+            Res R{L, per[s], per[s], 0, 0, false, false};
+            for (int i = s;; i = (i + 1) % m) {
+                R.dirty |= wr[i] != 0;
+                R.e = per[i] >= R.f ? per[i] : per[i] + nw;
+                if (wr[i]) R.fw = std::min(R.fw, R.e);
+                if (i == t) break;
+            }
+            res_of[L].push_back((int)rs.size());
+            rs.push_back(R);
+        }
+        std::sort(res_of[L].begin(), res_of[L].end(), [&](int x, int y) { return rs[x].f < rs[y].f; });
+    }
+    for (Res &R : rs) {
+        R.tl = R.f - LC_LEAD;
+        R.tw = R.dirty ? R.e + 1 : R.e;
+    }
+    // the store of a residency -> the next residency's load of the same line
+    // >= 3 periods later (cyclic, the next one may be itself an iteration on)
+    auto next_of = [&](int id) -> int {
+        const auto &v = res_of[rs[id].line];
+        const size_t i = std::find(v.begin(), v.end(), id) - v.begin();
+        return v[(i + 1) % v.size()];
+    };
+    auto prev_of = [&](int id) -> int {
+        const auto &v = res_of[rs[id].line];
+        const size_t i = std::find(v.begin(), v.end(), id) - v.begin();
+        return v[(i + v.size() - 1) % v.size()];
+    };
+    auto reload_ok = [&](int a, int b) {   // a's store before b's load
+        const Res &A = rs[a], &B = rs[b];
+        if (A.whole || B.whole || !A.dirty) return true;
+        int btl = B.tl;
+        while (btl + 0 <= A.tl) btl += nw;   // B's load after A's (unrolled)
+        return btl >= A.tw + 3;
+    };
+    // constraints: no load in the last two periods of an iteration; at most
+    // LC_OPS loads / writebacks per period (moving loads earlier, writebacks later)
+    for (int round = 0;; round++) {
+        if (round == 256) return lc_fail(__LINE__);
+        bool moved = false;
+        std::vector<std::vector<int>> lp(nw), wp(nw);
+        for (int i = 0; i < (int)rs.size(); i++) {
+            Res &R = rs[i];
+            if (R.whole) continue;
+            while (cmod(R.tl, nw) >= nw - 2) {
+                R.tl--;
+                moved = true;
+                if (!reload_ok(prev_of(i), i)) return lc_fail(__LINE__);
+            }
+            lp[cmod(R.tl, nw)].push_back(i);
+            if (R.dirty) wp[cmod(R.tw, nw)].push_back(i);
+        }
+        for (int p = 0; p < nw; p++) {
+            auto life = [&](int x) { return rs[x].tw - rs[x].tl; };
+            if ((int)lp[p].size() > LC_OPS) {
+                std::stable_sort(lp[p].begin(), lp[p].end(), [&](int x, int y) { return life(x) < life(y); });
+                int over = (int)lp[p].size() - LC_OPS;
+                for (size_t j = 0; j < lp[p].size() && over > 0; j++) {
+                    const int i = lp[p][j];
+                    rs[i].tl--;
+                    if (!reload_ok(prev_of(i), i)) {
+                        rs[i].tl++;
+                        continue;
+                    }
+                    over--;
+                    moved = true;
+                }
+                if (over > 0) return lc_fail(__LINE__);
+            }
+            if ((int)wp[p].size() > LC_OPS) {
+                std::stable_sort(wp[p].begin(), wp[p].end(), [&](int x, int y) { return life(x) < life(y); });
+                int over = (int)wp[p].size() - LC_OPS;
+                for (size_t j = 0; j < wp[p].size() && over > 0; j++) {
+                    const int i = wp[p][j];
+                    rs[i].tw++;
+                    if (!reload_ok(i, next_of(i))) {
+                        rs[i].tw--;
+                        continue;
+                    }
+                    over--;
+                    moved = true;
+                }
+                if (over > 0) return lc_fail(__LINE__);
+            }
+        }
+        if (!moved) break;
+    }
+    for (int i = 0; i < (int)rs.size(); i++) {
+        if (rs[i].whole) continue;
+        if (rs[i].tw - (rs[i].tl + 2) >= nw - 1) return lc_fail(__LINE__);
+        if (!reload_ok(prev_of(i), i) || !reload_ok(i, next_of(i))) return lc_fail(__LINE__);
+    }
+    // slots: circular-arc assignment of the holds [tl + 2, tw].  Cut at the
+    // period p0 with the fewest holds: the holds across p0 get a slot each,
+    // the rest go in order of their start to the free slot whose next hold
+    // starts soonest after them (best fit)
+    std::vector<int> live(nw, 0);
+    for (const Res &R : rs)
+        if (!R.whole)
+            for (int p = R.tl + 2; p <= R.tw; p++) live[cmod(p, nw)]++;
+    const int p0 = (int)(std::min_element(live.begin(), live.end()) - live.begin());
+    std::vector<int> free_from, next_busy;   // per slot 1.. (index + 1), relative to p0
+    constexpr int INF = 1 << 30;
+    std::vector<int> order;
+    for (int i = 0; i < (int)rs.size(); i++) {
+        Res &R = rs[i];
+        if (R.whole) {
+            R.slot = (int)free_from.size() + 1;
+            free_from.push_back(INF);
+            next_busy.push_back(-1);
+            continue;
+        }
+        const int a = R.tl + 2, len = R.tw - a;
+        if (cmod(p0 - a, nw) <= len) {   // across p0
+            R.slot = (int)free_from.size() + 1;
+            free_from.push_back(cmod(R.tw - p0, nw) + 1);
+            next_busy.push_back(cmod(a - p0, nw));
+        } else {
+            order.push_back(i);
+        }
+    }
+    std::sort(order.begin(), order.end(), [&](int x, int y) {
+        const int ax = cmod(rs[x].tl + 2 - p0, nw), ay = cmod(rs[y].tl + 2 - p0, nw);
+        return ax != ay ? ax < ay : x < y;
+    });
+    for (int i : order) {
+        Res &R = rs[i];
+        const int ra = cmod(R.tl + 2 - p0, nw), rb = ra + (R.tw - (R.tl + 2));
+        int best = -1;
+        for (int c = 0; c < (int)free_from.size(); c++) {
+            if (free_from[c] > ra || next_busy[c] <= rb) continue;
+            if (best < 0 || next_busy[c] < next_busy[best] ||
+                (next_busy[c] == next_busy[best] && free_from[c] > free_from[best]))
+                best = c;
+        }
+        if (best < 0) {
+            best = (int)free_from.size();
+            free_from.push_back(0);
+            next_busy.push_back(INF);
+        }
+        free_from[best] = rb + 1;
+        R.slot = best + 1;
+    }
+    o.slots = (int)free_from.size() + 1;
+    o.residencies = (int)rs.size();
+    if (o.slots > max_slots) return lc_fail(__LINE__);
+    // per-period op lists
+    std::vector<std::vector<int>> lp(nw), wp(nw);
+    for (int i = 0; i < (int)rs.size(); i++) {
+        Res &R = rs[i];
+        if (R.whole) continue;
+        R.li = (int)lp[cmod(R.tl, nw)].size();
+        lp[cmod(R.tl, nw)].push_back(i);
+        if (R.dirty) {
+            R.wi = (int)wp[cmod(R.tw, nw)].size();
+            wp[cmod(R.tw, nw)].push_back(i);
+        }
+    }
+    o.ops.assign((size_t)nw * LC_OPS * 2, 0);
+    for (size_t i = 0; i < o.ops.size(); i += 2) {
+        o.ops[i] = sink_line | sink_line << 16;   // load / writeback line: the sink
+        o.ops[i + 1] = 0;                         // ds_write / writeback slot: the sink
+    }
+    for (const Res &R : rs) {
+        if (R.whole) continue;
+        uint32_t *ld = &o.ops[((size_t)cmod(R.tl, nw) * LC_OPS + R.li) * 2];
+        ld[0] = (ld[0] & 0xFFFF0000u) | R.line;
+        uint32_t *dw = &o.ops[((size_t)cmod(R.tl + 2, nw) * LC_OPS + R.li) * 2];
+        dw[1] = (dw[1] & 0xFFFF0000u) | (uint32_t)R.slot;
+        if (R.dirty) {
+            uint32_t *wb = &o.ops[((size_t)cmod(R.tw, nw) * LC_OPS + R.wi) * 2];
+            wb[0] = (wb[0] & 0xFFFFu) | R.line << 16;
+            wb[1] = (wb[1] & 0xFFFFu) | (uint32_t)R.slot << 16;
+        }
+    }
+    // residency holding line L at access period p (cyclic)
+    auto res_at = [&](uint32_t L, int p) -> const Res * {
+        for (int id : res_of[L]) {
+            const Res &R = rs[id];
+            if (R.whole || cmod(p - R.f, nw) <= R.e - R.f) return &R;
+        }
+        return nullptr;
+    };
+    o.piece.assign((size_t)nw * S * X, 0);
+    for (int u = 0; u < nw; u++)
+        for (int kk = 0; kk < S; kk++) {
+            const uint32_t *r = rec_at(u, kk);
+            if (!(r[D0] & COOP_M_ACT)) continue;   // sink slot 0, piece 0
+            for (int j = 0; j < X; j++) {
+                const Res *R = res_at(r[j] / 8, cmod(u - 1, nw));
+                if (!R || R != res_at(r[j] / 8, cmod(u + 1, nw))) return lc_fail(__LINE__);
+                o.piece[((size_t)u * S + kk) * X + j] = (uint32_t)R->slot * 128u + (r[j] % 8) * 16u;
+            }
+        }
+    // segment prologue / epilogue: holds across the iteration boundary
+    for (const Res &R : rs) {
+        const uint32_t w = (uint32_t)R.slot << 16 | R.line;
+        if (R.whole) {
+            o.pro.push_back(w);
+            if (R.dirty) o.epi.push_back(w);
+        } else if (R.tl + 2 <= -1 || R.tw >= nw) {
+            o.pro.push_back(w);
+            // dirty at a segment end: written before it (posts run up to period nw) and not yet written back
+            if (R.dirty && R.tw >= nw + 1 && R.fw <= nw) o.epi.push_back(w);
+        }
+    }
+    return lc_check_plan(o, tab, recw, nw, S, D0, n, k, 3);
+}
+
+// Replays `iters` iterations of the plan period by period, in the kernel's
+// order (coop3_decode): every pre read / post write finds its line in the slot
+// the record names, a slot is only refilled once its dirty line was written
+// back, a writeback is never in a period that also accesses the line, a line
+// is loaded >= 3 periods after its last store and never while a dirty copy is
+// resident, and the dirty lines left at the end are exactly the epilogue's.
+int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int n, int k,
+                  int iters)
+{
+    const int X = D0 - 2;
+    const uint32_t sink_line = (uint32_t)(n / 8);
+    const int NSL = o.slots;
+    std::vector<int> line_of(NSL, -1);
+    std::vector<char> dirty(NSL, 0);
+    std::vector<long> last_store((size_t)k / 8, -1000000);
+    std::vector<int> dirty_copies((size_t)k / 8, 0);
+    auto fail = [&](const char *what, long P, int a, int b) {
+        fprintf(stderr, "coop3 line cache plan check: %s (period %ld, %d, %d)\n", what, P, a, b);
+        return -1;
+    };
+    for (uint32_t w : o.pro) {
+        const int s = (int)(w >> 16), L = (int)(w & 0xFFFFu);
+        if (s <= 0 || s >= NSL || line_of[s] >= 0) return fail("prologue slot", -1, s, L);
+        line_of[s] = L;
+    }
+    auto rec_at = [&](int u, int kk) { return &tab[((size_t)u * S + kk) * recw]; };
+    auto access = [&](int u, bool wr, long P) -> int {   // window u's info entries
+        u = cmod(u, nw);
+        for (int kk = 0; kk < S; kk++) {
+            const uint32_t *r = rec_at(u, kk);
+            if (!(r[D0] & COOP_M_ACT)) continue;
+            for (int j = 0; j < X; j++) {
+                const uint32_t off = o.piece[((size_t)u * S + kk) * X + j];
+                const int s = (int)(off / 128);
+                if (off % 128 != (r[j] % 8) * 16 || s <= 0 || s >= NSL || line_of[s] != (int)(r[j] / 8))
+                    return fail(wr ? "post finds another line" : "pre finds another line", P, s, (int)r[j]);
+                if (wr && !dirty[s]) {
+                    dirty[s] = 1;
+                    dirty_copies[r[j] / 8]++;
+                }
+            }
+        }
+        return 0;
+    };
+    const long G = (long)nw * iters;
+    std::vector<uint32_t> pend((size_t)3 * LC_OPS, sink_line);   // loads of periods P-2, P-1, P
+    if (access(0, false, -1)) return -1;                           // the pre of window 0 before period 0
+    for (long P = 0; P <= G; P++) {
+        const int p = (int)(P % nw);
+        const uint32_t *ops = &o.ops[(size_t)p * LC_OPS * 2];
+        std::vector<char> touched((size_t)k / 8, 0);
+        auto touch = [&](int u) {
+            u = cmod(u, nw);
+            for (int kk = 0; kk < S; kk++) {
+                const uint32_t *r = rec_at(u, kk);
+                if (r[D0] & COOP_M_ACT)
+                    for (int j = 0; j < X; j++) touched[r[j] / 8] = 1;
+            }
+        };
+        if (P >= 1) touch(p - 1);
+        if (P + 1 < G) touch(p + 1);
+        // writebacks
+        for (int i = 0; i < LC_OPS; i++) {
+            const uint32_t L = ops[2 * i] >> 16;
+            const int s = (int)(ops[2 * i + 1] >> 16);
+            if (L == sink_line) continue;
+            if (L >= (uint32_t)k / 8 || s <= 0 || s >= NSL || line_of[s] != (int)L)
+                return fail("writeback of a line not in its slot", P, s, (int)L);
+            if (touched[L]) return fail("writeback in a period accessing the line", P, s, (int)L);
+            if (dirty[s]) dirty_copies[L]--;
+            dirty[s] = 0;
+            last_store[L] = P;
+        }
+        // post of window p-1
+        if (P >= 1 && access(p - 1, true, P)) return -1;
+        // slot writes of the loads of period P-2
+        for (int i = 0; i < LC_OPS; i++) {
+            const int s = (int)(ops[2 * i + 1] & 0xFFFFu);
+            const uint32_t L = pend[(size_t)((P + 1) % 3) * LC_OPS + i];
+            if (s == 0) {
+                if (L != sink_line && P >= 2) return fail("load without a slot", P, s, (int)L);
+                continue;
+            }
+            if (L == sink_line) return fail("slot write without a load", P, s, (int)L);
+            if (s >= NSL || dirty[s]) return fail("slot refilled before its writeback", P, s, line_of[s]);
+            line_of[s] = (int)L;
+        }
+        // pre of window p+1
+        if (P + 1 < G && access(p + 1, false, P)) return -1;
+        // loads
+        for (int i = 0; i < LC_OPS; i++) {
+            const uint32_t L = ops[2 * i] & 0xFFFFu;
+            pend[(size_t)(P % 3) * LC_OPS + i] = L;
+            if (L == sink_line) continue;
+            if (L >= (uint32_t)k / 8) return fail("load of a bad line", P, i, (int)L);
+            if (dirty_copies[L] != 0) return fail("load while a dirty copy is resident", P, i, (int)L);
+            if (P - last_store[L] < 3) return fail("load too soon after the line's store", P, i, (int)L);
+        }
+    }
+    // what is left dirty must be the epilogue
+    std::vector<uint32_t> left;
+    for (int s = 1; s < NSL; s++)
+        if (dirty[s]) left.push_back((uint32_t)s << 16 | (uint32_t)line_of[s]);
+    std::vector<uint32_t> epi = o.epi;
+    std::sort(left.begin(), left.end());
+    std::sort(epi.begin(), epi.end());
+    if (left != epi) return fail("dirty lines at the end != epilogue", G, (int)left.size(), (int)epi.size());
+    return 0;
+}

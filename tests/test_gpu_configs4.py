@@ -111,12 +111,12 @@ def test_coop_xcd_remap_vs_oracle(code, early):
     dec.close()
 
 
-@pytest.mark.parametrize("kernel,env", [(5, {"LDPC_COOP_ET_KERNEL": "0"}), (8, {"LDPC_COOP3_WS": "4"})])
+@pytest.mark.parametrize("kernel,env", [(5, {"LDPC_COOP_ET_KERNEL": "0"})])
 def test_per_iteration_early_termination_padded_pitch(kernel, env):
     """The per-iteration early-termination launches (coop with
-    LDPC_COOP_ET_KERNEL=0; coop3 at WS = 4, whose ET is not in-kernel) address
-    V by its padded row pitch (LDPC_VPITCH_PAD, default 64 codewords): results
-    equal the oracle's (regression: they used to fail with LDPC_EDEVICE)."""
+    LDPC_COOP_ET_KERNEL=0) address V by its padded row pitch (LDPC_VPITCH_PAD,
+    default 64 codewords): results equal the oracle's (regression: they used to
+    fail with LDPC_EDEVICE).  coop3 has only its in-kernel early termination."""
     torch = _torch()
     t = load_table("dvbs2_r1_2")
     B, iters = 64, 30
