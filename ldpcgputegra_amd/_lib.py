@@ -104,6 +104,8 @@ def lib():
                               " (expected at %s)" % LIB_PATH)
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("LDPC_MI355X_LIB") and not hasattr(L, name):
+                continue   # an older experiment build (tools/ab.sh): its missing entry points stay unbound
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

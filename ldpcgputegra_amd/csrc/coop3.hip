@@ -850,7 +850,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         int uB = 1 % a.nw;   // local index of window p+1 (pre)
         StIn sc;             // the store of window p-2 (read from the stage at the end of period p-1)
         sc.addr = Pr + (size_t)a.m * 16;
-        bool sc_tl = false;  // ... window p-2 is the tail
         // Period p: post of window p-1 (state st[(p-1) % NS], x inputs from the
         // chain's window p-1, info V into the line cache); pre of window p+1
         // (inputs from the line cache and in[w][(p+1) % NI], -> st[(p+1) % NS]).
@@ -870,7 +869,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             constexpr bool GU = decltype(guarded)::value;
             if (STAMP) tx = stampL();
             const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
-            const bool fast = !GU && uA != a.tail && uB != a.tail && !sc_tl;
+            const bool fast = !GU;   // (a trip touching the tail window runs guarded)
             PreIn in;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
@@ -921,7 +920,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                 if (STAMP) t1 = t2 = t3 = stampL();
                 if (dpo) {
                     sl.read_st(p - 1, uA == a.tail, sc);
-                    sc_tl = uA == a.tail;
                 } else {
                     sc.addr = Pr + (size_t)a.m * 16;
                 }
@@ -954,11 +952,21 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, T{}, decltype(jc)::value);
         });
         int p = U + 1;
-        // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U
-        for (; p + U - 1 <= G - 2; p += U)
-            static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
-                period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, F{}, p + decltype(jc)::value);
-            });
+        // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U.  A trip
+        // is fast unless one of its periods posts, pres or stores the tail
+        // window (windows p-2 .. p+U of the trip): then it runs guarded
+        for (; p + U - 1 <= G - 2; p += U) {
+            int d = (a.tail - uA + 1) % a.nw;   // windows from p-2 to the tail
+            if (d < 0) d += a.nw;
+            if (d >= U + 3)
+                static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
+                    period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, F{}, p + decltype(jc)::value);
+                });
+            else
+                static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
+                    period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
+                });
+        }
         // the rest (at most U + 1 periods: p .. G), guarded
         static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
             if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)

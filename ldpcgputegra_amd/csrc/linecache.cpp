@@ -220,50 +220,69 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     for (const Res &R : rs)
         if (!R.whole)
             for (int p = R.tl + 2; p <= R.tw; p++) live[cmod(p, nw)]++;
-    const int p0 = (int)(std::min_element(live.begin(), live.end()) - live.begin());
-    std::vector<int> free_from, next_busy;   // per slot 1.. (index + 1), relative to p0
-    constexpr int INF = 1 << 30;
-    std::vector<int> order;
-    for (int i = 0; i < (int)rs.size(); i++) {
-        Res &R = rs[i];
-        if (R.whole) {
-            R.slot = (int)free_from.size() + 1;
-            free_from.push_back(INF);
-            next_busy.push_back(-1);
-            continue;
+    // assignment from the cut at p0; returns the slots used (sink excluded)
+    auto assign = [&](int p0) -> int {
+        std::vector<int> free_from, next_busy;   // per slot 1.. (index + 1), relative to p0
+        constexpr int INF = 1 << 30;
+        std::vector<int> order;
+        for (int i = 0; i < (int)rs.size(); i++) {
+            Res &R = rs[i];
+            if (R.whole) {
+                R.slot = (int)free_from.size() + 1;
+                free_from.push_back(INF);
+                next_busy.push_back(-1);
+                continue;
+            }
+            const int a = R.tl + 2, len = R.tw - a;
+            if (cmod(p0 - a, nw) <= len) {   // across p0
+                R.slot = (int)free_from.size() + 1;
+                free_from.push_back(cmod(R.tw - p0, nw) + 1);
+                next_busy.push_back(cmod(a - p0, nw));
+            } else {
+                order.push_back(i);
+            }
         }
-        const int a = R.tl + 2, len = R.tw - a;
-        if (cmod(p0 - a, nw) <= len) {   // across p0
-            R.slot = (int)free_from.size() + 1;
-            free_from.push_back(cmod(R.tw - p0, nw) + 1);
-            next_busy.push_back(cmod(a - p0, nw));
-        } else {
-            order.push_back(i);
+        std::sort(order.begin(), order.end(), [&](int x, int y) {
+            const int ax = cmod(rs[x].tl + 2 - p0, nw), ay = cmod(rs[y].tl + 2 - p0, nw);
+            return ax != ay ? ax < ay : x < y;
+        });
+        for (int i : order) {
+            Res &R = rs[i];
+            const int ra = cmod(R.tl + 2 - p0, nw), rb = ra + (R.tw - (R.tl + 2));
+            int best = -1;
+            for (int c = 0; c < (int)free_from.size(); c++) {
+                if (free_from[c] > ra || next_busy[c] <= rb) continue;
+                if (best < 0 || next_busy[c] < next_busy[best] ||
+                    (next_busy[c] == next_busy[best] && free_from[c] > free_from[best]))
+                    best = c;
+            }
+            if (best < 0) {
+                best = (int)free_from.size();
+                free_from.push_back(0);
+                next_busy.push_back(INF);
+            }
+            free_from[best] = rb + 1;
+            R.slot = best + 1;
+        }
+        return (int)free_from.size();
+    };
+    // cut candidates: the periods with the fewest holds
+    std::vector<int> cand(nw);
+    for (int p = 0; p < nw; p++) cand[p] = p;
+    std::stable_sort(cand.begin(), cand.end(), [&](int x, int y) { return live[x] < live[y]; });
+    const char *ev = getenv("LDPC_LC_CUTS");
+    const int ncut = std::min(nw, ev && *ev ? atoi(ev) : 1);
+    int best_p0 = cand[0], best_n = 1 << 30;
+    for (int i = 0; i < ncut; i++) {
+        const int nsl = assign(cand[i]);
+        if (ev && *ev) fprintf(stderr, "cut %d live %d -> %d slots\n", cand[i], live[cand[i]], nsl);
+        if (nsl < best_n) {
+            best_n = nsl;
+            best_p0 = cand[i];
         }
     }
-    std::sort(order.begin(), order.end(), [&](int x, int y) {
-        const int ax = cmod(rs[x].tl + 2 - p0, nw), ay = cmod(rs[y].tl + 2 - p0, nw);
-        return ax != ay ? ax < ay : x < y;
-    });
-    for (int i : order) {
-        Res &R = rs[i];
-        const int ra = cmod(R.tl + 2 - p0, nw), rb = ra + (R.tw - (R.tl + 2));
-        int best = -1;
-        for (int c = 0; c < (int)free_from.size(); c++) {
-            if (free_from[c] > ra || next_busy[c] <= rb) continue;
-            if (best < 0 || next_busy[c] < next_busy[best] ||
-                (next_busy[c] == next_busy[best] && free_from[c] > free_from[best]))
-                best = c;
-        }
-        if (best < 0) {
-            best = (int)free_from.size();
-            free_from.push_back(0);
-            next_busy.push_back(INF);
-        }
-        free_from[best] = rb + 1;
-        R.slot = best + 1;
-    }
-    o.slots = (int)free_from.size() + 1;
+    const int used = assign(best_p0);
+    o.slots = used + 1;
     o.residencies = (int)rs.size();
     if (o.slots > max_slots) return lc_fail(__LINE__);
     // per-period op lists
