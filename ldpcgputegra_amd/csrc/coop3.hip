@@ -203,10 +203,24 @@ struct Slab3 {
     char *sbase;
     uint32_t smul;
     uint32_t mrd, prd;                // byte offsets in an In record: this lane's message pair / o-edge V dword
+    // read_st's per-lane constants (set by init_st): record word byte offset and
+    // mask, sink masks (window not / the tail), stage-source mask and offset of
+    // the 16-B piece from mst[w][kl][0]
+    uint32_t stw = 0, stm = 0, snk = 0, snk_tl = 0, stst = 0, sto = 0;
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
 
+    LDPC_DEV void init_st()
+    {
+        stw = 4u * (uint32_t)(q < 4 ? W_META : q == 4 ? W_X : W_O);
+        stm = q < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
+        snk = q >= 5 ? 0xFFFFFFFFu : 0u;
+        snk_tl = q >= 6 ? 0xFFFFFFFFu : 0u;
+        stst = q >= 4 ? 0xFFFFFFFFu : 0u;
+        const char *src = q < 4 ? (const char *)&sm.mst[w][kl][q] : (const char *)&sm.stg[0][q == 4 ? 0 : 1][k];
+        sto = (uint32_t)(src - (const char *)&sm.mst[w][kl][0]);
+    }
     LDPC_DEV const char *lcb() const { return (const char *)&sm.lc[0][0]; }
     LDPC_DEV char *lcw() const { return (char *)&sm.lc[0][0]; }
 
@@ -232,15 +246,16 @@ struct Slab3 {
         in.mb = mm.y;
         in.meta = rc.pm.w;
     }
-    // the store of window g (tl: the tail window): address and 16-B piece of this lane
+    // the store of window g (tl: the tail window): address and 16-B piece of
+    // this lane.  Branch-free: lane q reads record word stw (q < 4 the meta,
+    // q = 4 the x row, q >= 5 the o row), lanes past the op's width take the sink
     LDPC_DEV void read_st(int g, bool tl, StIn &in) const
     {
-        const uint32_t *r = &sm.tab[g & (TQ - 1)][k][0];
-        const uint32_t idx = q < 4 ? (r[W_META] & COOP_CHK_MASK) : q == 4 ? r[W_X] : (q == 5 && tl) ? r[W_O]
-                                                                                                : (uint32_t)a.m;
+        const uint32_t rw = *(const uint32_t *)((const char *)&sm.tab[g & (TQ - 1)][k][0] + stw) & stm;
+        const uint32_t idx = bfi(tl ? snk_tl : snk, (uint32_t)a.m, rw);
         in.addr = sbase + (size_t)idx * smul;
-        const char *src = q < 4 ? (const char *)&sm.mst[w][kl][q] : (const char *)&sm.stg[g % NR][q == 4 ? 0 : 1][k];
-        in.d = *(const uint4 *)src;
+        in.d = *(const uint4 *)((const char *)&sm.mst[w][kl][0] + sto +
+                                (stst & ((uint32_t)(g % NR) * (uint32_t)sizeof(sm.stg[0]))));
     }
     LDPC_DEV uint32_t read_gidx(int g) const   // the gather's row / check of window g (lane (e, slot))
     {
@@ -288,7 +303,7 @@ struct Slab3 {
             // same edges either way, and min1 == msg_max implies cst1 == cst2)
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t, K.m3, K.c4)), neg127);
                 const uint32_t aj = abs_r(c, c510);
                 s.c[J] = c;
                 s.a[J] = aj;
@@ -298,14 +313,14 @@ struct Slab3 {
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
-            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t)), neg127);
+            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t, K.m3, K.c4)), neg127);
             const uint32_t ao = abs_r(cor, c510);
             s.c[X] = cor;
             s.a[X] = ao;
             s.sacc = sacc ^ cor;
             s.mn2 = pk_max(min1, pk_min(ao, min2));
             s.mn1 = pk_min(min1, ao);
-            const uint32_t mx = old_msg<X>(MA, t);
+            const uint32_t mx = old_msg<X>(MA, t, K.m3, K.c4);
             s.mx = mx;
             // chain constants in value form (R >> 8, C >> 8), both codewords at once
             COV = pk_ashr8(cor);
@@ -338,7 +353,7 @@ struct Slab3 {
             // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t)), neg127);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t, K.m3, K.c4)), neg127);
                 // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2
                 const uint32_t aj = NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510);
                 s.c[J] = c;
@@ -379,7 +394,12 @@ struct Slab3 {
             L = VNEG127;
             H = V127;
         }
-        // per codeword records: (A, B), (eps, c_o), (L, H) as i16 pairs
+        // per codeword records: (A, B), (eps, c_o), (L, H) as i16 pairs (writing
+        // the halves with ds_write_b16 / _d16_hi instead of these 6 v_perm ran
+        // 3 % slower: 43.7 vs 42.4 ms)
+        const int cb = g & 1;
+        const uint32_t step = (meta >> STEP_SHIFT) & 63u;
+        s.xs = (step >> 3) * (CW * 8) + (step & 7);
         uint4 r0, r1;
         r0.x = perm(B, A, 0x05040100u);
         r1.x = perm(B, A, 0x07060302u);
@@ -388,9 +408,6 @@ struct Slab3 {
         r0.z = perm(H, L, 0x05040100u);
         r1.z = perm(H, L, 0x07060302u);
         r0.w = r1.w = 0;
-        const int cb = g & 1;
-        const uint32_t step = (meta >> STEP_SHIFT) & 63u;
-        s.xs = (step >> 3) * (CW * 8) + (step & 7);
         uint4 *cp = &sm.cst[cb][0][0][q] + step * (2 * NP);
         cp[0] = r0;
         cp[NP] = r1;
@@ -664,12 +681,12 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             auto hbits = [](uint4 y) {
                 return (uint16_t)high_bits16(make_uint4(pos_bits(y.x), pos_bits(y.y), pos_bits(y.z), pos_bits(y.w)));
             };
-            for (int r0 = 0; r0 < a.n; r0 += NT * 16) {
-                uint4 y[16];
+            for (int r0 = 0; r0 < a.n; r0 += NT * 8) {
+                uint4 y[8];
 #pragma unroll
-                for (int i = 0; i < 16; i++) y[i] = *et_row((uint32_t)min(r0 + i * NT + (int)threadIdx.x, a.n - 1));
+                for (int i = 0; i < 8; i++) y[i] = *et_row((uint32_t)min(r0 + i * NT + (int)threadIdx.x, a.n - 1));
 #pragma unroll
-                for (int i = 0; i < 16; i++)
+                for (int i = 0; i < 8; i++)
                     if (r0 + i * NT + (int)threadIdx.x < a.n) hb[r0 + i * NT + threadIdx.x] = hbits(y[i]);
             }
             __syncthreads();
@@ -796,7 +813,8 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     lane,
                     a.tail,
                     0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
-                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff)},
+                    PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff), opaque(0x03000300u),
+                        opaque(0x040c000cu)},
                     opaque(a.nmsf),
                     Vg,
                     (uint32_t)(4 * (q >> 1)),
@@ -812,6 +830,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     q < 4 ? (uint32_t)MREC : 16u,
                     (uint32_t)(((q >> 1) * 8 + kl) * 16 + (q & 1) * 8),
                     (uint32_t)((32 + kl) * 16 + 4 * (q >> 1))};
+    sl.init_st();
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     constexpr int NI = CF::NI, NS = CF::NS;
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
@@ -864,12 +883,18 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         // which posts before its pre (LDS keeps a wave's order).
         constexpr int MP1 = -1, MP2 = -1;   // mid-phase priorities (none: quarter-period levels measured the same)
         const bool fair = a.slab_prio == 2;
-        auto period = [&](auto sc_, auto guarded, int p) __attribute__((always_inline)) {
+        // mode: 0 guarded, 1 fast, 2 decided here (fast unless the period posts,
+        // pres or stores the tail window)
+        auto period = [&](auto sc_, auto mode_, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
-            constexpr bool GU = decltype(guarded)::value;
+            constexpr int MODE = decltype(mode_)::value;
             if (STAMP) tx = stampL();
             const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
-            const bool fast = !GU;   // (a trip touching the tail window runs guarded)
+            bool fast = MODE == 1;
+            if constexpr (MODE == 2) {
+                const int d = uA == 0 ? (a.tail + 1 == a.nw ? 0 : a.tail + 1) : a.tail - uA + 1;   // tail - (p-2)
+                fast = d != 0 && d != 1 && d != 3 && d != 1 - a.nw && d != 3 - a.nw;
+            }
             PreIn in;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
@@ -945,32 +970,43 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             next(uA);
             next(uB);
         };
-        using T = std::true_type;
-        using F = std::false_type;
+        using GUARD = std::integral_constant<int, 0>;
+        using FAST = std::integral_constant<int, 1>;
+        using RT = std::integral_constant<int, 2>;
         // periods 0 .. U guarded
         static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
-            if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, T{}, decltype(jc)::value);
+            if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, GUARD{}, decltype(jc)::value);
         });
         int p = U + 1;
-        // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U.  A trip
-        // is fast unless one of its periods posts, pres or stores the tail
-        // window (windows p-2 .. p+U of the trip): then it runs guarded
-        for (; p + U - 1 <= G - 2; p += U) {
-            int d = (a.tail - uA + 1) % a.nw;   // windows from p-2 to the tail
-            if (d < 0) d += a.nw;
-            if (d >= U + 3)
+        // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U.
+        if constexpr (ET) {
+            // the ET kernel decides per period (one loop body keeps its
+            // registers within 256)
+            for (; p + U - 1 <= G - 2; p += U)
                 static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
-                    period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, F{}, p + decltype(jc)::value);
+                    period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, RT{}, p + decltype(jc)::value);
                 });
-            else
-                static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
-                    period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
-                });
+        } else {
+            // trips of U periods, fast unless one of them posts, pres or stores
+            // the tail window (windows p-2 .. p+U of the trip): no per-period
+            // branch, so the compiler's own vmcnt waits count exactly
+            for (; p + U - 1 <= G - 2; p += U) {
+                int d = (a.tail - uA + 1) % a.nw;   // windows from p-2 to the tail
+                if (d < 0) d += a.nw;
+                if (d >= U + 3)
+                    static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
+                        period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, FAST{}, p + decltype(jc)::value);
+                    });
+                else
+                    static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
+                        period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, GUARD{}, p + decltype(jc)::value);
+                    });
+            }
         }
         // the rest (at most U + 1 periods: p .. G), guarded
         static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
             if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)
-                period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
+                period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, GUARD{}, p + decltype(jc)::value);
         });
         sl.stores(sc);   // window G-1
         // line cache epilogue: the dirty lines still resident (LcPlan::epi)

@@ -81,6 +81,7 @@ LDPC_DEV uint32_t abs_r(uint32_t r, uint32_t c510) { return pk_max(r, pk_sub(c51
 // is read
 struct PkK {
     uint32_t neg127, r0, c510, rmm, coff;   // R(-127), R(0), 510, R(msg_max), C(offset) per half
+    uint32_t m3 = 0x03000300u, c4 = 0x040c000cu;   // old_msg's selector mask / constant
 };
 
 // byte tables [+cst1, -cst1, +cst2, -cst2] of the two codewords of a pair
@@ -93,16 +94,18 @@ LDPC_DEV MsgTab msg_tab(uint32_t MB)
     return {perm(pk_sub(0u, p0), p0, 0x06020400u), perm(pk_sub(0u, p1), p1, 0x06020400u)};
 }
 
-// old message of edge J (C pair): byte 1 = t0[code0], byte 3 = t1[code1]
+// old message of edge J (C pair): byte 1 = t0[code0], byte 3 = t1[code1].
+// m3 / c4: 0x03000300 / 0x040c000c held in VGPRs, so that the mask-and-or is
+// one v_bitop3 (gfx9 VOP3 encodes no literal)
 template <int J>
-LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t)
+LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t, uint32_t m3 = 0x03000300u, uint32_t c4 = 0x040c000cu)
 {
     uint32_t sh;
     if constexpr (J <= 4)
         sh = MA << (8 - 2 * J);
     else
         sh = MA >> (2 * J - 8);
-    return perm(t.t1, t.t0, (sh & 0x03000300u) | 0x040c000cu);
+    return perm(t.t1, t.t0, (sh & m3) | c4);
 }
 
 // new message of edge J: its code into MA, the new V (R pair) returned

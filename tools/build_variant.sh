@@ -8,7 +8,7 @@ set -e
 cd "$(dirname "$0")/.."
 name=$1
 shift
-src=coop2.hip
+src=coop3.hip
 if [[ "$1" == *.hip ]]; then
     src=$1
     shift
