@@ -74,7 +74,7 @@ constexpr int D0 = 7, X = D0 - 2;   // first-group check degree, information edg
 constexpr int RECW = 12;            // slot record words (coop3_upload)
 constexpr int DPER = 2;             // a window table's LDS-DMA is waited for DPER periods after its issue
 constexpr int TQ = 8;               // window-table slots in LDS
-constexpr int LC_SLOTS = 776;       // line-cache slots (128 B each; slot 0 is the sink)
+constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is the sink)
 
 // slot record (coop3_upload): words 0..4 the LDS byte offsets (from the line
 // cache) of the info entries' 16-B pieces, 5 / 6 the x / o edge parity rows
@@ -115,7 +115,8 @@ struct alignas(16) Smem3 {
     struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
         uint4 d[5][8];                //   e < 4: message bytes 16e .. 16e+15, e = 4: the o-edge parity row
     } in[WS][NI];
-    uint4 mst[WS][8][4];              // new messages of a window per slab wave, [slot] x 64 B
+    uint4 mst[2][WS][8][4];           // new messages of window g per slab wave in mst[g & 1], [slot] x 64 B
+                                      // (posted in period g+1, stored by the memory wave in period g+2)
 };
 
 struct Coop3Args {
@@ -459,7 +460,7 @@ struct Slab3 {
             MA = s.mn1;
             MB = s.mn2;
         }
-        *(uint2 *)((char *)&sm.mst[w][kl][0] + 8 * q) = make_uint2(MA, MB);
+        *(uint2 *)((char *)&sm.mst[g & 1][w][kl][0] + 8 * q) = make_uint2(MA, MB);
     }
 };
 
@@ -578,7 +579,7 @@ LDPC_DEV uint32_t high_bits16(uint4 x)   // byte high bits -> 16-bit codeword ma
 // as the reference's per-codeword stop (oracle: syndrome after every
 // iteration), in one launch.
 template <int WS, int R, bool STAMP, bool ET = false, bool NMS = false>
-__global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
+__global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 {
     using SM = Smem3<WS, R>;
     using CF = Cfg<WS, R>;
@@ -594,7 +595,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     char *Vg = (char *)a.V + (size_t)wg * a.gstride;
     // ---- ET state: [0] live codewords, [1] failing codewords (syndrome)
     __shared__ uint32_t et_sh[2];
-    constexpr int NT = 64 * (WS + 1);
+    constexpr int NT = 64 * (WS + 2);
     auto et_row = [&](uint32_t v) -> const uint4 * { return (const uint4 *)(Vg + (size_t)v * 16); };
     if constexpr (ET) {
         if (threadIdx.x == 0) {
@@ -741,7 +742,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     unsigned long long sA = 0, sP[4] = {0, 0, 0, 0}, sD = 0, t0 = 0, tx = 0;
     auto write_stamps = [&]() {
         if (STAMP && lane == 0) {
-            unsigned long long *o = a.stamps + ((size_t)id * (WS + 1) + wave) * 8;
+            unsigned long long *o = a.stamps + ((size_t)id * (WS + 2) + wave) * 8;
             o[0] = sA;
             for (int i = 0; i < 4; i++) o[1 + i] = sP[i];
             o[5] = stamp3() - t0;
@@ -774,6 +775,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             w4[0] = (uint32_t)(int)((const int8_t *)et_row((uint32_t)a.x0))[c] & 0xFFFFu;
             int un = KAHEAD % a.nw;
             __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 and the resident lines in LDS
+            __syncthreads();   // prologue 1b: the memory wave's first gathers landed
             __syncthreads();   // prologue 2: constants of window 0 in LDS
             if (STAMP) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
@@ -793,6 +795,145 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         return;
     }
 
+    char *Pr = Vg + (size_t)a.k * 16;   // parity row k + j at Pr + 16 j (row n: the sink)
+    const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
+    constexpr int NI = CF::NI, NS = CF::NS;
+    constexpr int MW = WS + 1;   // the memory wave (shares the chain wave's SIMD)
+    const int kl = lane >> 3, q = lane & 7;
+
+    if (wave == MW) {
+        // ------------------------------------------------------------ memory wave
+        // Every vector-memory operation of the workgroup, per period p for each
+        // slab wave's set of 8 slots (w = 0..WS-1), in this order: the slot
+        // writes of the lines loaded in period p-2; the LDS-DMA gathers of
+        // window p+1+R (messages + o-edge parity rows); the line loads of period
+        // p (8 lines per set); the line writebacks of period p (slot -> VGPRs ->
+        // HBM); the stores of window p-2 (messages + x-edge parity rows).  Then
+        // vmcnt(36): everything up to this period's predecessor's loads has
+        // landed -- the gathers for the pre of window p+2 (next period) and the
+        // lines written to their slots next period -- and a writeback completes
+        // two periods after its issue, before its line can be loaded again
+        // (linecache.cpp: >= 3).  Unused ops go to the sink row / line / slot,
+        // so the counts are static.
+        char *lcb = (char *)&sm.lc[0][0];
+        const uint32_t lq = 16u * (uint32_t)q;
+        // gathers: lane (e, slot) = (kl, q): e < 4 message piece e, e = 4 the o-edge parity row
+        const char *gbase = kl < 4 ? Mb + kl * 16 : (const char *)Pr;
+        const uint32_t gmul = kl < 4 ? (uint32_t)MREC : 16u, gmask = kl < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
+        const uint32_t gsel = (uint32_t)(kl < 4 ? W_META : W_O);
+        // stores: lane (kl, q) of slot 8w + kl: q < 4 message piece q, q = 4 the
+        // x-edge parity row, q = 5 the tail's last edge, the rest the sink row
+        char *sbase = q < 4 ? (char *)Mb + q * 16 : Pr;
+        const uint32_t smul = q < 4 ? (uint32_t)MREC : 16u;
+        const uint32_t stw = 4u * (uint32_t)(q < 4 ? W_META : q == 4 ? W_X : W_O);
+        const uint32_t stm = q < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
+        const uint32_t snk = q >= 5 ? 0xFFFFFFFFu : 0u, snk_tl = q >= 6 ? 0xFFFFFFFFu : 0u;
+        auto gather = [&](int w, int g, int ib) __attribute__((always_inline)) {
+            const uint32_t idx = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
+            if (lane < 40) dma16(gbase + (size_t)idx * gmul, (uint32_t)(uintptr_t)&sm.in[w][ib]);
+        };
+        // the store of window g's slots 8w .. 8w+7: its row / check index, read
+        // from window g's records one period before the store (the chain wave
+        // restages that table slot in the store's period); tl: the tail window,
+        // !live: the sink
+        auto store_idx = [&](int w, int g, bool tl, bool live) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t rw = *(const uint32_t *)((const char *)&sm.tab[g & (TQ - 1)][8 * w + kl][0] + stw) & stm;
+            return live ? bfi(tl ? snk_tl : snk, (uint32_t)a.m, rw) : (uint32_t)a.m;
+        };
+        auto store_win = [&](int w, int g, uint32_t idx) __attribute__((always_inline)) {
+            const uint4 *src = q < 4 ? &sm.mst[g & 1][w][kl][q] : &sm.stg[g & 1][q == 4 ? 0 : 1][8 * w + kl];
+            *(uint4 *)(sbase + (size_t)idx * smul) = *src;
+        };
+        for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
+            __syncthreads();   // prologue 1: tables and resident lines in LDS
+#pragma unroll
+            for (int i = 0; i <= R; i++)   // window i -> in[w][i]   (nw > R + 3)
+#pragma unroll
+                for (int w = 0; w < WS; w++) gather(w, i, i);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();   // prologue 1b: the first windows' gathers landed
+            __syncthreads();   // prologue 2
+            constexpr int NPD = LC_PUT + 1;
+            uint4 pend[NPD][WS];   // line loads of periods p-LC_PUT .. p (written to their slots LC_PUT periods on)
+#pragma unroll
+            for (int i = 0; i < NPD; i++)
+#pragma unroll
+                for (int w = 0; w < WS; w++) pend[i][w] = make_uint4(0, 0, 0, 0);
+            int uS = a.nw - 1;   // local index of window p-1 (the next period's stores)
+            uint32_t sidx[WS];   // the stores' indices (window p-2), read in period p-1
+            uint2 lop[WS];       // the line ops of period p, read in period p-1
+#pragma unroll
+            for (int w = 0; w < WS; w++) {
+                sidx[w] = (uint32_t)a.m;
+                lop[w] = *(const uint2 *)&sm.tab[0][8 * w + kl][W_LOP];
+            }
+            // period p: gathers of window p+1+R, line loads of period p, line
+            // writebacks of period p, stores of window p-2 (24 ops); vmcnt(42)
+            // at its end completes everything up to the gathers of period p-1
+            // (the pre of window p+2 reads them next period) and the line loads
+            // of period p-2 (their slot writes are next period's), and a
+            // writeback two periods after its issue (its line is loaded again
+            // >= 3 periods later, linecache.cpp)
+            auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
+                constexpr int s = decltype(sc_)::value;   // p % NPD
+                uint32_t gix[WS];
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    constexpr int w = decltype(wc)::value;
+                    gix[w] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
+                });
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
+                    constexpr int w = decltype(wc)::value;
+                    *(uint4 *)(lcb + (lop[w].y & 0xFFFFu) * 128u + lq) = pend[(s + 1) % NPD][w];
+                });
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    constexpr int w = decltype(wc)::value;
+                    if (lane < 40)
+                        dma16(gbase + (size_t)gix[w] * gmul, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
+                });
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    constexpr int w = decltype(wc)::value;
+                    pend[s][w] = *(const uint4 *)(Vg + (size_t)(lop[w].x & 0xFFFFu) * 128 + lq);
+                });
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    constexpr int w = decltype(wc)::value;
+                    const uint4 v = *(const uint4 *)(lcb + (lop[w].y >> 16) * 128u + lq);
+                    *(uint4 *)(Vg + (size_t)(lop[w].x >> 16) * 128 + lq) = v;
+                });
+                // the stores of window p-2 (the sink before period 2), then the
+                // indices of window p-1's and the next period's line ops
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    constexpr int w = decltype(wc)::value;
+                    store_win(w, p - 2, sidx[w]);
+                });
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    constexpr int w = decltype(wc)::value;
+                    sidx[w] = store_idx(w, p - 1, uS == a.tail, p >= 1);
+                    lop[w] = *(const uint2 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][W_LOP];
+                });
+                asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+                __syncthreads();
+                uS = (uS + 1 == a.nw) ? 0 : uS + 1;
+            };
+            int p = 0;
+            for (; p + NPD - 1 <= G; p += NPD)
+                static_for<0, NPD>([&](auto jc) __attribute__((always_inline)) {
+                    mperiod(std::integral_constant<int, decltype(jc)::value>{}, p + decltype(jc)::value);
+                });
+            static_for<0, NPD - 1>([&](auto jc) __attribute__((always_inline)) {
+                if (p + decltype(jc)::value <= G)
+                    mperiod(std::integral_constant<int, decltype(jc)::value>{}, p + decltype(jc)::value);
+            });
+            // the stores of window G-1 (its post ran in period G)
+            static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                store_win(decltype(wc)::value, G - 1, sidx[decltype(wc)::value]);
+            });
+            __syncthreads();   // epilogue (the slab waves write the resident dirty lines back)
+            if (!ET || !et_after(it)) break;
+        }
+        write_stamps();
+        return;
+    }
+
     // ------------------------------------------------------------ slab waves
     const int sw = wave - (wave > CHW ? 1 : 0);   // slab index
     constexpr int NSL = 64 * WS;                  // slab threads
@@ -801,9 +942,6 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
-    const int kl = lane >> 3, q = lane & 7;
-    const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
-    char *Pr = Vg + (size_t)a.k * 16;   // parity row k + j at Pr + 16 j (row n: the sink)
     Slab3<WS, R, NMS> sl{sm,
                     a,
                     8 * sw + kl,
@@ -820,19 +958,15 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
                     (uint32_t)(4 * (q >> 1)),
                     (uint32_t)(2 * q),
                     (uint32_t)(16 * q),
-                    // gathers: lane (e, slot) = (kl, q) here
                     kl < 4 ? Mb + kl * 16 : (const char *)Pr,
                     kl < 4 ? (uint32_t)MREC : 16u,
                     kl < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu,
                     (uint32_t)(kl < 4 ? W_META : W_O),
-                    // stores
                     q < 4 ? (char *)Mb + q * 16 : Pr,
                     q < 4 ? (uint32_t)MREC : 16u,
                     (uint32_t)(((q >> 1) * 8 + kl) * 16 + (q & 1) * 8),
                     (uint32_t)((32 + kl) * 16 + 4 * (q >> 1))};
-    sl.init_st();
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
-    constexpr int NI = CF::NI, NS = CF::NS;
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
         // line cache prologue: the lines resident at a segment start (LcPlan::pro)
         for (int i = st_id; i < 8 * a.n_pro; i += NSL) {
@@ -849,12 +983,7 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             sl.psel = 0x0c0c0000u | ((conv & 2u) ? 0x0300u : 0x0700u) | ((conv & 1u) ? 0x01u : 0x05u);
         }
         St3 st[NS];
-        uint4 pend[3];   // line loads of periods p-2, p-1, p (written to their slots in period p+2)
-#pragma unroll
-        for (int i = 0; i < 3; i++) pend[i] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i <= R; i++) sl.gathers(sl.read_gidx(i), i);   // window i -> in[w][i]   (nw > R + 3)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // prologue 1b: the memory wave's first gathers landed
         PreIn in;
         Rec rcn = sl.read_rec(1 % a.nw);   // records of the next pre's window
         sl.read_pre(0, sl.read_rec(0), in);
@@ -862,21 +991,15 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             sl.template pre<true, ET>(0, in, st[0]);
         else
             sl.template pre<false, ET>(0, in, st[0]);
-        uint2 lop = sl.read_lop(0);   // line ops of the next period
         __syncthreads();   // prologue 2
         if (STAMP) t0 = stamp3();
         int uA = a.nw - 1;   // local index of window p-1 (post)
         int uB = 1 % a.nw;   // local index of window p+1 (pre)
-        StIn sc;             // the store of window p-2 (read from the stage at the end of period p-1)
-        sc.addr = Pr + (size_t)a.m * 16;
         // Period p: post of window p-1 (state st[(p-1) % NS], x inputs from the
-        // chain's window p-1, info V into the line cache); pre of window p+1
-        // (inputs from the line cache and in[w][(p+1) % NI], -> st[(p+1) % NS]).
-        // Vector memory, in this order every period (the counts are static, so
-        // that vmcnt(6) before the pre is the gathers of window p+1 and the
-        // line loads of period p-2): the store of window p-2 (messages + parity
-        // rows), the line writeback of period p, the LDS-DMA gathers of window
-        // p+1+R, the line load of period p.  The plan only keeps neighbouring
+        // chain's window p-1, info V into the line cache, parity V and messages
+        // staged for the memory wave); pre of window p+1 (inputs from the line
+        // cache and in[w][(p+1) % NI], -> st[(p+1) % NS]).  No vector memory:
+        // the memory wave moves everything.  The plan only keeps neighbouring
         // windows free of shared information variables (dist 1): a value window
         // p+1 reads may have been written by the post of window p-1 in this same
         // period; the host puts every such writer and reader in slab wave 0,
@@ -885,73 +1008,40 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
         // start, 2 mid-post, 1 at the pre, 0 mid-pre) ran 1.2 % slower than two
         constexpr int MP1 = -1, MP2 = -1, P0 = 1, P1 = 0;
         const bool fair = a.slab_prio == 2;
-        // mode: 0 guarded, 1 fast, 2 decided here (fast unless the period posts,
-        // pres or stores the tail window)
-        auto period = [&](auto sc_, auto mode_, int p) __attribute__((always_inline)) {
+        // guarded: the first and last periods, and those posting or pre-ing the tail window
+        auto period = [&](auto sc_, auto guarded_, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
-            constexpr int MODE = decltype(mode_)::value;
+            constexpr bool GU = decltype(guarded_)::value;
             if (STAMP) tx = stampL();
             const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
-            bool fast = MODE == 1;
-            if constexpr (MODE == 2) {
-                const int d = uA == 0 ? (a.tail + 1 == a.nw ? 0 : a.tail + 1) : a.tail - uA + 1;   // tail - (p-2)
-                fast = d != 0 && d != 1 && d != 3 && d != 1 - a.nw && d != 3 - a.nw;
-            }
+            const bool fast = !GU && uA != a.tail && uB != a.tail;
             PreIn in;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
             const Rec rcp = sl.read_rec(p - 1);     // the post's records
-            const uint4 wbd = sl.wb_read(lop);      // the writeback's line piece (posts up to p-1 wrote it)
-            // every period issues the same four vector memory operations in
-            // the same order, guarded or not (unused ones on the sinks), so
-            // both vmcnt(6) here and the compiler's own waits for the line
-            // loads count exactly
-            uint32_t gi = (uint32_t)a.m;            // gathers of window p+1+R (sink rows when there is none)
-            uint32_t xr = 0;
             if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
-                // state in VGPRs) and waits for its window p+1 gathers and line
-                // loads only before its pre
+                // state in VGPRs), then reads and runs its pre
                 if (fair) __builtin_amdgcn_s_setprio(P0);
-                sl.stores(sc);
-                xr = sl.read_x(p - 1, sp);
-                gi = sl.read_gidx(p + 1 + R);
+                const uint32_t xr = sl.read_x(p - 1, sp);
                 sl.template post<false, ET, MP1>(p - 1, xr, sp, rcp);
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                sl.stores(sc);   // (the sink before period 2)
-                if (dpo) {
-                    xr = sl.read_x(p - 1, sp);
-                    if (uA == a.tail)
-                        sl.template post<true, ET>(p - 1, xr, sp, rcp);
-                    else
-                        sl.template post<false, ET>(p - 1, xr, sp, rcp);
-                }
-                if (dpr) gi = sl.read_gidx(p + 1 + R);
-            }
-            sl.wb_store(lop, wbd);
-            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // gathers of window p+1, line loads of period p-2
-            sl.line_put(lop, pend[(s + 1) % 3]);
-            if (fast || dpr) sl.read_pre((s + 1) % NI, rcn, in);
-            sl.gathers(gi, (s + R + 1) % NI);
-            pend[s] = sl.line_load(lop);
-            if (fast) {
-                sl.read_st(p - 1, false, sc);
+                sl.read_pre((s + 1) % NI, rcn, in);
                 rcn = sl.read_rec(p + 2);
-                lop = sl.read_lop(p + 1);
                 if (STAMP) t1 = t2 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(P1);
                 sl.template pre<false, ET, MP2>(p + 1, in, sn);
                 if (STAMP) t3 = stampL();
             } else {
-                if (STAMP) t1 = t2 = t3 = stampL();
                 if (dpo) {
-                    sl.read_st(p - 1, uA == a.tail, sc);
-                } else {
-                    sc.addr = Pr + (size_t)a.m * 16;
+                    const uint32_t xr = sl.read_x(p - 1, sp);
+                    if (uA == a.tail)
+                        sl.template post<true, ET>(p - 1, xr, sp, rcp);
+                    else
+                        sl.template post<false, ET>(p - 1, xr, sp, rcp);
                 }
+                if (STAMP) t1 = t2 = t3 = stampL();
+                if (dpr) sl.read_pre((s + 1) % NI, rcn, in);
                 rcn = sl.read_rec(p + 2);
-                lop = sl.read_lop(p + 1);
                 if (dpr) {
                     if (uB == a.tail)
                         sl.template pre<true, ET>(p + 1, in, sn);
@@ -972,45 +1062,23 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop3_decode(Coop3Args a)
             next(uA);
             next(uB);
         };
-        using GUARD = std::integral_constant<int, 0>;
-        using FAST = std::integral_constant<int, 1>;
-        using RT = std::integral_constant<int, 2>;
+        using T = std::true_type;
+        using F = std::false_type;
         // periods 0 .. U guarded
         static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
-            if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, GUARD{}, decltype(jc)::value);
+            if (decltype(jc)::value <= G) period(std::integral_constant<int, decltype(jc)::value % U>{}, T{}, decltype(jc)::value);
         });
         int p = U + 1;
-        // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U.
-        if constexpr (ET) {
-            // the ET kernel decides per period (one loop body keeps its
-            // registers within 256)
-            for (; p + U - 1 <= G - 2; p += U)
-                static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
-                    period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, RT{}, p + decltype(jc)::value);
-                });
-        } else {
-            // trips of U periods, fast unless one of them posts, pres or stores
-            // the tail window (windows p-2 .. p+U of the trip): no per-period
-            // branch, so the compiler's own vmcnt waits count exactly
-            for (; p + U - 1 <= G - 2; p += U) {
-                int d = (a.tail - uA + 1) % a.nw;   // windows from p-2 to the tail
-                if (d < 0) d += a.nw;
-                if (d >= U + 3)
-                    static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
-                        period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, FAST{}, p + decltype(jc)::value);
-                    });
-                else
-                    static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
-                        period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, GUARD{}, p + decltype(jc)::value);
-                    });
-            }
-        }
+        // periods p .. p+U-1 with p = 1 (mod U): slot index (1 + j) % U
+        for (; p + U - 1 <= G - 2; p += U)
+            static_for<0, U>([&](auto jc) __attribute__((always_inline)) {
+                period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, F{}, p + decltype(jc)::value);
+            });
         // the rest (at most U + 1 periods: p .. G), guarded
         static_for<0, U + 1>([&](auto jc) __attribute__((always_inline)) {
             if (p + decltype(jc)::value <= G && p + decltype(jc)::value > U)
-                period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, GUARD{}, p + decltype(jc)::value);
+                period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
         });
-        sl.stores(sc);   // window G-1
         // line cache epilogue: the dirty lines still resident (LcPlan::epi)
         __syncthreads();
         for (int i = st_id; i < 8 * a.n_epi; i += NSL) {
@@ -1040,7 +1108,7 @@ int env_int3(const char *name, int def)
 template <int WS>
 void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
 {
-    constexpr int nwaves = WS + 1, CHW = WS >= 3 ? 3 : WS;
+    constexpr int nwaves = WS + 2, CHW = WS >= 3 ? 3 : WS;
     std::vector<unsigned long long> h((size_t)grid * nwaves * 8);
     if (hipStreamSynchronize(s) != hipSuccess ||
         hipMemcpy(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
@@ -1068,7 +1136,7 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
 template <int WS, int R>
 int launch_wsr(const Coop3Args &a, int grid, bool stamped, hipStream_t s)
 {
-    constexpr int threads = 64 * (WS + 1);
+    constexpr int threads = 64 * (WS + 2);
     if (stamped)
         hipLaunchKernelGGL((coop3_decode<WS, R, true>), dim3(grid), dim3(threads), 0, s, a);
     else
@@ -1288,18 +1356,18 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups
     if (et) {
         if (nms)
-            hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+            hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 8), 0, s, a);
         else
-            hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+            hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (nms) {
-        hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true>), dim3(grid), dim3(64 * 7), 0, s, a);
+        hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0;
     if (stamped) {
-        const size_t bytes = (size_t)grid * 7 * 8 * sizeof(unsigned long long);
+        const size_t bytes = (size_t)grid * 8 * 8 * sizeof(unsigned long long);
         if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }

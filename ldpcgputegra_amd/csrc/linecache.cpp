@@ -17,10 +17,10 @@
 //     of window p+1);
 //   * a residency (a line's accesses, split where two are >= LC_GAP periods
 //     apart) is loaded into VGPRs in period tl <= f - 3 (f = first access) by
-//     lane group i of slab wave w, written into its LDS slot by the same lanes
-//     in period tl + 2, and -- if written to -- written back (slot -> VGPRs ->
-//     HBM, whole line) in period tw >= e + 1 (e = last access); the slot is
-//     held over [tl + 2, tw];
+//     lane group i of slab wave w's set, written into its LDS slot by the same
+//     lanes in period tl + LC_PUT, and -- if written to -- written back (slot ->
+//     VGPRs -> HBM, whole line) in period tw >= e + 1 (e = last access); the
+//     slot is held over [tl + LC_PUT, tw];
 //   * a line written back is loaded again >= 3 periods after its store (the
 //     kernel's per-period vmcnt waits complete a store by then);
 //   * at most LC_OPS loads and LC_OPS writebacks per period (6 slab waves x 8
@@ -164,7 +164,7 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
         for (int i = 0; i < (int)rs.size(); i++) {
             Res &R = rs[i];
             if (R.whole) continue;
-            while (cmod(R.tl, nw) >= nw - 2) {
+            while (cmod(R.tl, nw) >= nw - LC_PUT) {
                 R.tl--;
                 moved = true;
                 if (!reload_ok(prev_of(i), i)) return lc_fail(__LINE__);
@@ -209,17 +209,17 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     }
     for (int i = 0; i < (int)rs.size(); i++) {
         if (rs[i].whole) continue;
-        if (rs[i].tw - (rs[i].tl + 2) >= nw - 1) return lc_fail(__LINE__);
+        if (rs[i].tw - (rs[i].tl + LC_PUT) >= nw - 1) return lc_fail(__LINE__);
         if (!reload_ok(prev_of(i), i) || !reload_ok(i, next_of(i))) return lc_fail(__LINE__);
     }
-    // slots: circular-arc assignment of the holds [tl + 2, tw].  Cut at the
+    // slots: circular-arc assignment of the holds [tl + LC_PUT, tw].  Cut at the
     // period p0 with the fewest holds: the holds across p0 get a slot each,
     // the rest go in order of their start to the free slot whose next hold
     // starts soonest after them (best fit)
     std::vector<int> live(nw, 0);
     for (const Res &R : rs)
         if (!R.whole)
-            for (int p = R.tl + 2; p <= R.tw; p++) live[cmod(p, nw)]++;
+            for (int p = R.tl + LC_PUT; p <= R.tw; p++) live[cmod(p, nw)]++;
     // assignment from the cut at p0; returns the slots used (sink excluded)
     auto assign = [&](int p0) -> int {
         std::vector<int> free_from, next_busy;   // per slot 1.. (index + 1), relative to p0
@@ -233,7 +233,7 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
                 next_busy.push_back(-1);
                 continue;
             }
-            const int a = R.tl + 2, len = R.tw - a;
+            const int a = R.tl + LC_PUT, len = R.tw - a;
             if (cmod(p0 - a, nw) <= len) {   // across p0
                 R.slot = (int)free_from.size() + 1;
                 free_from.push_back(cmod(R.tw - p0, nw) + 1);
@@ -243,12 +243,12 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
             }
         }
         std::sort(order.begin(), order.end(), [&](int x, int y) {
-            const int ax = cmod(rs[x].tl + 2 - p0, nw), ay = cmod(rs[y].tl + 2 - p0, nw);
+            const int ax = cmod(rs[x].tl + LC_PUT - p0, nw), ay = cmod(rs[y].tl + LC_PUT - p0, nw);
             return ax != ay ? ax < ay : x < y;
         });
         for (int i : order) {
             Res &R = rs[i];
-            const int ra = cmod(R.tl + 2 - p0, nw), rb = ra + (R.tw - (R.tl + 2));
+            const int ra = cmod(R.tl + LC_PUT - p0, nw), rb = ra + (R.tw - (R.tl + LC_PUT));
             int best = -1;
             for (int c = 0; c < (int)free_from.size(); c++) {
                 if (free_from[c] > ra || next_busy[c] <= rb) continue;
@@ -306,7 +306,7 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
         if (R.whole) continue;
         uint32_t *ld = &o.ops[((size_t)cmod(R.tl, nw) * LC_OPS + R.li) * 2];
         ld[0] = (ld[0] & 0xFFFF0000u) | R.line;
-        uint32_t *dw = &o.ops[((size_t)cmod(R.tl + 2, nw) * LC_OPS + R.li) * 2];
+        uint32_t *dw = &o.ops[((size_t)cmod(R.tl + LC_PUT, nw) * LC_OPS + R.li) * 2];
         dw[1] = (dw[1] & 0xFFFF0000u) | (uint32_t)R.slot;
         if (R.dirty) {
             uint32_t *wb = &o.ops[((size_t)cmod(R.tw, nw) * LC_OPS + R.wi) * 2];
@@ -339,7 +339,7 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
         if (R.whole) {
             o.pro.push_back(w);
             if (R.dirty) o.epi.push_back(w);
-        } else if (R.tl + 2 <= -1 || R.tw >= nw) {
+        } else if (R.tl + LC_PUT <= -1 || R.tw >= nw) {
             o.pro.push_back(w);
             // dirty at a segment end: written before it (posts run up to period nw) and not yet written back
             if (R.dirty && R.tw >= nw + 1 && R.fw <= nw) o.epi.push_back(w);
@@ -393,7 +393,8 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
         return 0;
     };
     const long G = (long)nw * iters;
-    std::vector<uint32_t> pend((size_t)3 * LC_OPS, sink_line);   // loads of periods P-2, P-1, P
+    constexpr int NPD = LC_PUT + 1;
+    std::vector<uint32_t> pend((size_t)NPD * LC_OPS, sink_line);   // loads of periods P-LC_PUT .. P
     if (access(0, false, -1)) return -1;                           // the pre of window 0 before period 0
     for (long P = 0; P <= G; P++) {
         const int p = (int)(P % nw);
@@ -426,9 +427,9 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
         // slot writes of the loads of period P-2
         for (int i = 0; i < LC_OPS; i++) {
             const int s = (int)(ops[2 * i + 1] & 0xFFFFu);
-            const uint32_t L = pend[(size_t)((P + 1) % 3) * LC_OPS + i];
+            const uint32_t L = pend[(size_t)((P + 1) % NPD) * LC_OPS + i];   // the load of period P - LC_PUT
             if (s == 0) {
-                if (L != sink_line && P >= 2) return fail("load without a slot", P, s, (int)L);
+                if (L != sink_line && P >= LC_PUT) return fail("load without a slot", P, s, (int)L);
                 continue;
             }
             if (L == sink_line) return fail("slot write without a load", P, s, (int)L);
@@ -440,7 +441,7 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
         // loads
         for (int i = 0; i < LC_OPS; i++) {
             const uint32_t L = ops[2 * i] & 0xFFFFu;
-            pend[(size_t)(P % 3) * LC_OPS + i] = L;
+            pend[(size_t)(P % NPD) * LC_OPS + i] = L;
             if (L == sink_line) continue;
             if (L >= (uint32_t)k / 8) return fail("load of a bad line", P, i, (int)L);
             if (dirty_copies[L] != 0) return fail("load while a dirty copy is resident", P, i, (int)L);
