@@ -386,18 +386,22 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     // keeps V grouped per 16 codewords instead (coop3_group_bytes per group).
     const int vpad = kern == 5 ? std::max(0, getenv_int("LDPC_VPITCH_PAD", 64)) / 64 * 64 : 0;
     const int vpitch = stride + vpad;
-    const size_t vgroup = kern == 8 ? coop3_group_bytes(h) : 0;
+    size_t vpart = 0, vgroup = 0;   // coop3: per-group blocks of V rows then messages
+    if (kern == 8) coop3_group_layout(h, &vpart, &vgroup);
     const size_t v_bytes = kern == 8 ? (size_t)(stride / 16) * vgroup
                                      : ((size_t)h->n + 1) * vpitch * esz;   // row n: the coop kernel's sink row
     if ((rc = ensure(&sc.d_V, &sc.V_bytes, v_bytes)) != LDPC_OK) return rc;
-    if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_zero)) != LDPC_OK) return rc;
+    if (kern != 8 && (rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_zero)) != LDPC_OK) return rc;
     // early termination: live u8 | bad u32 | iterations used i32 (when the caller passed none)
     const bool et_state = (kern == 5 || kern == 8) && p->early_term;
     if (et_state && (rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
     if (alloc_only) return LDPC_OK;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
-    HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));
+    if (kern == 8)
+        HIP_TRY(hipMemset2DAsync((char *)sc.d_V + vpart, vgroup, 0, (size_t)(h->m + 1) * 64, (size_t)(stride / 16), s));
+    else
+        HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));
     if (is_float) {
         if (launch_interleave_f32((const float *)d_llr, (float *)sc.d_V, h->n, batch, vpitch, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
@@ -410,7 +414,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     }
     DecodeLaunch L{};
     L.V = sc.d_V;
-    L.msg = sc.d_msg;
+    L.msg = kern == 8 ? (void *)((char *)sc.d_V + vpart) : sc.d_msg;
     L.vgroup = vgroup;
     L.stride = stride;
     L.vpitch = vpitch;

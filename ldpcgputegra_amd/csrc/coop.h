@@ -60,7 +60,9 @@ int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPl
 // ---- coop3.hip: slab waves doing pre + post, i16 chain (D0 = 7) ----
 bool coop3_params_ok(const ldpc_params *p, const CoopCode &cc);
 bool coop3_stride_ok(int stride);
-// bytes between two codeword groups of coop3's grouped V (DecodeLaunch::vgroup)
+// coop3's per-group block (V rows, then messages): bytes of the V part and of
+// the block = the stride between two codeword groups (DecodeLaunch::vgroup)
+void coop3_group_layout(const ldpc_code *h, size_t *vpart, size_t *block);
 size_t coop3_group_bytes(const ldpc_code *h);
 // compressed messages: [stride / 16][m + 1][8 pairs][2] u32 (4 B per codeword and check; row m is the sink)
 size_t coop3_msg_bytes(const ldpc_code *h, int stride);

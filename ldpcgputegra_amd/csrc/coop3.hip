@@ -29,22 +29,26 @@
 // * V lives in the grouped layout Vg[group][row][16 codewords] and the
 //   information rows move between HBM and the workgroup's LDS as whole 128-B
 //   lines (8 rows x 16 codewords) through a line cache planned on the host
-//   (linecache.cpp: each line is loaded ~3 periods before its first use and
-//   written back after its last, one residency serving ~8 checks): a period's
-//   vector memory is one 64-lane store (messages + parity rows), one 64-lane
-//   line writeback, one 64-lane LDS-DMA gather (messages + o-edge parity rows)
-//   and one 64-lane line load per slab wave -- whole lines, no scattered 16-B
-//   V pieces (on MI355X the CU's texture path stalled on those: 47 ms per
-//   launch, 18 % of it on the info-row stores alone);
+//   (linecache.cpp: each line is loaded 4 periods before its first use and
+//   written back after its last, one residency serving ~8 checks) -- whole
+//   lines, no scattered 16-B V pieces (on MI355X the CU's texture path stalled
+//   on those: 47 ms per launch, 18 % of it on the info-row stores alone,
+//   DESIGN.md §8);
+// * an eighth wave, the memory wave, shares the chain wave's SIMD and issues
+//   every vector-memory operation of the workgroup: per period and slab-wave
+//   set of 8 slots one LDS-DMA gather (messages + o-edge parity rows), one
+//   64-lane line load, one line writeback and one store (messages + x-edge
+//   parity rows).  The slab waves only compute (their share of the memory
+//   work cost ~10 % of their VALU-bound period);
 // * the pre / post of a check read / write its info rows in the line cache,
 //   so a value written by the post of window u-1 .. u-2 is simply there for
 //   the pre of window u (the host keeps distance-2 writers and readers in slab
 //   wave 0, which posts before its pre).
 //
 // Period p (one s_barrier): chain = steps of window p; slab waves = post of
-// window p-1, pre of window p+1, stores of window p-2, gathers of window
-// p+1+R, the line cache's writebacks / loads of period p and the slot writes
-// of the lines loaded in period p-2.
+// window p-1, pre of window p+1; memory wave = stores of window p-2, gathers
+// of window p+1+R, the line cache's writebacks / loads of period p and the
+// slot writes of the lines loaded in period p-3.
 //
 // The chain recurrence (check i, x edge input Y = V[p_{i-1}]):
 //   V[p_i] = clamp(c_o + eps * sign(c_x) * min(max(|c_x| - off, 0), T), +-127)
@@ -68,7 +72,23 @@
 
 #include "pk16.h"
 
+// raw buffer access: address = resource base + voffset (+ soffset)
+__device__ i32x4 rbuf_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+__device__ void rbuf_store_v4(i32x4 v, i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.v4i32");
+
 namespace {
+
+// LDS-DMA through a buffer resource: every active lane copies the 16 B at
+// rsrc + voff to lds_dst + 16 * lane (as dma16, not counted by the compiler)
+LDPC_DEV void dma16_buf(i32x4 rsrc, uint32_t voff, uint32_t lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rsrc), "s"(lds_dst)
+                 : "memory");
+}
 
 constexpr int D0 = 7, X = D0 - 2;   // first-group check degree, information edges per check
 constexpr int RECW = 12;            // slot record words (coop3_upload)
@@ -796,7 +816,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     }
 
     char *Pr = Vg + (size_t)a.k * 16;   // parity row k + j at Pr + 16 j (row n: the sink)
-    const char *Mb = (const char *)a.Mc + (size_t)wg * a.mrows * MREC;
+    const char *Mb = (const char *)a.Mc + (size_t)wg * a.gstride;   // the group's messages (coop3_group_layout)
     constexpr int NI = CF::NI, NS = CF::NS;
     constexpr int MW = WS + 1;   // the memory wave (shares the chain wave's SIMD)
     const int kl = lane >> 3, q = lane & 7;
@@ -817,20 +837,25 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         // so the counts are static.
         char *lcb = (char *)&sm.lc[0][0];
         const uint32_t lq = 16u * (uint32_t)q;
+        // every access of the group's block (coop3_group_layout: V rows, then
+        // messages) through one buffer resource with 32-bit offsets: one VALU
+        // per address (shift-and-add with a per-lane shift and base)
+        const i32x4 vr = buffer_rsrc(Vg, 0u, 0xFFFFFFFFu);
+        const uint32_t moff = (uint32_t)(Mb - (const char *)Vg), poff = (uint32_t)a.k * 16u;
         // gathers: lane (e, slot) = (kl, q): e < 4 message piece e, e = 4 the o-edge parity row
-        const char *gbase = kl < 4 ? Mb + kl * 16 : (const char *)Pr;
-        const uint32_t gmul = kl < 4 ? (uint32_t)MREC : 16u, gmask = kl < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
+        const uint32_t gshl = kl < 4 ? 6u : 4u, goff = kl < 4 ? moff + 16u * (uint32_t)kl : poff;
+        const uint32_t gmask = kl < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
         const uint32_t gsel = (uint32_t)(kl < 4 ? W_META : W_O);
         // stores: lane (kl, q) of slot 8w + kl: q < 4 message piece q, q = 4 the
         // x-edge parity row, q = 5 the tail's last edge, the rest the sink row
-        char *sbase = q < 4 ? (char *)Mb + q * 16 : Pr;
-        const uint32_t smul = q < 4 ? (uint32_t)MREC : 16u;
+        const uint32_t sshl = q < 4 ? 6u : 4u, soff = q < 4 ? moff + 16u * (uint32_t)q : poff;
         const uint32_t stw = 4u * (uint32_t)(q < 4 ? W_META : q == 4 ? W_X : W_O);
         const uint32_t stm = q < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
         const uint32_t snk = q >= 5 ? 0xFFFFFFFFu : 0u, snk_tl = q >= 6 ? 0xFFFFFFFFu : 0u;
+        static_assert(MREC == 64, "message block of a check: 1 << 6 bytes");
         auto gather = [&](int w, int g, int ib) __attribute__((always_inline)) {
             const uint32_t idx = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
-            if (lane < 40) dma16(gbase + (size_t)idx * gmul, (uint32_t)(uintptr_t)&sm.in[w][ib]);
+            if (lane < 40) dma16_buf(vr, (idx << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][ib]);
         };
         // the store of window g's slots 8w .. 8w+7: its row / check index, read
         // from window g's records one period before the store (the chain wave
@@ -842,7 +867,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         };
         auto store_win = [&](int w, int g, uint32_t idx) __attribute__((always_inline)) {
             const uint4 *src = q < 4 ? &sm.mst[g & 1][w][kl][q] : &sm.stg[g & 1][q == 4 ? 0 : 1][8 * w + kl];
-            *(uint4 *)(sbase + (size_t)idx * smul) = *src;
+            rbuf_store_v4(__builtin_bit_cast(i32x4, *src), vr, (int)((idx << sshl) + soff), 0, 0);
         };
         for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
             __syncthreads();   // prologue 1: tables and resident lines in LDS
@@ -853,6 +878,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();   // prologue 1b: the first windows' gathers landed
             __syncthreads();   // prologue 2
+            if (STAMP) t0 = stamp3();
             constexpr int NPD = LC_PUT + 1;
             uint4 pend[NPD][WS];   // line loads of periods p-LC_PUT .. p (written to their slots LC_PUT periods on)
 #pragma unroll
@@ -876,6 +902,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             // >= 3 periods later, linecache.cpp)
             auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
                 constexpr int s = decltype(sc_)::value;   // p % NPD
+                if (STAMP) tx = stampL();
                 uint32_t gix[WS];
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
@@ -887,17 +914,18 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 });
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
-                    if (lane < 40)
-                        dma16(gbase + (size_t)gix[w] * gmul, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
+                    if (lane < 40) dma16_buf(vr, (gix[w] << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
                 });
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
-                    pend[s][w] = *(const uint4 *)(Vg + (size_t)(lop[w].x & 0xFFFFu) * 128 + lq);
+                    pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(((lop[w].x & 0xFFFFu) << 7) + lq), 0, 0));
                 });
+                // (reading all of a period's writeback / store pieces from LDS
+                // first, so that their latencies overlap, ran 2 % slower)
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
                     const uint4 v = *(const uint4 *)(lcb + (lop[w].y >> 16) * 128u + lq);
-                    *(uint4 *)(Vg + (size_t)(lop[w].x >> 16) * 128 + lq) = v;
+                    rbuf_store_v4(__builtin_bit_cast(i32x4, v), vr, (int)(((lop[w].x >> 16) << 7) + lq), 0, 0);
                 });
                 // the stores of window p-2 (the sink before period 2), then the
                 // indices of window p-1's and the next period's line ops
@@ -910,7 +938,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     sidx[w] = store_idx(w, p - 1, uS == a.tail, p >= 1);
                     lop[w] = *(const uint2 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][W_LOP];
                 });
+                if (STAMP) sP[1] += stampL() - tx;
                 asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+                if (STAMP) sA += stampL() - tx;
                 __syncthreads();
                 uS = (uS + 1 == a.nw) ? 0 : uS + 1;
             };
@@ -1297,14 +1327,24 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
     return LDPC_OK;
 }
 
-// the group stride of coop3's V: rows 0 .. n+7 (row n and the line n / 8:
-// the sinks) of 16 B, an odd number of 128-B lines (groups spread over the L2
-// channels)
+// coop3's per-group block: the group's V rows 0 .. n+7 (row n and the line
+// n / 8: the sinks) of 16 B, then its messages ((m + 1) checks x 64 B), an odd
+// number of 128-B lines in all (groups spread over the L2 channels).  One
+// block per group lets the memory wave address all of it with 32-bit buffer
+// offsets from one resource
+void coop3_group_layout(const ldpc_code *h, size_t *vpart, size_t *block)
+{
+    const size_t vlines = ((size_t)h->n + 8 + 7) / 8, mlines = ((size_t)(h->m + 1) * MREC + 127) / 128;
+    size_t lines = vlines + mlines;
+    if (lines % 2 == 0) lines++;
+    *vpart = vlines * 128;
+    *block = lines * 128;
+}
 size_t coop3_group_bytes(const ldpc_code *h)
 {
-    size_t lines = ((size_t)h->n + 8 + 7) / 8;
-    if (lines % 2 == 0) lines++;
-    return lines * 128;
+    size_t v, b;
+    coop3_group_layout(h, &v, &b);
+    return b;
 }
 
 // the workgroup's LDS (the ET kernel stages the hard bits of all n variables,

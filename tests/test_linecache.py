@@ -1,0 +1,26 @@
+"""coop3's LDS line cache plan (ldpcgputegra_amd/csrc/linecache.cpp), host
+side: built for DVB-S2 r1/2 within the kernel's slot budget and self-checked
+by the planner's replay (lc_check_plan: every pre read / post write of the
+coop3 schedule finds its line in the slot its record names, no slot is
+refilled before its dirty line is written back, a line is reloaded only after
+its store completed, and the lines left dirty at a segment end are exactly
+the epilogue's).  No GPU needed."""
+import pytest
+
+from ldpcgputegra_amd.codes import Code, available
+
+
+def test_dvbs2_r1_2_plan_fits_and_replays():
+    lc = Code("dvbs2_r1_2").coop3_line_cache()
+    assert lc is not None, "no line-cache plan (LDPC_LC_DEBUG=1 names the planner line)"
+    assert 2 <= lc["slots"] <= lc["max_slots"]
+    # ~8 accesses per residency: 162000 info-edge accesses per iteration (x2, pre and post)
+    assert 12000 <= lc["residencies"] <= 21000
+    assert 0 < lc["epilogue"] <= lc["prologue"] < lc["slots"]
+
+
+@pytest.mark.parametrize("name", ["576x288", "dvbs2_r2_3"])
+def test_codes_without_coop3_have_no_plan(name):
+    if name not in available():
+        pytest.skip("code table absent")
+    assert Code(name).coop3_line_cache() is None
