@@ -398,9 +398,10 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     if (alloc_only) return LDPC_OK;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
-    if (kern == 8)
-        HIP_TRY(hipMemset2DAsync((char *)sc.d_V + vpart, vgroup, 0, (size_t)(h->m + 1) * 64, (size_t)(stride / 16), s));
-    else
+    if (kern == 8) {
+        if (launch_zero_rows((char *)sc.d_V + vpart, vgroup, ((size_t)(h->m + 1) * 64 + 15) / 16 * 16, stride / 16, s))
+            return ldpc_set_error(LDPC_EDEVICE, "message zeroing: %s", hipGetErrorString(hipGetLastError()));
+    } else
         HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));
     if (is_float) {
         if (launch_interleave_f32((const float *)d_llr, (float *)sc.d_V, h->n, batch, vpitch, s))

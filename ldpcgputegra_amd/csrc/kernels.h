@@ -53,6 +53,8 @@ int launch_interleave_grp_i8(const int8_t *llr, int8_t *V, int n, int batch, int
 int launch_deinterleave_grp_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, size_t gbytes,
                                hipStream_t s);
 
+// zero `width` bytes at base + r * pitch, r < rows (width, pitch multiples of 16)
+int launch_zero_rows(void *base, size_t pitch, size_t width, int rows, hipStream_t s);
 // rows of `row_bytes` bytes: dst[i] = src[idx[i]] (gather) / dst[idx[i]] = src[i] (scatter)
 int launch_gather_rows(const void *src, void *dst, const int32_t *idx, int rows, int row_bytes, hipStream_t s);
 int launch_scatter_rows(const void *src, void *dst, const int32_t *idx, int rows, int row_bytes, hipStream_t s);

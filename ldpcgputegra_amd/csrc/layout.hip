@@ -175,6 +175,14 @@ __global__ void __launch_bounds__(256) copy_rows_k(const uint8_t *__restrict__ s
     }
 }
 
+// zero `width` bytes (multiple of 16) at base + r * pitch for r < rows: one
+// block per row
+__global__ void __launch_bounds__(256) zero_rows_k(uint8_t *__restrict__ base, size_t pitch, size_t width)
+{
+    uint4 *p = (uint4 *)(base + (size_t)blockIdx.x * pitch);
+    for (size_t i = threadIdx.x; i < width / 16; i += 256) p[i] = make_uint4(0, 0, 0, 0);
+}
+
 inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -1; }
 
 }  // namespace
@@ -243,6 +251,12 @@ int launch_deinterleave_grp_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int
 {
     dim3 g((n + 63) / 64, (batch + 63) / 64);
     hipLaunchKernelGGL(deinterleave_grp_k, g, dim3(256), 0, s, V, hard, soft, n, batch, gbytes);
+    return ok();
+}
+int launch_zero_rows(void *base, size_t pitch, size_t width, int rows, hipStream_t s)
+{
+    if (rows <= 0 || width % 16 != 0 || ((uintptr_t)base & 15) != 0 || pitch % 16 != 0) return -1;
+    hipLaunchKernelGGL(zero_rows_k, dim3(rows), dim3(256), 0, s, (uint8_t *)base, pitch, width);
     return ok();
 }
 int launch_awgn_i8(int8_t *llr, int n, int batch, uint64_t first_cw, uint64_t seed, const AwgnTable &t,
