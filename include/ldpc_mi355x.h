@@ -204,6 +204,16 @@ int ldpc_decode_i8_async(ldpc_ctx *ctx, void *hip_stream, const int8_t *d_llr, u
 int ldpc_decode_f32_async(ldpc_ctx *ctx, void *hip_stream, const float *d_llr, uint8_t *d_hard,
                           float *d_soft, int32_t *d_iters_used, int batch, int n_iter,
                           const ldpc_params *p);
+/* Node-major device input: the LLR of bit i of codeword b at d_llr[i * ld + b]
+ * (ld >= batch), the interleaved layout the reference's kernels run on
+ * (Interleaver_uint8, code/gpu_fixed/transpose/GPU_Transpose_uint8.cu:80-130)
+ * and that CGPU_Decoder_MS_SIMD_v2::decode takes from its caller
+ * (code/gpu_fixed/decoder_oms_v2/CGPU_Decoder_MS_SIMD_v2.cu:120-251).  Same
+ * results as ldpc_decode_i8_async on the transposed input; d_hard / d_soft
+ * are frame-major [batch][N], as that decoder returns them. */
+int ldpc_decode_i8_nm_async(ldpc_ctx *ctx, void *hip_stream, const int8_t *d_llr, size_t ld, uint8_t *d_hard,
+                            int8_t *d_soft, int32_t *d_iters_used, int batch, int n_iter,
+                            const ldpc_params *p);
 
 /* ---- mixed-rate batches (BASELINE config 5) ---------------------------- */
 /* A batch whose codewords use different codes of equal length N (e.g. the

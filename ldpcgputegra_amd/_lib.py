@@ -65,6 +65,7 @@ SIGNATURES = {
     "ldpc_decode_f32": (I, [P, P, P, I, I, C.POINTER(ldpc_params)]),
     "ldpc_decode_i8_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params)]),
     "ldpc_decode_f32_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params)]),
+    "ldpc_decode_i8_nm_async": (I, [P, P, P, C.c_size_t, P, P, P, I, I, C.POINTER(ldpc_params)]),
     "ldpc_mixed_create": (I, [P, I, I, I, C.POINTER(P)]),
     "ldpc_mixed_destroy": (None, [P]),
     "ldpc_decode_i8_mixed_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params)]),

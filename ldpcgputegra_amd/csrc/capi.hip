@@ -330,7 +330,7 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
 // the device)
 static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_llr, uint8_t *d_hard, void *d_soft,
                          int32_t *d_iters, int batch, int n_iter, const ldpc_params *p, bool is_float,
-                         bool alloc_only = false)
+                         bool alloc_only = false, size_t nm_ld = 0)
 {
     int rc = check_params(c, batch, n_iter, p, is_float);
     if (rc != LDPC_OK) return rc;
@@ -344,6 +344,12 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d selected but not applicable to these params", c->kernel);
     c->last_kernel = kern;
     if (kern == 7 && alloc_only) return LDPC_OK;
+    if (kern == 7 && nm_ld) {   // node-major input: transpose it to frame-major scratch first
+        if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, (size_t)h->n * batch)) != LDPC_OK) return rc;
+        if (launch_deinterleave_i8((const int8_t *)d_llr, nullptr, (int8_t *)sc.d_msg, h->n, batch, (int)nm_ld, s))
+            return ldpc_set_error(LDPC_EDEVICE, "node-major transpose: %s", hipGetErrorString(hipGetLastError()));
+        d_llr = sc.d_msg;
+    }
     if (kern == 7) {   // LDS-resident: frame-major in and out, no scratch, no transposes
         DecodeLaunch L{};
         L.batch = batch;
@@ -403,7 +409,11 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
             return ldpc_set_error(LDPC_EDEVICE, "message zeroing: %s", hipGetErrorString(hipGetLastError()));
     } else
         HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));
-    if (is_float) {
+    if (nm_ld) {   // node-major input: 16-codeword pieces copied straight into V (no transpose)
+        const size_t gstep = kern == 8 ? vgroup : 16, rstep = kern == 8 ? 16 : (size_t)vpitch;
+        if (launch_nm_pieces_i8((const int8_t *)d_llr, nm_ld, h->n, batch, stride, (int8_t *)sc.d_V, gstep, rstep, s))
+            return ldpc_set_error(LDPC_EDEVICE, "node-major load: %s", hipGetErrorString(hipGetLastError()));
+    } else if (is_float) {
         if (launch_interleave_f32((const float *)d_llr, (float *)sc.d_V, h->n, batch, vpitch, s))
             return ldpc_set_error(LDPC_EDEVICE, "interleave: %s", hipGetErrorString(hipGetLastError()));
     } else if (kern == 8) {
@@ -479,6 +489,23 @@ extern "C" int ldpc_decode_i8_async(ldpc_ctx *c, void *s, const int8_t *d_llr, u
 {
     if (!c || (!d_llr && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr");
     return decode_device(c, c->sc, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, false);
+}
+
+// Node-major input: LLR of bit i of codeword b at d_llr[i * ld + b] -- the
+// layout the reference's decoders run on (Interleaver_uint8's output,
+// code/gpu_fixed/transpose/GPU_Transpose_uint8.cu:80-130), which its v2 decoder
+// takes straight from the caller (CGPU_Decoder_MS_SIMD_v2::decode,
+// code/gpu_fixed/decoder_oms_v2/CGPU_Decoder_MS_SIMD_v2.cu:120-251: copy,
+// decode, InvInterleaver_uint8 with the hard decision).  Outputs frame-major,
+// as there.
+extern "C" int ldpc_decode_i8_nm_async(ldpc_ctx *c, void *s, const int8_t *d_llr, size_t ld, uint8_t *d_hard,
+                                       int8_t *d_soft, int32_t *d_iters, int batch, int n_iter, const ldpc_params *p)
+{
+    if (!c || (!d_llr && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr");
+    if (batch > 0 && ld < (size_t)batch)
+        return ldpc_set_error(LDPC_EINVAL, "node-major pitch %zu < batch %d", ld, batch);
+    return decode_device(c, c->sc, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, false, false,
+                         batch > 0 ? ld : 0);
 }
 
 extern "C" int ldpc_decode_f32_async(ldpc_ctx *c, void *s, const float *d_llr, uint8_t *d_hard, float *d_soft,

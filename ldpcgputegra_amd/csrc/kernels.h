@@ -53,6 +53,10 @@ int launch_interleave_grp_i8(const int8_t *llr, int8_t *V, int n, int batch, int
 int launch_deinterleave_grp_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, size_t gbytes,
                                hipStream_t s);
 
+// node-major [N][ld] (codeword fastest, the reference's interleaved layout) -> 16-codeword pieces:
+// piece (g, i) at dst + g * gstep + i * rstep, g < stride / 16; codewords >= batch zero
+int launch_nm_pieces_i8(const int8_t *llr, size_t ld, int n, int batch, int stride, int8_t *dst, size_t gstep,
+                        size_t rstep, hipStream_t s);
 // zero `width` bytes at base + r * pitch, r < rows (width, pitch multiples of 16)
 int launch_zero_rows(void *base, size_t pitch, size_t width, int rows, hipStream_t s);
 // rows of `row_bytes` bytes: dst[i] = src[idx[i]] (gather) / dst[idx[i]] = src[i] (scatter)

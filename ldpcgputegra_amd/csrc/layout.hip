@@ -114,6 +114,34 @@ __global__ void __launch_bounds__(256) deinterleave_grp_k(const int8_t *__restri
     }
 }
 
+// node-major input (the reference's interleaved layout, Interleaver_uint8's
+// output: LLR of node i, codeword b at src[i * ld + b]) -> the decoder's
+// 16-codeword pieces: piece (group g, node i) = codewords 16g..16g+15 of node
+// i, stored at dst + g * gstep + i * rstep (grouped layout: gstep = the group
+// block, rstep = 16; row layout: gstep = 16, rstep = the row pitch).  No
+// transpose: a wave reads 16 nodes x 4 groups (64 contiguous bytes per node)
+// and writes 4 runs of 16 contiguous pieces.  Codewords >= batch are zero.
+__global__ void __launch_bounds__(256) nm_pieces_k(const int8_t *__restrict__ src, size_t ld, int n, int batch,
+                                                   int groups, int8_t *__restrict__ dst, size_t gstep, size_t rstep,
+                                                   int vec)
+{
+    const int g = blockIdx.y * 4 + (threadIdx.x & 3), i = blockIdx.x * 64 + (threadIdx.x >> 2);
+    if (g >= groups || i >= n) return;
+    const int b0 = 16 * g;
+    const int8_t *p = src + (size_t)i * ld + b0;
+    uint4 v;
+    if (vec && b0 + 16 <= batch) {
+        v = *(const uint4 *)p;
+    } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if (b0 + j < batch) w[j >> 2] |= (uint32_t)(uint8_t)p[j] << (8 * (j & 3));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    *(uint4 *)(dst + (size_t)g * gstep + (size_t)i * rstep) = v;
+}
+
 __global__ void __launch_bounds__(256) awgn_i8_k(int8_t *__restrict__ llr, int n, int batch, uint64_t first_cw,
                                                  uint64_t seed, AwgnTable t, const uint8_t *__restrict__ cw)
 {
@@ -251,6 +279,15 @@ int launch_deinterleave_grp_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int
 {
     dim3 g((n + 63) / 64, (batch + 63) / 64);
     hipLaunchKernelGGL(deinterleave_grp_k, g, dim3(256), 0, s, V, hard, soft, n, batch, gbytes);
+    return ok();
+}
+int launch_nm_pieces_i8(const int8_t *llr, size_t ld, int n, int batch, int stride, int8_t *dst, size_t gstep,
+                        size_t rstep, hipStream_t s)
+{
+    const int groups = stride / 16;
+    const int vec = (ld % 16 == 0) && ((uintptr_t)llr % 16 == 0);
+    dim3 g((n + 63) / 64, (groups + 3) / 4);
+    hipLaunchKernelGGL(nm_pieces_k, g, dim3(256), 0, s, llr, ld, n, batch, groups, dst, gstep, rstep, vec);
     return ok();
 }
 int launch_zero_rows(void *base, size_t pitch, size_t width, int rows, hipStream_t s)

@@ -142,6 +142,20 @@ class Decoder:
             self._ctx, s, self._ptr(llr), self._ptr(hard), self._ptr(soft), self._ptr(iters_used), B, n_iter,
             C.byref(p))), self.device)
 
+    def decode_i8_nm_device(self, llr_nm, hard, n_iter, batch=None, params=None, soft=None, iters_used=None,
+                            stream=None):
+        """Node-major input llr_nm [N, ld] (codeword fastest; the reference's
+        interleaved layout, CGPU_Decoder_MS_SIMD_v2::decode), `batch` <= ld
+        codewords (default ld); hard / soft frame-major [batch, N]."""
+        assert llr_nm.dim() == 2 and llr_nm.shape[0] == self.code.n and llr_nm.stride(1) == 1
+        ld = llr_nm.stride(0)
+        B = llr_nm.shape[1] if batch is None else batch
+        assert B <= llr_nm.shape[1]
+        p = params or _lib.default_params()
+        self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_decode_i8_nm_async(
+            self._ctx, s, self._ptr(llr_nm), ld, self._ptr(hard), self._ptr(soft), self._ptr(iters_used), B, n_iter,
+            C.byref(p))), self.device)
+
     def decode_f32_device(self, llr, hard, n_iter, params=None, soft=None, iters_used=None, stream=None):
         B = llr.shape[0]
         assert llr.numel() == B * self.code.n and llr.is_contiguous()
