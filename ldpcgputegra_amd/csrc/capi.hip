@@ -411,7 +411,8 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));
     if (nm_ld) {   // node-major input: 16-codeword pieces copied straight into V (no transpose)
         const size_t gstep = kern == 8 ? vgroup : 16, rstep = kern == 8 ? 16 : (size_t)vpitch;
-        if (launch_nm_pieces_i8((const int8_t *)d_llr, nm_ld, h->n, batch, stride, (int8_t *)sc.d_V, gstep, rstep, s))
+        if (launch_nm_pieces_i8((const int8_t *)d_llr, nm_ld, h->n, batch, kern == 8 ? stride : vpitch, (int8_t *)sc.d_V,
+                                gstep, rstep, s))
             return ldpc_set_error(LDPC_EDEVICE, "node-major load: %s", hipGetErrorString(hipGetLastError()));
     } else if (is_float) {
         if (launch_interleave_f32((const float *)d_llr, (float *)sc.d_V, h->n, batch, vpitch, s))
