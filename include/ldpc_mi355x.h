@@ -187,6 +187,23 @@ int ldpc_decode_i8(ldpc_ctx *ctx, const int8_t *llr, uint8_t *hard, int batch, i
 int ldpc_decode_f32(ldpc_ctx *ctx, const float *llr, uint8_t *hard, int batch, int n_iter,
                     const ldpc_params *p);
 
+/* Host buffers, asynchronous: enqueue H2D(llr) -> decode -> D2H(hard) on
+ * hip_stream (NULL: the null stream) and return -- the reference's "W streams
+ * x F frames in flight" model (paper/ldpcGpuTegra.tex:279-289;
+ * CGPU_Decoder_MS_SIMD::decode_stream, code/gpu_fixed/decoder_ms/
+ * CGPU_Decoder_MS_SIMD.cu:219-275, without its blocking copies).  llr / hard
+ * should be page-locked (ldpc_host_alloc): pageable buffers make the copies
+ * synchronous.  The context's device staging and scratch are reused by its
+ * next call, so the calls on one context must use one stream; two contexts
+ * keep two batches in flight (H2D of batch k+1 and D2H of batch k-1 under the
+ * decode of batch k).  ldpc_ctx_synchronize waits for the context's last
+ * host_async call; hard is valid after it. */
+int ldpc_decode_i8_host_async(ldpc_ctx *ctx, void *hip_stream, const int8_t *llr, uint8_t *hard, int batch,
+                              int n_iter, const ldpc_params *p);
+int ldpc_decode_f32_host_async(ldpc_ctx *ctx, void *hip_stream, const float *llr, uint8_t *hard, int batch,
+                               int n_iter, const ldpc_params *p);
+int ldpc_ctx_synchronize(ldpc_ctx *ctx);
+
 /* Page-locked host memory for the host-buffer API, replacing the
  * reference's CUDA_MALLOC_HOST (code/gpu_fixed/custom_api/custom_cuda.cu:33). */
 int ldpc_host_alloc(void **ptr, size_t bytes);

@@ -80,6 +80,9 @@ SIGNATURES = {
     "ldpc_count_errors_async": (I, [P, P, P, I, I, P, P]),
     "ldpc_quantize_f32_i8_async": (I, [P, P, P, P, C.c_long, I, I, I]),
     "ldpc_quantize_f32_i8": (I, [P, P, P, C.c_long, I, I, I]),
+    "ldpc_decode_i8_host_async": (I, [P, P, P, P, I, I, C.POINTER(ldpc_params)]),
+    "ldpc_decode_f32_host_async": (I, [P, P, P, P, I, I, C.POINTER(ldpc_params)]),
+    "ldpc_ctx_synchronize": (I, [P]),
     "ldpc_host_alloc": (I, [C.POINTER(P), C.c_size_t]),
     "ldpc_host_free": (None, [P]),
 }
@@ -104,9 +107,13 @@ def lib():
             raise ImportError("libldpc_mi355x.so not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
                               " (expected at %s)" % LIB_PATH)
         L = C.CDLL(LIB_PATH)
+        missing = [name for name in SIGNATURES if not hasattr(L, name)]
+        if missing and os.environ.get("LDPC_AB_OLD_LIB") != "1":
+            raise ImportError("%s lacks entry points of include/ldpc_mi355x.h (stale build?): %s"
+                              % (LIB_PATH, ", ".join(missing)))
         for name, (res, args) in SIGNATURES.items():
-            if os.environ.get("LDPC_MI355X_LIB") and not hasattr(L, name):
-                continue   # an older experiment build (tools/ab.sh): its missing entry points stay unbound
+            if name in missing:
+                continue   # LDPC_AB_OLD_LIB=1 (tools/ab.sh's older experiment builds): left unbound
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

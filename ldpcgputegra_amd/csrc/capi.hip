@@ -77,6 +77,9 @@ struct ldpc_ctx {
     // host-buffer API pipeline (decode_host): chunk i of a batch runs on lane
     // i % lanes.size(): its own stream, scratch and input / output staging
     std::vector<Lane> lanes;
+    // asynchronous host-buffer API: the stream of the last call (ldpc_ctx_synchronize)
+    hipStream_t host_stream = nullptr;
+    bool host_pending = false;
     // kernel timing (ldpc_ctx_profile)
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -159,6 +162,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->host_pending) (void)hipStreamSynchronize(c->host_stream);
     windowed_code_free(&c->wcode);
     windowed2_free(&c->w16);
     coop_free(&c->coop);
@@ -566,11 +570,19 @@ static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, i
     // the 8 workgroups that share a V line on one XCD only when a grid splits
     // evenly into 8 x 8 of them; a chunk with the groups split across XCDs
     // runs ~20 % slower, measured r03h with a 2:1 split of 4096 codewords:
-    // 60.2 vs 55.7 ms per call), else 128 (the remap's grid % 8)
+    // 60.2 vs 55.7 ms per call), else 128 (the remap's grid % 8).  The 1024
+    // unit is used only while the chunks stay even (the last one at least half
+    // of the others): 2049 codewords as 2048 + 1 would leave the big chunk's
+    // decode and copy with nothing to overlap
     std::vector<int> b0s(1, 0);
     {
-        const int unit = batch >= nc_want * 1024 ? 1024 : 128;
-        const int cs0 = ((batch + nc_want - 1) / nc_want + unit - 1) / unit * unit;
+        auto size_for = [&](int unit) { return ((batch + nc_want - 1) / nc_want + unit - 1) / unit * unit; };
+        auto even = [&](int cs) {
+            const int full = std::min(nc_want, (batch + cs - 1) / cs);
+            return full <= 1 || 2 * (batch - (full - 1) * cs) >= cs;
+        };
+        int cs0 = size_for(128);
+        if (batch >= nc_want * 1024 && even(size_for(1024))) cs0 = size_for(1024);
         for (int i = 1; i < nc_want && i * cs0 < batch; i++) b0s.push_back(i * cs0);
         b0s.push_back(batch);
     }
@@ -627,6 +639,60 @@ static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, i
             return finish(ldpc_set_error(LDPC_EDEVICE, "host path D2H: %s", hipGetErrorString(hipGetLastError())));
     }
     return finish(LDPC_OK);
+}
+
+// The asynchronous host-buffer path: one batch, H2D -> decode -> D2H queued on
+// the caller's stream through the context's own staging (c->d_io) and scratch
+// (c->sc), nothing waited for.  Two contexts on two streams keep two batches in
+// flight: the copies of one overlap the decode of the other (the reference's
+// W streams x F frames, paper/ldpcGpuTegra.tex:279-289).
+static int decode_host_async(ldpc_ctx *c, void *sv, const void *llr, uint8_t *hard, int batch, int n_iter,
+                             const ldpc_params *p, bool is_float)
+{
+    if (!c || ((!llr || !hard) && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr/hard");
+    int rc = check_params(c, batch, n_iter, p, is_float);
+    if (rc != LDPC_OK || batch == 0) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    const hipStream_t s = (hipStream_t)sv;
+    const size_t n = (size_t)c->code->n, esz = is_float ? 4 : 1;
+    const size_t in_al = ((size_t)batch * n * esz + 255) / 256 * 256;
+    // size the staging and the scratch before anything is queued (a hipFree of
+    // a buffer the previous call still uses would wait for the device anyway)
+    if ((rc = ensure(&c->d_io, &c->io_bytes, in_al + (size_t)batch * n)) != LDPC_OK) return rc;
+    if ((rc = decode_device(c, c->sc, s, c->d_io, nullptr, nullptr, nullptr, batch, n_iter, p, is_float, true)) !=
+        LDPC_OK)
+        return rc;
+    char *d_in = (char *)c->d_io, *d_out = d_in + in_al;
+    HIP_TRY(hipMemcpyAsync(d_in, llr, (size_t)batch * n * esz, hipMemcpyHostToDevice, s));
+    if ((rc = decode_device(c, c->sc, s, d_in, (uint8_t *)d_out, nullptr, nullptr, batch, n_iter, p, is_float)) !=
+        LDPC_OK)
+        return rc;
+    HIP_TRY(hipMemcpyAsync(hard, d_out, (size_t)batch * n, hipMemcpyDeviceToHost, s));
+    c->host_stream = s;
+    c->host_pending = true;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_decode_i8_host_async(ldpc_ctx *c, void *s, const int8_t *llr, uint8_t *hard, int batch,
+                                         int n_iter, const ldpc_params *p)
+{
+    return decode_host_async(c, s, llr, hard, batch, n_iter, p, false);
+}
+
+extern "C" int ldpc_decode_f32_host_async(ldpc_ctx *c, void *s, const float *llr, uint8_t *hard, int batch,
+                                          int n_iter, const ldpc_params *p)
+{
+    return decode_host_async(c, s, llr, hard, batch, n_iter, p, true);
+}
+
+extern "C" int ldpc_ctx_synchronize(ldpc_ctx *c)
+{
+    if (!c) return ldpc_set_error(LDPC_EINVAL, "NULL ctx");
+    if (!c->host_pending) return LDPC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    c->host_pending = false;
+    HIP_TRY(hipStreamSynchronize(c->host_stream));
+    return LDPC_OK;
 }
 
 extern "C" int ldpc_host_alloc(void **p, size_t bytes)

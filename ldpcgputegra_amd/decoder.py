@@ -119,6 +119,22 @@ class Decoder:
         _lib.check(_lib.lib().ldpc_decode_f32(self._ctx, llr.ctypes.data, hard.ctypes.data, B, n_iter, C.byref(p)))
         return hard
 
+    # -- host buffers, asynchronous (H2D -> decode -> D2H queued on `stream`)
+    def decode_i8_host_async(self, llr, hard, n_iter, params=None, stream=None):
+        """Queue the decode of host (preferably pinned_empty) arrays llr -> hard
+        and return; hard is valid after synchronize().  One stream per context:
+        use two contexts to keep two batches in flight."""
+        assert llr.dtype == np.int8 and llr.flags.c_contiguous and hard.flags.c_contiguous
+        B = llr.shape[0]
+        assert llr.size == B * self.code.n and hard.size == B * self.code.n and hard.dtype == np.uint8
+        p = params or _lib.default_params()
+        self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_decode_i8_host_async(
+            self._ctx, s, llr.ctypes.data, hard.ctypes.data, B, n_iter, C.byref(p))), self.device)
+
+    def synchronize(self):
+        """Wait for this context's last decode_i8_host_async."""
+        _lib.check(_lib.lib().ldpc_ctx_synchronize(self._ctx))
+
     # -- device tensors (asynchronous on `stream`, default: torch current stream)
     @staticmethod
     def _ptr(t):

@@ -5,16 +5,18 @@ star: "BER curve identical to code/x86").
 The LLRs come from the device AWGN generator (all-zero codeword, BPSK,
 ``q = clamp(trunc(8 y), +-31)`` as code/x86/CFixPointConversion/
 CFastFixConversion.cpp:55-65), are copied to the host and decoded twice:
-on the GPU through the C-ABI (default kernel selection: coop2 for DVB-S2
+on the GPU through the C-ABI (default kernel selection: coop3 for DVB-S2
 r1/2) and by the reference's own CDecoder_OMS_fixed_SSE (oracle/_ref, built
 from the unmodified sources; 16-frame decode() calls as code/x86/main_p.cpp:485),
 or by the oracle's C restatement when _ref was not built.  Errors are
 counted over the K_info systematic positions as
 code/x86/CErrorAnalyzer/CErrorAnalyzer.cpp:123-154.
 
-The per-point frame count is LDPC_BER_FRAMES (default 256); with
-LDPC_BER_CURVE_OUT set, the curve is written there as JSON (the committed
-artefact profiles/r01d_ber_curve.json came from that).
+The per-point frame count is LDPC_BER_FRAMES (default 256), the Eb/N0 points
+LDPC_BER_EBN0 (comma-separated dB; default 0.7 .. 1.2 plus SURVEY.md §8(d)
+Config 3's 1.5); with LDPC_BER_CURVE_OUT set, the curve is written there as
+JSON (the committed artefacts profiles/r04_ber_curve.json, and r01d's before
+it, came from that).
 """
 import json
 import os
@@ -27,7 +29,7 @@ from ldpcgputegra_amd import Code, Decoder, channel
 
 pytestmark = pytest.mark.gpu
 
-EBN0 = (0.7, 0.8, 0.9, 1.0, 1.1, 1.2)
+EBN0 = tuple(float(x) for x in os.environ.get("LDPC_BER_EBN0", "0.7,0.8,0.9,1.0,1.1,1.2,1.5").split(","))
 
 
 def test_dvbs2_ber_curve_identical_to_reference():

@@ -524,6 +524,45 @@ def test_host_path_chunked_vs_device():
     assert np.array_equal(fd.decode_f32(y, 20), hf.cpu().numpy())
 
 
+def test_host_async_two_contexts_ping_pong():
+    """ldpc_decode_i8_host_async: two contexts on two streams keep two host
+    batches in flight (the reference's streams x frames model,
+    paper/ldpcGpuTegra.tex:279-289); six batches of alternating inputs (pinned
+    and pageable, a ragged 1000-codeword batch) give exactly the device API's
+    hard decisions, and ldpc_ctx_synchronize is a no-op with nothing queued."""
+    torch = _torch()
+    from ldpcgputegra_amd import pinned_empty
+    t = load_table("dvbs2_r1_2")
+    B = 1024
+    table = channel.i8_table(channel.sigma_from_ebn0(1.0, 0.5))
+    decs = [Decoder(Code("dvbs2_r1_2"), max_batch=B) for _ in range(2)]
+    decs[0].synchronize()
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    ins = [pinned_empty((B, t.n), np.int8), np.empty((B, t.n), np.int8)]
+    outs = [pinned_empty((B, t.n), np.uint8), np.empty((B, t.n), np.uint8)]
+    exp = []
+    for i in range(2):
+        ins[i][:] = channel.awgn_i8_host(t.n, B, 79, table, first_cw=i * B)
+        d_h = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+        decoder("dvbs2_r1_2", 0, B).decode_i8_device(torch.from_numpy(ins[i]).cuda(), d_h, 30)
+        torch.cuda.synchronize()
+        exp.append(d_h.cpu().numpy())
+    for k in range(6):
+        j = k % 2
+        if k >= 2:
+            decs[j].synchronize()
+            assert np.array_equal(outs[j][:nb[j]], exp[j][:nb[j]]), k
+        nb = nb if k else [B, B]
+        nb[j] = 1000 if k == 4 else B
+        outs[j][:] = 2
+        decs[j].decode_i8_host_async(ins[j][:nb[j]], outs[j][:nb[j]], 30, stream=streams[j].cuda_stream)
+    for j in range(2):
+        decs[j].synchronize()
+        assert np.array_equal(outs[j][:nb[j]], exp[j][:nb[j]]), j
+        assert decs[j].last_kernel == "coop3"
+        decs[j].close()
+
+
 def test_context_per_device_and_bad_device():
     """One context per device id (the multi-GPU layout): every
     visible device decodes the same codewords bit-identically; a device id

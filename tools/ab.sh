@@ -13,7 +13,7 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
     for v in ${VARIANTS:-cur}; do
         i=$((i + 1))
         if [ "$v" = cur ]; then lib=""; else lib="$v"; fi
-        LDPC_MI355X_LIB="$lib" timeout -k 10 240 env $AB_ENV python3 bench.py $ARGS > "$OUT/run$i.log" 2>&1
+        LDPC_MI355X_LIB="$lib" LDPC_AB_OLD_LIB=1 timeout -k 10 240 env $AB_ENV python3 bench.py $ARGS > "$OUT/run$i.log" 2>&1
         rc=$?
         if [ $rc -ne 0 ]; then
             echo "$v rc=$rc"
