@@ -110,8 +110,7 @@ struct Cfg {
     static constexpr int KAHEAD = R + 2 + DPER;        // tables staged KAHEAD windows ahead of the chain
     static constexpr int NI = R + 1;                   // LDS-DMA input windows in flight per slab wave
     static constexpr int NS = R + 1 < 3 ? 3 : R + 1;   // window states in VGPRs (pre at p-1, post at p+1)
-    static constexpr int U = NS;                       // periods unrolled (multiple of NI, NS and 3: line loads
-                                                       // are written to their slots two periods later)
+    static constexpr int U = NS;                       // periods unrolled (multiple of NI and NS)
     static constexpr int NR = 2;                       // staged-output windows: window g's parity V is staged in
                                                        // period g+1 and read for its stores at that period's end
     static constexpr int CHW = WS >= 3 ? 3 : WS;       // the chain wave (waves go to SIMDs 0,2,1,3,0,2,1: wave 3
@@ -299,7 +298,7 @@ struct Slab3 {
         if (lane < 40) dma16(gbase + (size_t)idx * gmul, base);
     }
     // line cache: writeback of period p (slot -> VGPRs, then HBM), load of
-    // period p (HBM -> VGPRs), slot write of the load of period p-2
+    // period p (HBM -> VGPRs), slot write of the load of period p-LC_PUT
     LDPC_DEV uint4 wb_read(uint2 lop) const { return *(const uint4 *)(lcb() + (lop.y >> 16) * 128u + lq); }
     LDPC_DEV void wb_store(uint2 lop, const uint4 &d) const { *(uint4 *)(Vg + (size_t)(lop.x >> 16) * 128 + lq) = d; }
     LDPC_DEV uint4 line_load(uint2 lop) const { return *(const uint4 *)(Vg + (size_t)(lop.x & 0xFFFFu) * 128 + lq); }
@@ -825,16 +824,13 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         // ------------------------------------------------------------ memory wave
         // Every vector-memory operation of the workgroup, per period p for each
         // slab wave's set of 8 slots (w = 0..WS-1), in this order: the slot
-        // writes of the lines loaded in period p-2; the LDS-DMA gathers of
+        // writes of the lines loaded in period p-LC_PUT; the LDS-DMA gathers of
         // window p+1+R (messages + o-edge parity rows); the line loads of period
         // p (8 lines per set); the line writebacks of period p (slot -> VGPRs ->
         // HBM); the stores of window p-2 (messages + x-edge parity rows).  Then
-        // vmcnt(36): everything up to this period's predecessor's loads has
-        // landed -- the gathers for the pre of window p+2 (next period) and the
-        // lines written to their slots next period -- and a writeback completes
-        // two periods after its issue, before its line can be loaded again
-        // (linecache.cpp: >= 3).  Unused ops go to the sink row / line / slot,
-        // so the counts are static.
+        // vmcnt(42) (see mperiod).  Unused ops go to the sink row / line / slot,
+        // so the counts are static; tools/check_vmcnt.py checks the emitted ISA
+        // against them at build time.
         char *lcb = (char *)&sm.lc[0][0];
         const uint32_t lq = 16u * (uint32_t)q;
         // every access of the group's block (coop3_group_layout: V rows, then
@@ -894,12 +890,16 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 lop[w] = *(const uint2 *)&sm.tab[0][8 * w + kl][W_LOP];
             }
             // period p: gathers of window p+1+R, line loads of period p, line
-            // writebacks of period p, stores of window p-2 (24 ops); vmcnt(42)
-            // at its end completes everything up to the gathers of period p-1
-            // (the pre of window p+2 reads them next period) and the line loads
-            // of period p-2 (their slot writes are next period's), and a
-            // writeback two periods after its issue (its line is loaded again
-            // >= 3 periods later, linecache.cpp)
+            // writebacks of period p, stores of window p-2 (4 WS = 24 ops);
+            // vmcnt(42) = 24 + 3 WS at its end completes everything up to the
+            // gathers of period p-1 (the pre of window p+2 reads them next
+            // period), hence the line loads of period p-2 and earlier (the
+            // slot writes of period p+1 take those of period p+1-LC_PUT), and
+            // a writeback two periods after its issue (its line is loaded
+            // again >= 3 periods later, linecache.cpp).  The count holds only
+            // while the compiler emits exactly these 24 vector-memory
+            // instructions per period: tools/check_vmcnt.py (run by
+            // __graft_entry__.build) checks the ISA
             auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
                 constexpr int s = decltype(sc_)::value;   // p % NPD
                 if (STAMP) tx = stampL();

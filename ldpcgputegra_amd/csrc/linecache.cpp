@@ -26,7 +26,7 @@
 //   * at most LC_OPS loads and LC_OPS writebacks per period (6 slab waves x 8
 //     lane groups: one 64-lane global load and one 64-lane global store per
 //     wave and period, unused lane groups on the sink line / sink slot);
-//   * no load in the last two periods of an iteration, so that a segment start
+//   * no load in the last LC_PUT periods of an iteration, so that a segment start
 //     has no load in flight: the lines resident at a segment start are filled
 //     by its prologue (LcPlan::pro) and the dirty ones left at its end are
 //     written back by its epilogue (LcPlan::epi);
@@ -155,7 +155,7 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
         while (btl + 0 <= A.tl) btl += nw;   // B's load after A's (unrolled)
         return btl >= A.tw + 3;
     };
-    // constraints: no load in the last two periods of an iteration; at most
+    // constraints: no load in the last LC_PUT periods of an iteration; at most
     // LC_OPS loads / writebacks per period (moving loads earlier, writebacks later)
     for (int round = 0;; round++) {
         if (round == 256) return lc_fail(__LINE__);
@@ -348,10 +348,16 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     return lc_check_plan(o, tab, recw, nw, S, D0, n, k, 3);
 }
 
-// Replays `iters` iterations of the plan period by period, in the kernel's
-// order (coop3_decode): every pre read / post write finds its line in the slot
-// the record names, a slot is only refilled once its dirty line was written
-// back, a writeback is never in a period that also accesses the line, a line
+// Replays `iters` iterations of the plan period by period, as the kernel runs
+// a period (coop3_decode): the memory wave's slot writes (lines loaded LC_PUT
+// periods earlier), then its writebacks (slot -> VGPRs -> HBM) and loads, all
+// CONCURRENT with the slab waves' post of window p-1 and pre of window p+1 --
+// only the period's closing barrier orders them.  So within one period a slot
+// written must hold no line the post / pre touch, its new line must not be
+// accessed before the next period, a slot is never both written and written
+// back, and a writeback's line is not accessed.  Beyond that: every pre read /
+// post write finds its line in the slot the record names, a slot is only
+// refilled once its dirty line was written back in an earlier period, a line
 // is loaded >= 3 periods after its last store and never while a dirty copy is
 // resident, and the dirty lines left at the end are exactly the epilogue's.
 int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int n, int k,
@@ -374,6 +380,7 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
         line_of[s] = L;
     }
     auto rec_at = [&](int u, int kk) { return &tab[((size_t)u * S + kk) * recw]; };
+    std::vector<long> put_at(NSL, -1000000);   // period of the slot's last write by the memory wave
     auto access = [&](int u, bool wr, long P) -> int {   // window u's info entries
         u = cmod(u, nw);
         for (int kk = 0; kk < S; kk++) {
@@ -384,6 +391,9 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
                 const int s = (int)(off / 128);
                 if (off % 128 != (r[j] % 8) * 16 || s <= 0 || s >= NSL || line_of[s] != (int)(r[j] / 8))
                     return fail(wr ? "post finds another line" : "pre finds another line", P, s, (int)r[j]);
+                if (put_at[s] == P)
+                    return fail(wr ? "post of a line written to its slot this period"
+                                   : "pre of a line written to its slot this period", P, s, (int)r[j]);
                 if (wr && !dirty[s]) {
                     dirty[s] = 1;
                     dirty_copies[r[j] / 8]++;
@@ -410,7 +420,42 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
         };
         if (P >= 1) touch(p - 1);
         if (P + 1 < G) touch(p + 1);
-        // writebacks
+        // LDS slots the post / pre of this period read or write
+        std::vector<char> used_slot(NSL, 0);
+        auto use = [&](int u) {
+            u = cmod(u, nw);
+            for (int kk = 0; kk < S; kk++)
+                if (rec_at(u, kk)[D0] & COOP_M_ACT)
+                    for (int j = 0; j < X; j++) {
+                        const uint32_t s = o.piece[((size_t)u * S + kk) * X + j] / 128;
+                        if (s < (uint32_t)NSL) used_slot[s] = 1;
+                    }
+        };
+        if (P >= 1) use(p - 1);
+        if (P + 1 < G) use(p + 1);
+        std::vector<char> wb_slot(NSL, 0);
+        for (int i = 0; i < LC_OPS; i++)
+            if ((ops[2 * i] >> 16) != sink_line) {
+                const int s = (int)(ops[2 * i + 1] >> 16);
+                if (s > 0 && s < NSL) wb_slot[s] = 1;
+            }
+        // slot writes of the loads of period P - LC_PUT (first in the memory wave's period)
+        for (int i = 0; i < LC_OPS; i++) {
+            const int s = (int)(ops[2 * i + 1] & 0xFFFFu);
+            const uint32_t L = pend[(size_t)((P + 1) % NPD) * LC_OPS + i];   // the load of period P - LC_PUT
+            if (s == 0) {
+                if (L != sink_line && P >= LC_PUT) return fail("load without a slot", P, s, (int)L);
+                continue;
+            }
+            if (L == sink_line) return fail("slot write without a load", P, s, (int)L);
+            if (s >= NSL || dirty[s]) return fail("slot refilled before its writeback", P, s, line_of[s]);
+            if (put_at[s] == P) return fail("slot written twice in one period", P, s, (int)L);
+            if (wb_slot[s]) return fail("slot written and written back in one period", P, s, (int)L);
+            if (used_slot[s]) return fail("slot refilled in a period whose post / pre access it", P, s, line_of[s]);
+            line_of[s] = (int)L;
+            put_at[s] = P;
+        }
+        // writebacks (concurrent with the post / pre below)
         for (int i = 0; i < LC_OPS; i++) {
             const uint32_t L = ops[2 * i] >> 16;
             const int s = (int)(ops[2 * i + 1] >> 16);
@@ -422,21 +467,8 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
             dirty[s] = 0;
             last_store[L] = P;
         }
-        // post of window p-1
+        // post of window p-1, pre of window p+1
         if (P >= 1 && access(p - 1, true, P)) return -1;
-        // slot writes of the loads of period P-2
-        for (int i = 0; i < LC_OPS; i++) {
-            const int s = (int)(ops[2 * i + 1] & 0xFFFFu);
-            const uint32_t L = pend[(size_t)((P + 1) % NPD) * LC_OPS + i];   // the load of period P - LC_PUT
-            if (s == 0) {
-                if (L != sink_line && P >= LC_PUT) return fail("load without a slot", P, s, (int)L);
-                continue;
-            }
-            if (L == sink_line) return fail("slot write without a load", P, s, (int)L);
-            if (s >= NSL || dirty[s]) return fail("slot refilled before its writeback", P, s, line_of[s]);
-            line_of[s] = (int)L;
-        }
-        // pre of window p+1
         if (P + 1 < G && access(p + 1, false, P)) return -1;
         // loads
         for (int i = 0; i < LC_OPS; i++) {
