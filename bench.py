@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--iters", type=int, default=None, help="default 50 (i8) / 20 (f32)")
     ap.add_argument("--ebn0", type=float, default=1.0, help="Eb/N0 (dB) of the synthetic channel")
     ap.add_argument("--kernel", type=int, default=0,
-                    help="0 auto, 1 generic, 2 windowed, 3 windowed2 S=16, 5 coop, 7 lds, 8 coop3")
+                    help="0 auto, 1 generic, 2 windowed, 3 windowed2 S=16, 5 coop, 7 lds, 8 coop3, 9 ldsep (float)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (cgroup quota / affinity)")
@@ -496,7 +496,7 @@ def main():
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": alg_bytes,
             },
         }
-        if dec.last_kernel == "lds":
+        if dec.last_kernel in ("lds", "ldsep"):
             # the LDS-resident kernel keeps V and the messages in LDS: HBM sees
             # only LLRs in / hard decisions out (the measured traffic), so the
             # algorithmic bytes are LDS bytes, priced against the LDS array's
@@ -509,8 +509,11 @@ def main():
                 "frac": round(achieved / lds_peak, 4), "traffic": traffic,
                 "hbm_achieved": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic else None,
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": alg_bytes,
-                "note": "algorithmic bytes are LDS traffic (V and messages never leave LDS); bound in practice: "
-                        "dependent LDS round trips per layer at one wave per SIMD (latency, not bandwidth)",
+                "note": ("algorithmic bytes are on-chip traffic (V in LDS, messages in VGPRs: neither leaves the CU); "
+                         "bound in practice: VALU issue at one wave per SIMD (DPP butterflies per check, DESIGN.md)"
+                         if dec.last_kernel == "ldsep" else
+                         "algorithmic bytes are LDS traffic (V and messages never leave LDS); bound in practice: "
+                         "dependent LDS round trips per layer at one wave per SIMD (latency, not bandwidth)"),
             }
         if world == 1 and a.cpu_seconds > 0:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -57,7 +57,8 @@ struct ldpc_ctx {
     int device = 0;
     int max_batch = 0;
     int max_stride = 0;
-    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3 windowed2 (S16), 5 coop, 7 lds, 8 coop3
+    int kernel = 0;                 // 0 auto, 1 generic, 2 windowed, 3 windowed2 (S16), 5 coop, 7 lds, 8 coop3,
+                                    // 9 ldsep (edge-parallel float)
                                     // (4 and 6, windowed2 S32 and coop2, were superseded and removed)
     int last_kernel = 0;
     int last_skipped = 0;   // the preferred kernel the last decode could not use at its batch size (0: none)
@@ -197,14 +198,15 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 
 bool ldpc_ctx_has_kernel(const ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 8) return false;
+    if (!c || k < 0 || k > 9) return false;
     return !((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || k == 4 ||
-             (k == 5 && !c->coop.valid) || k == 6 || (k == 7 && !c->lds.valid) || (k == 8 && !c->coop3.valid));
+             (k == 5 && !c->coop.valid) || k == 6 || (k == 7 && !c->lds.valid) || (k == 8 && !c->coop3.valid) ||
+             (k == 9 && !c->lds.ep_valid));
 }
 
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 8) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 8");
+    if (!c || k < 0 || k > 9) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 9");
     if (!ldpc_ctx_has_kernel(c, k)) return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
     c->kernel = k;
     return LDPC_OK;
@@ -303,7 +305,11 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
     c->last_skipped = 0;
     const bool ld = lds_applicable(c->code, c->lds, is_float);
     if (c->kernel == 7) return ld ? 7 : -1;
-    if (is_float) return (c->kernel == 0 && lds_preferred(c->code, c->lds, true)) ? 7 : (c->kernel <= 1 ? 1 : -1);
+    if (c->kernel == 9) return ldsep_applicable(c->code, c->lds, is_float) ? 9 : -1;
+    if (is_float) {
+        if (c->kernel == 0 && ldsep_applicable(c->code, c->lds, true)) return 9;
+        return (c->kernel == 0 && lds_preferred(c->code, c->lds, true)) ? 7 : (c->kernel <= 1 ? 1 : -1);
+    }
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
     const bool w2 = windowed2_params_ok(p);
     const bool co = c->coop.valid && coop_params_ok(p);
@@ -347,14 +353,14 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     if (kern < 0)
         return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d selected but not applicable to these params", c->kernel);
     c->last_kernel = kern;
-    if (kern == 7 && alloc_only) return LDPC_OK;
+    if ((kern == 7 || kern == 9) && alloc_only) return LDPC_OK;
     if (kern == 7 && nm_ld) {   // node-major input: transpose it to frame-major scratch first
         if ((rc = ensure(&sc.d_msg, &sc.msg_bytes, (size_t)h->n * batch)) != LDPC_OK) return rc;
         if (launch_deinterleave_i8((const int8_t *)d_llr, nullptr, (int8_t *)sc.d_msg, h->n, batch, (int)nm_ld, s))
             return ldpc_set_error(LDPC_EDEVICE, "node-major transpose: %s", hipGetErrorString(hipGetLastError()));
         d_llr = sc.d_msg;
     }
-    if (kern == 7) {   // LDS-resident: frame-major in and out, no scratch, no transposes
+    if (kern == 7 || kern == 9) {   // LDS-resident: frame-major in and out, no scratch, no transposes
         DecodeLaunch L{};
         L.batch = batch;
         L.iters = n_iter;
@@ -372,7 +378,9 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
             HIP_TRY(hipEventCreate(&ev1));
             HIP_TRY(hipEventRecord(ev0, s));
         }
-        const int lr = launch_lds(c->lds, h, d_llr, d_hard, d_soft, batch, n_iter, L, s);
+        const int lr = kern == 9 ? launch_ldsep(c->lds, h, (const float *)d_llr, d_hard, (float *)d_soft, batch,
+                                                n_iter, L, s)
+                                 : launch_lds(c->lds, h, d_llr, d_hard, d_soft, batch, n_iter, L, s);
         if (c->profile) {
             HIP_TRY(hipEventRecord(ev1, s));
             c->events.emplace_back(ev0, ev1);

@@ -405,13 +405,14 @@ int lds_upload(const ldpc_code *h, LdsCode *lc)
         return ldpc_set_error(LDPC_EDEVICE, "lds table upload");
     }
     lc->valid = 1;
-    return LDPC_OK;
+    return ldsep_upload(h, layers, lc);
 }
 
 void lds_free(LdsCode *lc)
 {
     (void)hipFree(lc->d_tab);
     (void)hipFree(lc->d_layers);
+    (void)hipFree(lc->d_ep_tab);
     *lc = LdsCode{};
 }
 

@@ -96,19 +96,47 @@ def old_msg(MA, tab, j):
     return perm(tab[1], tab[0], (sh & 0x03000300) | 0x040C000C)
 
 
-def new_msg(j, c, a, min1, k1, k2, P, MA):
+def abs_sat(r):                              # |x| of R(x) or of the saturated 0x8000, capped at R(127)
+    return pk_max(r, pk_sub_sat(C510, r))
+
+
+def signed_csts(k1, k2, sacc, D):
+    """eps * k1, eps * k2 (C form), eps = -1 where the sign parity of the
+    check's contributions (and the odd-degree flip) is odd."""
+    Pm = pk_sra15(sacc ^ (SIGNS if D & 1 else 0))
+    return pk_sub(k1 ^ Pm, Pm), pk_sub(k2 ^ Pm, Pm)
+
+
+def new_v(j, c, a, min1, e1, e2, MA):
+    """pk16.h new_v: V' = sign(c) * min(|c| + eps * cst, 127) -- the reference's
+    max(sat(c + m), -127) with m = (c < 0) ^ par ? -cst : cst -- and edge j's
+    code (bit 0: c < 0, bit 1: got cst2) into MA."""
     neq = pk_sra15(pk_sub(min1, a))
-    rr = bfi(neq, k2, k1)
-    sgn = pk_sra15(c ^ P)
-    MA = MA | (sgn & (0x00010001 << (2 * j))) | (neq & (0x00020002 << (2 * j)))
-    return pk_max(pk_add_sat(c, pk_sub(rr ^ sgn, sgn)), RNEG127), MA
+    T = pk_add_sat(a, bfi(neq, e2, e1))
+    sc = pk_sra15(c)
+    MA = MA | (sc & (0x00010001 << (2 * j))) | (neq & (0x00020002 << (2 * j)))
+    return bfi(sc, pk_sub(C510, T), T), MA
+
+
+def new_v_later(j, c, a, min1, e1, e2, MA):
+    """The later degree group (a = |min(c, msg_max)| is not |c|): c clamped at
+    -127 first, V' = max(sat(c + m), -127), same code / MB encoding."""
+    neq = pk_sra15(pk_sub(min1, a))
+    sc = pk_sra15(c)
+    m = bfi(neq, e2, e1)
+    MA = MA | (sc & (0x00010001 << (2 * j))) | (neq & (0x00020002 << (2 * j)))
+    return pk_max(pk_add_sat(c, pk_sub(m ^ sc, sc)), RNEG127), MA
 
 
 def kernel_check(vraw, MA, MB, off, mm, later):
     """One check for a vector of codeword pairs: vraw[j] = u16 V pair of edge
     j.  Returns (new V u16 pairs, MA, MB).  The kernel splits a first-group
     check into pre / chain / post; the chain only supplies the x edge's V, so
-    the per-edge algebra is the same for every edge."""
+    the per-edge algebra is the same for every edge.  The first group works on
+    the unclamped contributions (only their sign and saturated magnitude are
+    used); MB holds eps * cst1, eps * cst2 (signed bytes) and MA bit 0 of an
+    edge the sign of its contribution, so that the old message decodes as
+    (-1)^sign * eps * cst through the same byte table."""
     D = len(vraw)
     rmm, coff = (mm * 256 + 255) * 0x10001, off * 256 * 0x10001
     tab = msg_tab(MB)
@@ -117,24 +145,28 @@ def kernel_check(vraw, MA, MB, off, mm, later):
     min2 = min1.copy()
     sacc = np.zeros(MA.shape, np.int64)
     for j in range(D):
-        cj = pk_max(pk_sub_sat(unpack_v(vraw[j]), old_msg(MA, tab, j)), RNEG127)
-        aj = abs_r(pk_min(cj, rmm)) if later else pk_min(abs_r(cj), rmm)
+        cj = pk_sub_sat(unpack_v(vraw[j]), old_msg(MA, tab, j))
+        if later:
+            cj = pk_max(cj, RNEG127)
+            aj = abs_r(pk_min(cj, rmm))
+        else:   # |c| unclipped (coop3: msg_max clips min1 / min2 instead, the same edges win)
+            aj = abs_sat(cj)
         c.append(cj)
         a.append(aj)
         sacc = sacc ^ cj
         min2, min1 = pk_max(min1, pk_min(aj, min2)), pk_min(min1, aj)
-    k1 = pk_max(pk_sub(min2, coff), R0)
-    k2 = pk_max(pk_sub(min1, coff), R0)
     if later:
-        k1, k2 = pk_min(k1, rmm), pk_min(k2, rmm)
+        k1, k2 = pk_min(pk_max(pk_sub(min2, coff), R0), rmm), pk_min(pk_max(pk_sub(min1, coff), R0), rmm)
+    else:
+        k1, k2 = pk_max(pk_sub(pk_min(min2, rmm), coff), R0), pk_max(pk_sub(pk_min(min1, rmm), coff), R0)
     k1, k2 = k1 & HIBYTES, k2 & HIBYTES
-    P = (sacc ^ (SIGNS if D & 1 else 0)) & SIGNS
+    e1, e2 = signed_csts(k1, k2, sacc, D)
     MAn = np.zeros(MA.shape, np.int64)
     vnew = []
     for j in range(D):
-        vn, MAn = new_msg(j, c[j], a[j], min1, k1, k2, P, MAn)
+        vn, MAn = (new_v_later if later else new_v)(j, c[j], a[j], min1, e1, e2, MAn)
         vnew.append(pack_v(vn))
-    return vnew, MAn, perm(k2, k1, 0x07030501)
+    return vnew, MAn, perm(e2, e1, 0x07030501)
 
 
 # ---- reference and pair helpers --------------------------------------------

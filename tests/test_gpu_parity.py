@@ -14,7 +14,7 @@ import pytest
 from conftest import golden_cases, golden_inputs
 
 import oracle as O
-from ldpcgputegra_amd import ALGO_MS, ALGO_NMS, ALGO_OMS, Code, Decoder, channel, default_params, load_table
+from ldpcgputegra_amd import ALGO_MS, ALGO_NMS, ALGO_OMS, Code, Decoder, LdpcError, channel, default_params, load_table
 
 pytestmark = pytest.mark.gpu
 FLOAT_TOL = 1e-6
@@ -134,7 +134,7 @@ def test_config1_single_codeword_float_sweep():
         sigma = channel.sigma_from_ebn0(ebn0, t.k_info / t.n)
         llr = (-1.0 + sigma * rng.standard_normal((1, t.n))).astype(np.float32)
         ref_hard, ref_soft, _ = O.decode_f32(t, llr, 10, O.OMS, 0.0)
-        for k in (0, 1, 7):
+        for k in (0, 1, 7, 9):
             dec = decoder("648x324", k, 64)
             d_hard = torch.empty((1, t.n), dtype=torch.uint8, device="cuda")
             d_soft = torch.empty((1, t.n), dtype=torch.float32, device="cuda")
@@ -209,9 +209,18 @@ def test_early_termination_vs_oracle(code):
         assert np.array_equal(d_soft.cpu().numpy(), ref_soft), "kernel %d" % k
 
 
+def has_kernel(code, k):
+    try:
+        decoder(code, k, 64)
+        return True
+    except LdpcError:
+        return False
+
+
 @pytest.mark.parametrize("code,algo,beta,batch", [("1944x972", ALGO_MS, 0.0, 33), ("576x288", ALGO_OMS, 0.15, 33),
                                                   ("576x288", ALGO_NMS, 0.75, 33), ("dvbs2_r1_2", ALGO_MS, 0.0, 33),
-                                                  ("648x324", ALGO_MS, 0.0, 1024)])
+                                                  ("648x324", ALGO_MS, 0.0, 1024), ("648x324", ALGO_OMS, 0.15, 37),
+                                                  ("648x324", ALGO_NMS, 0.75, 37), ("576x288", ALGO_MS, 0.0, 1030)])
 def test_float_decoder_vs_oracle(code, algo, beta, batch):
     """648x324 at batch 1024 / 20 it / float min-sum is BASELINE.json configs[1]."""
     torch = _torch()
@@ -222,7 +231,9 @@ def test_float_decoder_vs_oracle(code, algo, beta, batch):
     iters = 5 if t.n > 10000 else 20
     o_algo = O.NMS if algo == ALGO_NMS else O.OMS
     ref_hard, ref_soft, _ = O.decode_f32(t, llr, iters, o_algo, beta)
-    ks = [1] + ([7] if Code(code).layer_info()["lds_f32"] else [])
+    ks = [1] + ([7] if Code(code).layer_info()["lds_f32"] else []) + ([9] if has_kernel(code, 9) else [])
+    if code in ("648x324", "576x288"):
+        assert 9 in ks                                       # the edge-parallel kernel covers both shapes
     for k in ks:
         dec = decoder(code, k, max(64, batch))
         d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
@@ -233,6 +244,31 @@ def test_float_decoder_vs_oracle(code, algo, beta, batch):
         soft = d_soft.cpu().numpy()
         assert np.max(np.abs(soft - ref_soft)) <= FLOAT_TOL, "kernel %d" % k
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard), "kernel %d" % k
+
+
+@pytest.mark.parametrize("code,batch", [("648x324", 1024), ("576x288", 37)])
+def test_ldsep_auto_early_termination_vs_oracle(code, batch):
+    """The float default for the short QC codes is the edge-parallel kernel
+    (9, ldsep.hip): with early termination its hard decisions, soft output and
+    iterations used equal the oracle's (syndrome after every iteration,
+    oracle/ldpc_oracle.c check_syndrome_ok_f)."""
+    torch = _torch()
+    t = load_table(code)
+    rng = np.random.default_rng(8)
+    llr = (-1.0 + channel.sigma_from_ebn0(2.0, 0.5) * rng.standard_normal((batch, t.n))).astype(np.float32)
+    ref_hard, ref_soft, ref_its = O.decode_f32(t, llr, 20, O.OMS, 0.0, early_term=True)
+    assert ref_its.min() < 20
+    dec = decoder(code, 0, batch)
+    d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+    d_soft = torch.empty((batch, t.n), dtype=torch.float32, device="cuda")
+    d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
+    dec.decode_f32_device(torch.from_numpy(llr).cuda(), d_hard, 20, params=default_params(algo=ALGO_MS, early_term=1),
+                          soft=d_soft, iters_used=d_its)
+    torch.cuda.synchronize()
+    assert dec.last_kernel == "ldsep"
+    assert np.array_equal(d_its.cpu().numpy(), ref_its)
+    assert np.max(np.abs(d_soft.cpu().numpy() - ref_soft)) <= FLOAT_TOL
+    assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
 
 
 def test_device_channel_matches_host_generator():
