@@ -177,7 +177,6 @@ LDPC_DEV uint32_t pk_add(uint32_t a, uint32_t b) { return us(sv(a) + sv(b)); }
 
 constexpr uint32_t V127 = 0x007F007Fu, VNEG127 = 0xFF81FF81u;   // +-127 per half (value form)
 
-LDPC_DEV uint32_t pk_mul_lo(uint32_t a, uint32_t b) { return us(__builtin_bit_cast(s16x2, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b))); }
 // NMS constant of a clipped minimum r (R form, value <= 63) for factor f <= 64
 // (value form per half): (v * f) >> 5 as a value / in C form (256 x)
 LDPC_DEV uint32_t nms_v(uint32_t r, uint32_t f) { return us(__builtin_bit_cast(s16x2, __builtin_bit_cast(u16x2, pk_mul_lo(pk_ashr8(r), f)) >> (unsigned short)5)); }
@@ -321,15 +320,25 @@ struct Slab3 {
             // first degree group (OMS_fixed_SSE.cpp:201-218); a = |c| here, the
             // msg_max clip is applied to min1 / min2 (a_j == min1 decides the
             // same edges either way, and min1 == msg_max implies cst1 == cst2)
+            // the info edges' contributions stay unclamped (the saturated
+            // 0x8000 below R(-128) included): the post uses only their sign
+            // and |c| (abs_sat caps it at R(127) as the reference's clamp does)
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t, K.m3, K.c4)), neg127);
-                const uint32_t aj = abs_r(c, c510);
+                const uint32_t c = pk_sub_sat(v[J], old_msg<J>(MA, t, K.m3, K.c4));
+                const uint32_t aj = abs_sat(c, c510);
                 s.c[J] = c;
                 s.a[J] = aj;
                 sacc ^= c;
-                min2 = pk_max(min1, pk_min(aj, min2));
-                min1 = pk_min(min1, aj);
+                if constexpr (J == 0) {   // a <= R(127): the first edge is min1
+                    min1 = aj;
+                } else if constexpr (J == 1) {
+                    min2 = pk_max(min1, aj);
+                    min1 = pk_min(min1, aj);
+                } else {
+                    min2 = pk_max(min1, pk_min(aj, min2));
+                    min1 = pk_min(min1, aj);
+                }
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
@@ -386,17 +395,17 @@ struct Slab3 {
                                     : pk_min(pk_max(pk_sub(min2, K.coff), K.r0), K.rmm) & HIBYTES;
             const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
                                     : pk_min(pk_max(pk_sub(min1, K.coff), K.r0), K.rmm) & HIBYTES;
-            const uint32_t P = (sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u)) & SIGNS;
-            uint32_t MAn = 0;
+            uint32_t e1, e2, MAn = 0;
+            signed_csts(k1, k2, sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u), e1, e2);
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                s.c[J] = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MAn, neg127);
+                s.c[J] = new_v_later<J>(s.c[J], s.a[J], min1, e1, e2, MAn, neg127);
                 if constexpr (FZ) s.c[J] = bfi(fm, v[J], s.c[J]);   // converged codewords keep their V
             });
             s.mx = 0;
             s.sacc = 0;
             s.mn1 = MAn;
-            s.mn2 = perm(k2, k1, 0x07030501u);
+            s.mn2 = perm(e2, e1, 0x07030501u);
             // the chain passes V[p_0] (the tail's last edge) on: A = B = c_o = L = H = y
             // (NMS: A = 32 y, B = 32 y + 31)
             const uint32_t Y = pk_ashr8(s.c[X]);
@@ -447,28 +456,29 @@ struct Slab3 {
         };
         uint32_t MA, MB;
         if constexpr (!TL) {
-            const uint32_t cx = pk_max(pk_sub_sat(xr, s.mx), K.neg127);
-            const uint32_t ax = abs_r(cx, K.c510);
+            const uint32_t cx = pk_sub_sat(xr, s.mx);   // unclamped, as the info edges' (new_v)
+            const uint32_t ax = abs_sat(cx, K.c510);
             const uint32_t sacc = s.sacc ^ cx;
             const uint32_t min2 = pk_max(s.mn1, pk_min(ax, s.mn2)), min1 = pk_min(ax, s.mn1);
             const uint32_t k1 = NMS ? nms_c(pk_min(min2, K.rmm), fk)
                                     : pk_max(pk_sub(pk_min(min2, K.rmm), K.coff), K.r0) & HIBYTES;
             const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
                                     : pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0) & HIBYTES;
-            const uint32_t P = (sacc ^ ((D0 & 1) ? SIGNS : 0u)) & SIGNS;
+            uint32_t e1, e2;
+            signed_csts(k1, k2, sacc ^ ((D0 & 1) ? SIGNS : 0u), e1, e2);
             MA = 0;
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t n = new_msg<J>(s.c[J], s.a[J], min1, k1, k2, P, MA, K.neg127);
+                const uint32_t n = new_v<J>(s.c[J], s.a[J], min1, e1, e2, MA, K.c510);
                 put(J, FZ ? perm(n, s.v[J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
-            const uint32_t nx = new_msg<X>(cx, ax, min1, k1, k2, P, MA, K.neg127);
+            const uint32_t nx = new_v<X>(cx, ax, min1, e1, e2, MA, K.c510);
             *sx = (unsigned short)(FZ ? perm(nx, xr, psel) : pack_v(nx));
-            // the o edge: message bits only (the next check rewrites V[o] as its x edge)
-            (void)new_msg<D0 - 1>(s.c[X], s.a[X], min1, k1, k2, P, MA, K.neg127);
-            MB = perm(k2, k1, 0x07030501u);
+            // the o edge: its code only (the next check rewrites V[o] as its x edge)
+            msg_code<D0 - 1>(s.c[X], s.a[X], min1, MA);
+            MB = perm(e2, e1, 0x07030501u);
         } else {
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;

@@ -54,6 +54,10 @@ LDPC_DEV uint32_t pk_max(uint32_t a, uint32_t b) { return us(__builtin_elementwi
 LDPC_DEV uint32_t pk_min(uint32_t a, uint32_t b) { return us(__builtin_elementwise_min(sv(a), sv(b))); }
 LDPC_DEV uint32_t pk_sub(uint32_t a, uint32_t b) { return us(sv(a) - sv(b)); }
 LDPC_DEV uint32_t pk_sra15(uint32_t a) { return us(sv(a) >> (short)15); }
+LDPC_DEV uint32_t pk_mul_lo(uint32_t a, uint32_t b)   // v_pk_mul_lo_u16
+{
+    return us(__builtin_bit_cast(s16x2, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b)));
+}
 LDPC_DEV uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 LDPC_DEV uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) { return __builtin_amdgcn_perm(s0, s1, sel); }
 // hide a value from the optimiser: keeps sign-splat masks as bit masks (v_bfi_b32)
@@ -108,16 +112,62 @@ LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t, uint32_t m3 = 0x03000300
     return perm(t.t1, t.t0, (sh & m3) | c4);
 }
 
-// new message of edge J: its code into MA, the new V (R pair) returned
+// Message record of a check (coop3): MB = eps * cst1, eps * cst2 as signed
+// bytes per codeword (eps = -1 where the sign parity of the check's
+// contributions, odd-degree flip included, is odd), MA = a 2-bit code per
+// edge: bit 0 = the edge's contribution c was negative, bit 1 = the edge got
+// cst2 (a > min1).  The message (reference: ((c < 0) ^ par) ? -cst : cst) is
+// then (-1)^bit0 * eps * cst, decoded by old_msg through the byte table
+// [+eps cst1, -eps cst1, +eps cst2, -eps cst2].
+
+// |x| of an R pair, or of a contribution saturated below R(-128) (0x8000):
+// the saturating 510 - c caps it at R(127), the reference's |max(c, -127)|
+LDPC_DEV uint32_t abs_sat(uint32_t r, uint32_t c510) { return pk_max(r, pk_sub_sat(c510, r)); }
+
+// eps * k (C form) of the check's two constants; par: sign bits = the parity
+LDPC_DEV void signed_csts(uint32_t k1, uint32_t k2, uint32_t par, uint32_t &e1, uint32_t &e2)
+{
+    const uint32_t eps = pk_sra15(par) | 0x00010001u;   // +-1 per half
+    e1 = pk_mul_lo(k1, eps);
+    e2 = pk_mul_lo(k2, eps);
+}
+
+// new V of first-group edge J (R pair), its code into MA.  Sign-magnitude
+// form of the reference's max(sat(c + m), -127) (code/x86/CDecoder/OMS/
+// CDecoder_OMS_fixed_SSE.cpp:239-254): c + m = sign(c) * (|c| + eps * cst),
+// so V' = sign(c) * min(|c| + eps * cst, 127) -- |c| + eps cst >= -cst >= -127
+// needs no lower clamp, and c enters only through its sign (a = |c| from
+// abs_sat), so c itself need not be clamped at -127
 template <int J>
-LDPC_DEV uint32_t new_msg(uint32_t c, uint32_t a, uint32_t min1, uint32_t k1, uint32_t k2, uint32_t P, uint32_t &MA,
-                          uint32_t neg127)
+LDPC_DEV uint32_t new_v(uint32_t c, uint32_t a, uint32_t min1, uint32_t e1, uint32_t e2, uint32_t &MA, uint32_t c510)
 {
     const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));   // -1: a > min1, the edge gets cst2
-    const uint32_t rr = bfi(neq, k2, k1);
-    const uint32_t sgn = pk_sra15(c ^ P);             // -1: the message is negative
-    MA |= (sgn & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
-    return pk_max(pk_add_sat(c, pk_sub(rr ^ sgn, sgn)), neg127);
+    const uint32_t T = pk_add_sat(a, bfi(neq, e2, e1));       // R(|c| + eps cst), capped at R(127)
+    const uint32_t sc = opaque(pk_sra15(c));                  // -1: c < 0
+    MA |= (sc & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
+    return bfi(sc, pk_sub(c510, T), T);
+}
+
+// the code of edge J only (an edge whose V the next check rewrites)
+template <int J>
+LDPC_DEV void msg_code(uint32_t c, uint32_t a, uint32_t min1, uint32_t &MA)
+{
+    const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));
+    const uint32_t sc = opaque(pk_sra15(c));
+    MA |= (sc & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
+}
+
+// later degree groups (a = |min(c, msg_max)| is not |c|; c clamped at -127):
+// V' = max(sat(c + m), -127) with m = (-1)^(c < 0) * (eps * cst), same record
+template <int J>
+LDPC_DEV uint32_t new_v_later(uint32_t c, uint32_t a, uint32_t min1, uint32_t e1, uint32_t e2, uint32_t &MA,
+                              uint32_t neg127)
+{
+    const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));
+    const uint32_t sc = pk_sra15(c);
+    const uint32_t m = bfi(neq, e2, e1);
+    MA |= (sc & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
+    return pk_max(pk_add_sat(c, pk_sub(m ^ sc, sc)), neg127);
 }
 
 template <int I, int N, typename F>
