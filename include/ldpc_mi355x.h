@@ -150,6 +150,12 @@ int ldpc_code_layer_info(const ldpc_code *h, int *n_layers, int *max_width, int 
 void ldpc_code_destroy(ldpc_code *h);
 
 /* ---- decoder context --------------------------------------------------- */
+/* device >= 0: a GPU context on that HIP device.  device = -1: a host context
+ * (no GPU needed): ldpc_decode_i8 / ldpc_decode_f32 /
+ * ldpc_quantize_f32_i8 run on the CPU (AVX2 int8 over blocks of 32 codewords
+ * on all host threads, LDPC_HOST_THREADS to cap them; the same bit-exact
+ * results as the GPU kernels), the device-buffer entry points return
+ * LDPC_EUNSUPPORTED and ldpc_ctx_last_kernel reports 10. */
 int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ldpc_ctx **out);
 void ldpc_ctx_destroy(ldpc_ctx *ctx);
 int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
@@ -165,7 +171,8 @@ int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel family the last decode actually ran (1 generic, 2 windowed,
- * 3 windowed2 S=16, 5 coop, 7 lds, 8 coop3, 9 ldsep; 0 before the first decode). */
+ * 3 windowed2 S=16, 5 coop, 7 lds, 8 coop3, 9 ldsep, 10 the host decoder of a
+ * device -1 context; 0 before the first decode). */
 int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
 /* The fastest kernel of this code that the last automatic selection could
  * not use for the call's parameters (8: coop3, 5: coop -- they take OMS / MS

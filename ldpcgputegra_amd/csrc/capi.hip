@@ -10,6 +10,8 @@
 // stream -- created once, not per call as the reference's decode_stream does
 // (code/gpu_fixed/decoder_ms/CGPU_Decoder_MS_SIMD.cu:223-224).
 #include <algorithm>
+#include <climits>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -19,6 +21,7 @@
 #include "windowed.h"
 #include "coop.h"
 #include "lds.h"
+#include "host.h"
 
 #define HIP_TRY(expr)                                                                          \
     do {                                                                                       \
@@ -116,12 +119,29 @@ extern "C" int ldpc_device_count(int *count)
     return LDPC_OK;
 }
 
+// device = -1: a host context (host.cpp) -- host-buffer decodes on the CPU,
+// no HIP call at all; the device-pointer entry points reject it
+static int host_only(const ldpc_ctx *c)
+{
+    return ldpc_set_error(LDPC_EUNSUPPORTED, "context %p is a host context (device -1): device buffers need a GPU "
+                          "context", (const void *)c);
+}
+
 extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ldpc_ctx **out)
 {
     if (!out) return ldpc_set_error(LDPC_EINVAL, "out is NULL");
     *out = nullptr;
     if (!h || max_batch <= 0) return ldpc_set_error(LDPC_EINVAL, "NULL code or max_batch <= 0");
     if (h->max_deg > 32) return ldpc_set_error(LDPC_EUNSUPPORTED, "check degree %d > 32", h->max_deg);
+    if (device == -1) {
+        auto *c = new ldpc_ctx();
+        c->code = h;
+        c->device = -1;
+        c->max_batch = max_batch;
+        c->max_stride = (max_batch + 63) / 64 * 64;
+        *out = c;
+        return LDPC_OK;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return ldpc_set_error(LDPC_EDEVICE, "no HIP device visible");
@@ -161,6 +181,10 @@ extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ld
 extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
 {
     if (!c) return;
+    if (c->device < 0) {
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->host_pending) (void)hipStreamSynchronize(c->host_stream);
@@ -199,6 +223,7 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 bool ldpc_ctx_has_kernel(const ldpc_ctx *c, int k)
 {
     if (!c || k < 0 || k > 9) return false;
+    if (c->device < 0) return k == 0;
     return !((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || k == 4 ||
              (k == 5 && !c->coop.valid) || k == 6 || (k == 7 && !c->lds.valid) || (k == 8 && !c->coop3.valid) ||
              (k == 9 && !c->lds.ep_valid));
@@ -222,6 +247,11 @@ extern "C" int ldpc_ctx_profile(ldpc_ctx *c, int enable)
 extern "C" int ldpc_ctx_kernel_time(ldpc_ctx *c, double *total_ms, int *launches, int reset)
 {
     if (!c) return ldpc_set_error(LDPC_EINVAL, "NULL ctx");
+    if (c->device < 0) {   // host context: no kernels
+        if (total_ms) *total_ms = 0.0;
+        if (launches) *launches = 0;
+        return LDPC_OK;
+    }
     HIP_TRY(hipSetDevice(c->device));
     double tot = 0.0;
     for (auto &pr : c->events) {
@@ -344,6 +374,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
 {
     int rc = check_params(c, batch, n_iter, p, is_float);
     if (rc != LDPC_OK) return rc;
+    if (c->device < 0) return host_only(c);
     if (batch == 0) return LDPC_OK;
     HIP_TRY(hipSetDevice(c->device));
     const ldpc_code *h = c->code;
@@ -570,6 +601,11 @@ static int decode_host(ldpc_ctx *c, const void *llr, uint8_t *hard, int batch, i
     if (!c || ((!llr || !hard) && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr/hard");
     int rc = check_params(c, batch, n_iter, p, is_float);
     if (rc != LDPC_OK || batch == 0) return rc;
+    if (c->device < 0) {   // host context: the CPU decoder (host.cpp)
+        c->last_kernel = 10;
+        return is_float ? host_decode_f32(c->code, (const float *)llr, hard, batch, n_iter, p)
+                        : host_decode_i8(c->code, (const int8_t *)llr, hard, batch, n_iter, p);
+    }
     HIP_TRY(hipSetDevice(c->device));
     const size_t esz = is_float ? 4 : 1;
     const int n = c->code->n, nc_want = host_chunks(batch, (size_t)batch * n * esz);
@@ -660,6 +696,7 @@ static int decode_host_async(ldpc_ctx *c, void *sv, const void *llr, uint8_t *ha
     if (!c || ((!llr || !hard) && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr/hard");
     int rc = check_params(c, batch, n_iter, p, is_float);
     if (rc != LDPC_OK || batch == 0) return rc;
+    if (c->device < 0) return host_only(c);
     HIP_TRY(hipSetDevice(c->device));
     const hipStream_t s = (hipStream_t)sv;
     const size_t n = (size_t)c->code->n, esz = is_float ? 4 : 1;
@@ -737,6 +774,7 @@ extern "C" int ldpc_awgn_i8_async(ldpc_ctx *c, void *s, int8_t *d_llr, int batch
                                   const uint32_t *table, const uint8_t *d_codeword)
 {
     if (!c || !d_llr || !table || batch < 0) return ldpc_set_error(LDPC_EINVAL, "awgn args");
+    if (c->device < 0) return host_only(c);
     if (table[63] < 1 || table[63] > 31) return ldpc_set_error(LDPC_EINVAL, "awgn table sat");
     HIP_TRY(hipSetDevice(c->device));
     AwgnTable t;
@@ -756,6 +794,7 @@ extern "C" int ldpc_quantize_f32_i8_async(ldpc_ctx *c, void *s, const float *d_y
 {
     if (!c || (count > 0 && (!d_y || !d_q)) || !quantize_args_ok(count, factor, sat_neg, sat_pos))
         return ldpc_set_error(LDPC_EINVAL, "quantize args");
+    if (c->device < 0) return host_only(c);
     HIP_TRY(hipSetDevice(c->device));
     if (launch_quantize_f32_i8(d_y, d_q, count, factor, sat_neg, sat_pos, (hipStream_t)s))
         return ldpc_set_error(LDPC_EDEVICE, "quantize: %s", hipGetErrorString(hipGetLastError()));
@@ -768,6 +807,15 @@ extern "C" int ldpc_quantize_f32_i8(ldpc_ctx *c, const float *y, int8_t *q, long
     if (!c || (count > 0 && (!y || !q)) || !quantize_args_ok(count, factor, sat_neg, sat_pos))
         return ldpc_set_error(LDPC_EINVAL, "quantize args");
     if (count == 0) return LDPC_OK;
+    if (c->device < 0) {   // host context: CFastFixConversion::generate's rule on the CPU (quantize_k's)
+        for (long i = 0; i < count; i++) {
+            const float v = (float)factor * y[i];
+            int value = (std::fabs(v) < 2147483648.0f) ? (int)v : INT_MIN;
+            value = std::min(std::max(value, sat_neg), sat_pos);
+            q[i] = (int8_t)value;
+        }
+        return LDPC_OK;
+    }
     HIP_TRY(hipSetDevice(c->device));
     const size_t in_bytes = (size_t)count * sizeof(float), al = (in_bytes + 255) & ~(size_t)255;
     int rc;
@@ -788,6 +836,7 @@ extern "C" int ldpc_count_errors_async(ldpc_ctx *c, void *s, const uint8_t *d_ha
 {
     if (!c || !d_hard || !d_counts || batch < 0 || k < 0 || k > c->code->n)
         return ldpc_set_error(LDPC_EINVAL, "count_errors args");
+    if (c->device < 0) return host_only(c);
     HIP_TRY(hipSetDevice(c->device));
     if (launch_count_errors(d_hard, c->code->n, batch, k, d_ref, d_counts, (hipStream_t)s))
         return ldpc_set_error(LDPC_EDEVICE, "count_errors: %s", hipGetErrorString(hipGetLastError()));

@@ -98,11 +98,16 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 
 // slot record (coop3_upload): words 0..4 the LDS byte offsets (from the line
 // cache) of the info entries' 16-B pieces, 5 / 6 the x / o edge parity rows
-// (row - k), 7 meta = check | COOP_M_ACT | chain step << STEP_SHIFT, 8 the
-// period's line load / writeback (line | line << 16) and 9 its slot write /
-// writeback slot (slot | slot << 16) of lane group (slot & 7) of the slot's
-// slab wave (LcPlan::ops), 10 .. 11 zero
+// (row - k) in their low halves -- word 5's high half the u16 index of the
+// slot's chain input in xo[buf] and word 6's the byte offset of its chain
+// constants in cst[buf] (from its chain step: the pre needs no arithmetic on
+// it) -- 7 meta = check | COOP_M_ACT | chain step << STEP_SHIFT, 8 .. 11
+// the period's line ops of lane group (slot & 7) of the slot's slab wave
+// (LcPlan::ops) as byte offsets: 8 the line loaded, 9 the line written back
+// (from the group's V block), 10 the slot written with the load of LC_PUT
+// periods earlier, 11 the slot written back (from the line cache)
 constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
+static_assert(W_LOP + 4 <= RECW, "line-op words");
 
 template <int WS, int R>
 struct Cfg {
@@ -111,8 +116,6 @@ struct Cfg {
     static constexpr int NI = R + 1;                   // LDS-DMA input windows in flight per slab wave
     static constexpr int NS = R + 1 < 3 ? 3 : R + 1;   // window states in VGPRs (pre at p-1, post at p+1)
     static constexpr int U = NS;                       // periods unrolled (multiple of NI and NS)
-    static constexpr int NR = 2;                       // staged-output windows: window g's parity V is staged in
-                                                       // period g+1 and read for its stores at that period's end
     static constexpr int CHW = WS >= 3 ? 3 : WS;       // the chain wave (waves go to SIMDs 0,2,1,3,0,2,1: wave 3
                                                        // has a SIMD of its own for WS = 3 and WS = 6)
     static constexpr int NB = S / 8;                   // chain blocks of 8 steps
@@ -123,10 +126,8 @@ struct Cfg {
 template <int WS, int R>
 struct alignas(16) Smem3 {
     using CF = Cfg<WS, R>;
-    static constexpr int S = CF::S, NI = CF::NI, NR = CF::NR;
+    static constexpr int S = CF::S, NI = CF::NI;
     uint4 lc[LC_SLOTS][8];            // line cache: slot = 8 V rows x 16 codewords (LcPlan; slot 0: the sink)
-    uint4 stg[NR][2][S + 1];          // parity V of a window, [x edge / the tail's last edge][slot] x 16
-                                      // codewords (int8): the stores' staging
     uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
@@ -134,8 +135,10 @@ struct alignas(16) Smem3 {
     struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
         uint4 d[5][8];                //   e < 4: message bytes 16e .. 16e+15, e = 4: the o-edge parity row
     } in[WS][NI];
-    uint4 mst[2][WS][8][4];           // new messages of window g per slab wave in mst[g & 1], [slot] x 64 B
-                                      // (posted in period g+1, stored by the memory wave in period g+2)
+    uint4 mst[2][WS][8][6];           // window g's outputs per slab wave in mst[g & 1], per slot: its new
+                                      // messages (pieces 0..3, 8 pairs x 8 B), the x edge's new V (piece 4)
+                                      // and the tail's last edge's (5), 16 codewords each (posted in period
+                                      // g+1, stored by the memory wave in period g+2: lane q its piece q)
 };
 
 struct Coop3Args {
@@ -153,7 +156,7 @@ struct Coop3Args {
     int G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
     uint32_t nmsf;                    // NMS factor per half (value form)
     size_t gstride;                   // bytes between two codeword groups' V
-    uint32_t rmm, coff, offp;         // R(msg_max), C(offset), offset per half (value form)
+    uint32_t rmm, coff, offp;         // R(msg_max), C(offset) + 255 (R - coff: C form), offset per half (value form)
 };
 
 struct St3 {                          // one window's state from pre to post (R / C pairs)
@@ -162,6 +165,7 @@ struct St3 {                          // one window's state from pre to post (R 
     uint32_t mn1, mn2, sacc, mx;      // min1 / min2 / sign parity over info + o; x-edge old message
                                       // tail: mn1 = MA, mn2 = MB
     uint32_t xs;                      // the slot's chain step: u16 index of its x input in xo[buf]
+    uint32_t ad[X];                   // the info edges' pair addresses in the line cache (pre reads, post writes)
     uint32_t v[X];                    // FZ (early termination): the info edges' V as read (R pairs)
 };
 
@@ -191,18 +195,15 @@ struct Rec {
 // what a pre reads from LDS
 struct PreIn {
     uint32_t v[D0 - 1];               // raw V dwords (info edges from the line cache, the o edge from In)
+    uint32_t ad[X];                   // the info pairs' byte offsets in the line cache
     uint32_t ma, mb;                  // old message record of this pair
-    uint32_t meta;
-};
-struct StIn {                         // the store of window p-2: one 16-B piece per lane
-    uint4 d;
-    char *addr;
+    uint32_t meta, wx, wo;            // record words 7, 5, 6
 };
 
 template <int WS, int R, bool NMS = false>
 struct Slab3 {
     using SM = Smem3<WS, R>;
-    static constexpr int S = SM::S, NR = SM::NR;
+    static constexpr int S = SM::S;
     SM &sm;
     const Coop3Args &a;
     int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
@@ -211,35 +212,13 @@ struct Slab3 {
     uint32_t fk;                      // NMS factor per half (value form)
     char *Vg;                         // the group's V rows (16 B each; parity row k + j at Pr + 16 j)
     // LDS byte offsets of this lane inside a line-cache piece: the pre's V
-    // dword (4 (q >> 1)), the post's u16 (2 q), and a line op's 16-B piece (16 q)
-    uint32_t lrd, lwr, lq;
-    // gathers, lane (e, slot) = (lane >> 3, lane & 7): e < 4 message piece e of
-    // the slot's check, e = 4 its o-edge parity row, e > 4 idle
-    const char *gbase;
-    uint32_t gmul, gmask, gsel;
-    // stores, lane (kl, q): q < 4 message piece q, q = 4 the x-edge parity
-    // row, q = 5 the tail's last edge (else the sink row)
-    char *sbase;
-    uint32_t smul;
+    // dword (4 (q >> 1)) and the post's u16 (2 q)
+    uint32_t lrd, lwr;
     uint32_t mrd, prd;                // byte offsets in an In record: this lane's message pair / o-edge V dword
-    // read_st's per-lane constants (set by init_st): record word byte offset and
-    // mask, sink masks (window not / the tail), stage-source mask and offset of
-    // the 16-B piece from mst[w][kl][0]
-    uint32_t stw = 0, stm = 0, snk = 0, snk_tl = 0, stst = 0, sto = 0;
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
 
-    LDPC_DEV void init_st()
-    {
-        stw = 4u * (uint32_t)(q < 4 ? W_META : q == 4 ? W_X : W_O);
-        stm = q < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
-        snk = q >= 5 ? 0xFFFFFFFFu : 0u;
-        snk_tl = q >= 6 ? 0xFFFFFFFFu : 0u;
-        stst = q >= 4 ? 0xFFFFFFFFu : 0u;
-        const char *src = q < 4 ? (const char *)&sm.mst[w][kl][q] : (const char *)&sm.stg[0][q == 4 ? 0 : 1][k];
-        sto = (uint32_t)(src - (const char *)&sm.mst[w][kl][0]);
-    }
     LDPC_DEV const char *lcb() const { return (const char *)&sm.lc[0][0]; }
     LDPC_DEV char *lcw() const { return (char *)&sm.lc[0][0]; }
 
@@ -249,12 +228,16 @@ struct Slab3 {
         const uint4 *r = (const uint4 *)&sm.tab[g & (TQ - 1)][k][0];
         return {r[0], r[1]};
     }
-    LDPC_DEV uint2 read_lop(int g) const { return *(const uint2 *)&sm.tab[g & (TQ - 1)][k][W_LOP]; }
     // pre inputs of the window whose records are rc (its gathers landed in in[w][ib])
     LDPC_DEV void read_pre(int ib, const Rec &rc, PreIn &in) const
     {
         const char *inb = (const char *)&sm.in[w][ib];
-        in.v[0] = *(const uint32_t *)(lcb() + rc.pc.x + lrd);
+        in.ad[0] = rc.pc.x + lwr;
+        in.ad[1] = rc.pc.y + lwr;
+        in.ad[2] = rc.pc.z + lwr;
+        in.ad[3] = rc.pc.w + lwr;
+        in.ad[4] = rc.pm.x + lwr;
+        in.v[0] = *(const uint32_t *)(lcb() + rc.pc.x + lrd);   // the dword holding this lane's pair
         in.v[1] = *(const uint32_t *)(lcb() + rc.pc.y + lrd);
         in.v[2] = *(const uint32_t *)(lcb() + rc.pc.z + lrd);
         in.v[3] = *(const uint32_t *)(lcb() + rc.pc.w + lrd);
@@ -264,21 +247,8 @@ struct Slab3 {
         in.ma = mm.x;
         in.mb = mm.y;
         in.meta = rc.pm.w;
-    }
-    // the store of window g (tl: the tail window): address and 16-B piece of
-    // this lane.  Branch-free: lane q reads record word stw (q < 4 the meta,
-    // q = 4 the x row, q >= 5 the o row), lanes past the op's width take the sink
-    LDPC_DEV void read_st(int g, bool tl, StIn &in) const
-    {
-        const uint32_t rw = *(const uint32_t *)((const char *)&sm.tab[g & (TQ - 1)][k][0] + stw) & stm;
-        const uint32_t idx = bfi(tl ? snk_tl : snk, (uint32_t)a.m, rw);
-        in.addr = sbase + (size_t)idx * smul;
-        in.d = *(const uint4 *)((const char *)&sm.mst[w][kl][0] + sto +
-                                (stst & ((uint32_t)(g % NR) * (uint32_t)sizeof(sm.stg[0]))));
-    }
-    LDPC_DEV uint32_t read_gidx(int g) const   // the gather's row / check of window g (lane (e, slot))
-    {
-        return sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
+        in.wx = rc.pm.y;
+        in.wo = rc.pm.z;
     }
     LDPC_DEV uint32_t read_x(int g, const St3 &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
@@ -286,22 +256,6 @@ struct Slab3 {
         const uint32_t x0 = xs[0], x1 = xs[8];
         return perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127]
     }
-
-    // ---- vector memory (every op unconditional and 64 lanes wide: unused
-    // lanes go to the sink row / line / slot, so the per-period vmcnt counts
-    // are static)
-    LDPC_DEV void stores(const StIn &in) const { *(uint4 *)in.addr = in.d; }
-    LDPC_DEV void gathers(uint32_t idx, int ib) const
-    {
-        const uint32_t base = (uint32_t)(uintptr_t)&sm.in[w][ib];
-        if (lane < 40) dma16(gbase + (size_t)idx * gmul, base);
-    }
-    // line cache: writeback of period p (slot -> VGPRs, then HBM), load of
-    // period p (HBM -> VGPRs), slot write of the load of period p-LC_PUT
-    LDPC_DEV uint4 wb_read(uint2 lop) const { return *(const uint4 *)(lcb() + (lop.y >> 16) * 128u + lq); }
-    LDPC_DEV void wb_store(uint2 lop, const uint4 &d) const { *(uint4 *)(Vg + (size_t)(lop.x >> 16) * 128 + lq) = d; }
-    LDPC_DEV uint4 line_load(uint2 lop) const { return *(const uint4 *)(Vg + (size_t)(lop.x & 0xFFFFu) * 128 + lq); }
-    LDPC_DEV void line_put(uint2 lop, const uint4 &d) const { *(uint4 *)(lcw() + (lop.y & 0xFFFFu) * 128u + lq) = d; }
 
     // pre of window g: chain constants -> cst[g & 1], state -> s
     template <bool TL, bool FZ_ = false, int MP = -1>
@@ -312,6 +266,8 @@ struct Slab3 {
         uint32_t v[D0 - 1];
 #pragma unroll
         for (int j = 0; j <= X; j++) v[j] = unpack_v(in.v[j], usel);
+#pragma unroll
+        for (int j = 0; j < X; j++) s.ad[j] = in.ad[j];
         const MsgTab t = msg_tab(in.mb);
         const uint32_t MA = in.ma, neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
@@ -362,7 +318,7 @@ struct Slab3 {
                 A = pk_sub(pk_shl5(COV), efm);                                // 32 c_o - eps f m_x
                 B = pk_add(A, 0x001F001Fu);
             } else {
-                TV = pk_ashr8(pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0));
+                TV = pk_ashr8(pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), 0u));   // coff = C(off) + 255: C form
                 EPS = EM | 0x00010001u;
                 const uint32_t base = pk_sub(COV, pk_sub(pk_ashr8(mx) ^ EM, EM));   // c_o - eps * m_x
                 A = pk_sub(base, a.offp);
@@ -392,9 +348,9 @@ struct Slab3 {
                 min1 = pk_min(min1, aj);
             });
             const uint32_t k1 = NMS ? nms_c(pk_min(min2, K.rmm), fk)
-                                    : pk_min(pk_max(pk_sub(min2, K.coff), K.r0), K.rmm) & HIBYTES;
+                                    : pk_min(pk_max(pk_sub(min2, K.coff), 0u), K.rmm) & HIBYTES;
             const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
-                                    : pk_min(pk_max(pk_sub(min1, K.coff), K.r0), K.rmm) & HIBYTES;
+                                    : pk_min(pk_max(pk_sub(min1, K.coff), 0u), K.rmm) & HIBYTES;
             uint32_t e1, e2, MAn = 0;
             signed_csts(k1, k2, sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u), e1, e2);
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
@@ -427,8 +383,7 @@ struct Slab3 {
         // the halves with ds_write_b16 / _d16_hi instead of these 6 v_perm ran
         // 3 % slower: 43.7 vs 42.4 ms)
         const int cb = g & 1;
-        const uint32_t step = (meta >> STEP_SHIFT) & 63u;
-        s.xs = (step >> 3) * (CW * 8) + (step & 7);
+        s.xs = in.wx >> 16;
         uint4 r0, r1;
         r0.x = perm(B, A, 0x05040100u);
         r1.x = perm(B, A, 0x07060302u);
@@ -437,22 +392,21 @@ struct Slab3 {
         r0.z = perm(H, L, 0x05040100u);
         r1.z = perm(H, L, 0x07060302u);
         r0.w = r1.w = 0;
-        uint4 *cp = &sm.cst[cb][0][0][q] + step * (2 * NP);
+        uint4 *cp = (uint4 *)((char *)&sm.cst[cb][0][0][q] + (in.wo >> 16));
         cp[0] = r0;
         cp[NP] = r1;
     }
 
-    // post of window g (x inputs xr, records rc): new info V pairs -> the line
-    // cache, parity V -> stg[g % NR], messages -> mst[w]; the last two leave
-    // in the store of period g + 2
+    // post of window g (x inputs xr): new info V pairs -> the line cache (at
+    // the addresses its pre read), messages and parity V -> mst[g & 1][w][kl];
+    // those leave in the memory wave's store of period g + 2
     template <bool TL, bool FZ_ = false, int MP = -1>
-    LDPC_DEV void post(int g, uint32_t xr, const St3 &s, const Rec &rc) const
+    LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
     {
         constexpr bool FZ = FZ_;
-        unsigned short *sx = (unsigned short *)&sm.stg[g % NR][0][k] + q, *so = (unsigned short *)&sm.stg[g % NR][1][k] + q;
-        const uint32_t pcs[X] = {rc.pc.x, rc.pc.y, rc.pc.z, rc.pc.w, rc.pm.x};
+        unsigned short *sx = (unsigned short *)&sm.mst[g & 1][w][kl][4] + q, *so = (unsigned short *)&sm.mst[g & 1][w][kl][5] + q;
         auto put = [&](int j, uint32_t v) __attribute__((always_inline)) {
-            *(unsigned short *)(lcw() + pcs[j] + lwr) = (unsigned short)v;
+            *(unsigned short *)(lcw() + s.ad[j]) = (unsigned short)v;
         };
         uint32_t MA, MB;
         if constexpr (!TL) {
@@ -461,9 +415,9 @@ struct Slab3 {
             const uint32_t sacc = s.sacc ^ cx;
             const uint32_t min2 = pk_max(s.mn1, pk_min(ax, s.mn2)), min1 = pk_min(ax, s.mn1);
             const uint32_t k1 = NMS ? nms_c(pk_min(min2, K.rmm), fk)
-                                    : pk_max(pk_sub(pk_min(min2, K.rmm), K.coff), K.r0) & HIBYTES;
+                                    : pk_max(pk_sub(pk_min(min2, K.rmm), K.coff), 0u);   // C(max(min - off, 0))
             const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
-                                    : pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), K.r0) & HIBYTES;
+                                    : pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), 0u);
             uint32_t e1, e2;
             signed_csts(k1, k2, sacc ^ ((D0 & 1) ? SIGNS : 0u), e1, e2);
             MA = 0;
@@ -824,7 +778,6 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         return;
     }
 
-    char *Pr = Vg + (size_t)a.k * 16;   // parity row k + j at Pr + 16 j (row n: the sink)
     const char *Mb = (const char *)a.Mc + (size_t)wg * a.gstride;   // the group's messages (coop3_group_layout)
     constexpr int NI = CF::NI, NS = CF::NS;
     constexpr int MW = WS + 1;   // the memory wave (shares the chain wave's SIMD)
@@ -850,13 +803,13 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         const uint32_t moff = (uint32_t)(Mb - (const char *)Vg), poff = (uint32_t)a.k * 16u;
         // gathers: lane (e, slot) = (kl, q): e < 4 message piece e, e = 4 the o-edge parity row
         const uint32_t gshl = kl < 4 ? 6u : 4u, goff = kl < 4 ? moff + 16u * (uint32_t)kl : poff;
-        const uint32_t gmask = kl < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
+        const uint32_t gmask = kl < 4 ? COOP_CHK_MASK : 0xFFFFu;
         const uint32_t gsel = (uint32_t)(kl < 4 ? W_META : W_O);
         // stores: lane (kl, q) of slot 8w + kl: q < 4 message piece q, q = 4 the
         // x-edge parity row, q = 5 the tail's last edge, the rest the sink row
         const uint32_t sshl = q < 4 ? 6u : 4u, soff = q < 4 ? moff + 16u * (uint32_t)q : poff;
         const uint32_t stw = 4u * (uint32_t)(q < 4 ? W_META : q == 4 ? W_X : W_O);
-        const uint32_t stm = q < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu;
+        const uint32_t stm = q < 4 ? COOP_CHK_MASK : 0xFFFFu;
         const uint32_t snk = q >= 5 ? 0xFFFFFFFFu : 0u, snk_tl = q >= 6 ? 0xFFFFFFFFu : 0u;
         static_assert(MREC == 64, "message block of a check: 1 << 6 bytes");
         auto gather = [&](int w, int g, int ib) __attribute__((always_inline)) {
@@ -871,9 +824,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             const uint32_t rw = *(const uint32_t *)((const char *)&sm.tab[g & (TQ - 1)][8 * w + kl][0] + stw) & stm;
             return live ? bfi(tl ? snk_tl : snk, (uint32_t)a.m, rw) : (uint32_t)a.m;
         };
+        const int qp = q < 5 ? q : 5;   // lane q's piece of a slot's outputs (q > 5: any, stored to the sink)
         auto store_win = [&](int w, int g, uint32_t idx) __attribute__((always_inline)) {
-            const uint4 *src = q < 4 ? &sm.mst[g & 1][w][kl][q] : &sm.stg[g & 1][q == 4 ? 0 : 1][8 * w + kl];
-            rbuf_store_v4(__builtin_bit_cast(i32x4, *src), vr, (int)((idx << sshl) + soff), 0, 0);
+            rbuf_store_v4(__builtin_bit_cast(i32x4, sm.mst[g & 1][w][kl][qp]), vr, (int)((idx << sshl) + soff), 0, 0);
         };
         for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
             __syncthreads();   // prologue 1: tables and resident lines in LDS
@@ -893,11 +846,11 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 for (int w = 0; w < WS; w++) pend[i][w] = make_uint4(0, 0, 0, 0);
             int uS = a.nw - 1;   // local index of window p-1 (the next period's stores)
             uint32_t sidx[WS];   // the stores' indices (window p-2), read in period p-1
-            uint2 lop[WS];       // the line ops of period p, read in period p-1
+            uint4 lop[WS];       // the line ops of period p (byte offsets, record words 8 .. 11), read in period p-1
 #pragma unroll
             for (int w = 0; w < WS; w++) {
                 sidx[w] = (uint32_t)a.m;
-                lop[w] = *(const uint2 *)&sm.tab[0][8 * w + kl][W_LOP];
+                lop[w] = *(const uint4 *)&sm.tab[0][8 * w + kl][W_LOP];
             }
             // period p: gathers of window p+1+R, line loads of period p, line
             // writebacks of period p, stores of window p-2 (4 WS = 24 ops);
@@ -910,17 +863,28 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             // while the compiler emits exactly these 24 vector-memory
             // instructions per period: tools/check_vmcnt.py (run by
             // __graft_entry__.build) checks the ISA
+            // Latency: every LDS read the period's vector-memory ops need is
+            // issued at its start -- the gather indices, and the writeback and
+            // store data (their writers ran before the barrier) -- so the
+            // round trips overlap the slot writes, gathers and loads issued
+            // meanwhile instead of each preceding its store
             auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
                 constexpr int s = decltype(sc_)::value;   // p % NPD
                 if (STAMP) tx = stampL();
                 uint32_t gix[WS];
+                uint4 wbd[WS], std_[WS];
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
                     gix[w] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
                 });
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    constexpr int w = decltype(wc)::value;
+                    wbd[w] = *(const uint4 *)(lcb + lop[w].w + lq);
+                    std_[w] = sm.mst[(p - 2) & 1][w][kl][qp];
+                });
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
                     constexpr int w = decltype(wc)::value;
-                    *(uint4 *)(lcb + (lop[w].y & 0xFFFFu) * 128u + lq) = pend[(s + 1) % NPD][w];
+                    *(uint4 *)(lcb + lop[w].z + lq) = pend[(s + 1) % NPD][w];
                 });
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
@@ -928,25 +892,21 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 });
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
-                    pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(((lop[w].x & 0xFFFFu) << 7) + lq), 0, 0));
+                    pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w].x + lq), 0, 0));
                 });
-                // (reading all of a period's writeback / store pieces from LDS
-                // first, so that their latencies overlap, ran 2 % slower)
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // writebacks of period p
                     constexpr int w = decltype(wc)::value;
-                    const uint4 v = *(const uint4 *)(lcb + (lop[w].y >> 16) * 128u + lq);
-                    rbuf_store_v4(__builtin_bit_cast(i32x4, v), vr, (int)(((lop[w].x >> 16) << 7) + lq), 0, 0);
+                    rbuf_store_v4(__builtin_bit_cast(i32x4, wbd[w]), vr, (int)(lop[w].y + lq), 0, 0);
                 });
-                // the stores of window p-2 (the sink before period 2), then the
-                // indices of window p-1's and the next period's line ops
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // stores of window p-2 (sink before period 2)
                     constexpr int w = decltype(wc)::value;
-                    store_win(w, p - 2, sidx[w]);
+                    rbuf_store_v4(__builtin_bit_cast(i32x4, std_[w]), vr, (int)((sidx[w] << sshl) + soff), 0, 0);
                 });
+                // the indices of window p-1's stores and of the next period's line ops
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
                     sidx[w] = store_idx(w, p - 1, uS == a.tail, p >= 1);
-                    lop[w] = *(const uint2 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][W_LOP];
+                    lop[w] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][W_LOP];
                 });
                 if (STAMP) sP[1] += stampL() - tx;
                 asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
@@ -997,13 +957,6 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     Vg,
                     (uint32_t)(4 * (q >> 1)),
                     (uint32_t)(2 * q),
-                    (uint32_t)(16 * q),
-                    kl < 4 ? Mb + kl * 16 : (const char *)Pr,
-                    kl < 4 ? (uint32_t)MREC : 16u,
-                    kl < 4 ? COOP_CHK_MASK : 0xFFFFFFFFu,
-                    (uint32_t)(kl < 4 ? W_META : W_O),
-                    q < 4 ? (char *)Mb + q * 16 : Pr,
-                    q < 4 ? (uint32_t)MREC : 16u,
                     (uint32_t)(((q >> 1) * 8 + kl) * 16 + (q & 1) * 8),
                     (uint32_t)((32 + kl) * 16 + 4 * (q >> 1))};
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
@@ -1058,14 +1011,21 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             PreIn in;
             St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
-            const Rec rcp = sl.read_rec(p - 1);     // the post's records
             if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs), then reads and runs its pre
                 if (fair) __builtin_amdgcn_s_setprio(P0);
-                const uint32_t xr = sl.read_x(p - 1, sp);
-                sl.template post<false, ET, MP1>(p - 1, xr, sp, rcp);
-                sl.read_pre((s + 1) % NI, rcn, in);
+                if (sl.w != 0) {
+                    // no distance-2 reader outside slab wave 0: the pre's LDS
+                    // reads are issued first and land under the post
+                    sl.read_pre((s + 1) % NI, rcn, in);
+                    const uint32_t xr = sl.read_x(p - 1, sp);
+                    sl.template post<false, ET, MP1>(p - 1, xr, sp);
+                } else {
+                    const uint32_t xr = sl.read_x(p - 1, sp);
+                    sl.template post<false, ET, MP1>(p - 1, xr, sp);
+                    sl.read_pre((s + 1) % NI, rcn, in);
+                }
                 rcn = sl.read_rec(p + 2);
                 if (STAMP) t1 = t2 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(P1);
@@ -1075,9 +1035,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 if (dpo) {
                     const uint32_t xr = sl.read_x(p - 1, sp);
                     if (uA == a.tail)
-                        sl.template post<true, ET>(p - 1, xr, sp, rcp);
+                        sl.template post<true, ET>(p - 1, xr, sp);
                     else
-                        sl.template post<false, ET>(p - 1, xr, sp, rcp);
+                        sl.template post<false, ET>(p - 1, xr, sp);
                 }
                 if (STAMP) t1 = t2 = t3 = stampL();
                 if (dpr) sl.read_pre((s + 1) % NI, rcn, in);
@@ -1281,11 +1241,15 @@ static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vec
             const uint32_t *src = &ho.pl.tab[((size_t)u * S + kk) * RECW];
             uint32_t *rec = &out[((size_t)u * S + kk) * RECW];
             for (int j = 0; j < X; j++) rec[j] = lp.piece[((size_t)u * S + kk) * X + j];
-            rec[W_X] = src[X] - (uint32_t)k;
-            rec[W_O] = src[D0 - 1] - (uint32_t)k;
+            const uint32_t step = (src[D0] >> STEP_SHIFT) & 63u;   // (rows - k <= m < 65536: checked by coop3_plan_lc)
+            rec[W_X] = (src[X] - (uint32_t)k) | ((step >> 3) * (CW * 8) + (step & 7)) << 16;   // + xo index
+            rec[W_O] = (src[D0 - 1] - (uint32_t)k) | (step * 2 * NP * 16) << 16;              // + cst offset
             rec[W_META] = src[D0];
-            rec[W_LOP] = lp.ops[((size_t)u * LC_OPS + kk) * 2];
-            rec[W_LOP + 1] = lp.ops[((size_t)u * LC_OPS + kk) * 2 + 1];
+            const uint32_t lines = lp.ops[((size_t)u * LC_OPS + kk) * 2], slots = lp.ops[((size_t)u * LC_OPS + kk) * 2 + 1];
+            rec[W_LOP] = (lines & 0xFFFFu) * 128u;        // line loaded (byte offset in the group's V block)
+            rec[W_LOP + 1] = (lines >> 16) * 128u;        // line written back
+            rec[W_LOP + 2] = (slots & 0xFFFFu) * 128u;    // slot written with the load of LC_PUT periods earlier
+            rec[W_LOP + 3] = (slots >> 16) * 128u;        // slot written back
         }
 }
 
@@ -1295,6 +1259,7 @@ int coop3_plan_lc(const ldpc_code *h, Coop3Host &ho, LcPlan &lp)
     const int rc = coop3_plan_host(h, ws, r, ho);
     if (rc != 0) return rc;
     const int k = h->n - h->m;
+    if (h->m > 0xFFFF) return 1;   // parity rows - k (and the sink row n - k = m) share a record word with 16-bit fields
     if (lc_build_plan(ho.pl.tab, RECW, ho.nw, ho.S, D0, h->n, k, LC_SLOTS, lp) != 0) return 1;
     return 0;
 }
@@ -1397,7 +1362,7 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.d1 = cc.d1;
     a.rmm = (uint32_t)(L.msg_max * 256 + 255) * 0x00010001u;
     const bool nms = L.algo == LDPC_ALGO_NMS;
-    a.coff = nms ? 0u : (uint32_t)(L.param * 256) * 0x00010001u;
+    a.coff = nms ? 0u : (uint32_t)(L.param * 256 + 255) * 0x00010001u;
     a.offp = nms ? 0u : (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
     a.nmsf = nms ? (uint32_t)(L.param & 0xFFFF) * 0x00010001u : 0u;
     a.prio = env_int3("LDPC_COOP3_PRIO", 1);

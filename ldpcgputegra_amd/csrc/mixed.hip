@@ -49,6 +49,7 @@ extern "C" int ldpc_mixed_create(const ldpc_code *const *codes, int n_codes, int
     if (!out) return ldpc_set_error(LDPC_EINVAL, "out is NULL");
     *out = nullptr;
     if (!codes || n_codes <= 0 || max_batch <= 0) return ldpc_set_error(LDPC_EINVAL, "mixed: bad arguments");
+    if (device < 0) return ldpc_set_error(LDPC_EUNSUPPORTED, "mixed: device buffers need a GPU (device %d)", device);
     for (int c = 0; c < n_codes; c++)
         if (!codes[c] || codes[c]->n != codes[0]->n)
             return ldpc_set_error(LDPC_EINVAL, "mixed: all codes must be non-NULL with equal N");

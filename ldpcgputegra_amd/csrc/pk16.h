@@ -120,6 +120,16 @@ LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t, uint32_t m3 = 0x03000300
 // then (-1)^bit0 * eps * cst, decoded by old_msg through the byte table
 // [+eps cst1, -eps cst1, +eps cst2, -eps cst2].
 
+// (a & m) | b as one v_bitop3_b32 (truth table 0xEA); written with | and &
+// the compiler builds an and + or3 tree: 1.5 instructions per flag, not 1
+LDPC_DEV uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) { return __builtin_amdgcn_bitop3_b32(a, m, b, 0xEA); }
+// edge J's code (bit 0: c < 0, bit 1: got cst2) into MA, from the two half masks
+template <int J>
+LDPC_DEV uint32_t add_code(uint32_t MA, uint32_t sc, uint32_t neq)
+{
+    return and_or(neq, 0x00020002u << (2 * J), and_or(sc, 0x00010001u << (2 * J), MA));
+}
+
 // |x| of an R pair, or of a contribution saturated below R(-128) (0x8000):
 // the saturating 510 - c caps it at R(127), the reference's |max(c, -127)|
 LDPC_DEV uint32_t abs_sat(uint32_t r, uint32_t c510) { return pk_max(r, pk_sub_sat(c510, r)); }
@@ -144,7 +154,7 @@ LDPC_DEV uint32_t new_v(uint32_t c, uint32_t a, uint32_t min1, uint32_t e1, uint
     const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));   // -1: a > min1, the edge gets cst2
     const uint32_t T = pk_add_sat(a, bfi(neq, e2, e1));       // R(|c| + eps cst), capped at R(127)
     const uint32_t sc = opaque(pk_sra15(c));                  // -1: c < 0
-    MA |= (sc & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
+    MA = add_code<J>(MA, sc, neq);
     return bfi(sc, pk_sub(c510, T), T);
 }
 
@@ -154,7 +164,7 @@ LDPC_DEV void msg_code(uint32_t c, uint32_t a, uint32_t min1, uint32_t &MA)
 {
     const uint32_t neq = opaque(pk_sra15(pk_sub(min1, a)));
     const uint32_t sc = opaque(pk_sra15(c));
-    MA |= (sc & (0x00010001u << (2 * J))) | (neq & (0x00020002u << (2 * J)));
+    MA = add_code<J>(MA, sc, neq);
 }
 
 // later degree groups (a = |min(c, msg_max)| is not |c|; c clamped at -127):

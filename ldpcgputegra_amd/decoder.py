@@ -78,7 +78,7 @@ class Decoder:
         _lib.check(_lib.lib().ldpc_ctx_kernel_time(self._ctx, C.byref(ms), C.byref(n), int(reset)))
         return ms.value, n.value
 
-    KERNEL_NAMES = {0: "none", 1: "generic", 2: "windowed", 3: "windowed2_s16", 4: "windowed2_s32", 5: "coop", 6: "coop2", 7: "lds", 8: "coop3", 9: "ldsep"}
+    KERNEL_NAMES = {0: "none", 1: "generic", 2: "windowed", 3: "windowed2_s16", 4: "windowed2_s32", 5: "coop", 6: "coop2", 7: "lds", 8: "coop3", 9: "ldsep", 10: "host"}
 
     @property
     def last_kernel(self):

@@ -123,6 +123,35 @@ def test_node_major_input_vs_oracle(code, batch, ld):
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard), "kernel %d" % k
 
 
+@pytest.mark.parametrize("kernel", [5, 8])
+def test_node_major_input_xcd_remap_early_termination(kernel):
+    """The node-major path at a batch that turns the XCD-aware
+    workgroup remap on (200 codewords: stride 256, grid 16, grid % 8 == 0)
+    with a pitch ld = 300 > batch and a ragged last group, early termination
+    and iterations used: soft output, hard decisions and iterations equal the
+    oracle's on coop (5) and coop3 (8)."""
+    torch = _torch()
+    t = load_table("dvbs2_r1_2")
+    batch, ld, iters = 200, 300, 25
+    llr = channel.awgn_i8_host(t.n, batch, seed=31, table=channel.i8_table(channel.sigma_from_ebn0(1.1, 0.5)))
+    ref_hard, ref_soft, ref_its = O.decode_i8(t, llr, iters, O.OMS, 1, early_term=True, return_soft=True,
+                                              threads=O.host_threads())
+    assert ref_its.min() < iters
+    nm = np.full((t.n, ld), -5, dtype=np.int8)
+    nm[:, :batch] = llr.T
+    dec = decoder("dvbs2_r1_2", kernel, max_batch=256)
+    d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+    d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
+    d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
+    dec.decode_i8_nm_device(torch.from_numpy(nm).cuda(), d_hard, iters, batch=batch,
+                            params=default_params(early_term=1), soft=d_soft, iters_used=d_its)
+    torch.cuda.synchronize()
+    assert dec.last_kernel == {5: "coop", 8: "coop3"}[kernel]
+    assert np.array_equal(d_its.cpu().numpy(), ref_its)
+    assert np.array_equal(d_soft.cpu().numpy(), ref_soft)
+    assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
+
+
 def test_config1_single_codeword_float_sweep():
     """BASELINE.json configs[0] shape on the GPU path: 802.11n N=648 r1/2, one
     codeword, 10 iterations, float min-sum, Eb/N0 0.5 .. 3.0 dB (SURVEY.md
