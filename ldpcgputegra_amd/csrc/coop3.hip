@@ -106,6 +106,9 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 // (LcPlan::ops) as byte offsets: 8 the line loaded, 9 the line written back
 // (from the group's V block), 10 the slot written with the load of LC_PUT
 // periods earlier, 11 the slot written back (from the line cache)
+#ifndef LDPC_C3_EARLY_PRE
+#define LDPC_C3_EARLY_PRE 1   // experiment switch: slab waves 1..5 issue the pre's LDS reads before the post
+#endif
 constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
 static_assert(W_LOP + 4 <= RECW, "line-op words");
 
@@ -1015,7 +1018,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs), then reads and runs its pre
                 if (fair) __builtin_amdgcn_s_setprio(P0);
-                if (sl.w != 0) {
+                if (LDPC_C3_EARLY_PRE && sl.w != 0) {
                     // no distance-2 reader outside slab wave 0: the pre's LDS
                     // reads are issued first and land under the post
                     sl.read_pre((s + 1) % NI, rcn, in);

@@ -216,9 +216,9 @@ int launch_ldsep(const LdsCode &lc, const ldpc_code *h, const float *llr, uint8_
     a.early = L.early;
     a.beta = L.beta;
     a.iters_used = L.iters_used;
+    const bool nms = L.algo == 1;
     const size_t shm = (size_t)EP_WAVES * a.vstride * 4;
     const dim3 grid((batch + EP_WAVES - 1) / EP_WAVES), block(64 * EP_WAVES);
-    const bool nms = L.algo == 1;
     switch (lc.ep_shape * 2 + (nms ? 1 : 0)) {
     case 0: hipLaunchKernelGGL((ldsep_decode<12, 4, false>), grid, block, shm, s, a); break;
     case 1: hipLaunchKernelGGL((ldsep_decode<12, 4, true>), grid, block, shm, s, a); break;

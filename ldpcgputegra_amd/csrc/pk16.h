@@ -122,7 +122,17 @@ LDPC_DEV uint32_t old_msg(uint32_t MA, const MsgTab &t, uint32_t m3 = 0x03000300
 
 // (a & m) | b as one v_bitop3_b32 (truth table 0xEA); written with | and &
 // the compiler builds an and + or3 tree: 1.5 instructions per flag, not 1
-LDPC_DEV uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) { return __builtin_amdgcn_bitop3_b32(a, m, b, 0xEA); }
+#ifndef LDPC_PK_ANDOR
+#define LDPC_PK_ANDOR 1   // experiment switch (tools/build_variant.sh): 0 = plain & and |
+#endif
+LDPC_DEV uint32_t and_or(uint32_t a, uint32_t m, uint32_t b)
+{
+#if LDPC_PK_ANDOR
+    return __builtin_amdgcn_bitop3_b32(a, m, b, 0xEA);
+#else
+    return (a & m) | b;
+#endif
+}
 // edge J's code (bit 0: c < 0, bit 1: got cst2) into MA, from the two half masks
 template <int J>
 LDPC_DEV uint32_t add_code(uint32_t MA, uint32_t sc, uint32_t neq)

@@ -2,7 +2,7 @@
 # Build an alternative libldpc_mi355x.so with one kernel source compiled with
 # extra defines, for kernel experiments on the GPU box (LDPC_MI355X_LIB=...):
 #   tools/build_variant.sh <name> [<src>.hip] -DLDPC_COOP2_R=4 ...
-#     -> build/variants/<name>/libldpc_mi355x.so   (<src> default coop2.hip)
+#     -> var/variants/<name>/libldpc_mi355x.so   (<src> default coop3.hip; var/ travels to the GPU box)
 # Run in the dev container after `make -C ldpcgputegra_amd/csrc` (reuses its objects).
 set -e
 cd "$(dirname "$0")/.."
@@ -14,7 +14,7 @@ if [[ "$1" == *.hip ]]; then
     shift
 fi
 base=${src%.hip}
-out=build/variants/$name
+out=var/variants/$name
 mkdir -p "$out"
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function"
 /opt/rocm/bin/hipcc $HIPFLAGS "$@" -c -o "$out/$base.o" ldpcgputegra_amd/csrc/$src
