@@ -107,7 +107,7 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 // (from the group's V block), 10 the slot written with the load of LC_PUT
 // periods earlier, 11 the slot written back (from the line cache)
 #ifndef LDPC_C3_EARLY_PRE
-#define LDPC_C3_EARLY_PRE 1   // experiment switch: slab waves 1..5 issue the pre's LDS reads before the post
+#define LDPC_C3_EARLY_PRE 0   // experiment switch: 1 = slab waves 1..5 issue the pre's LDS reads before the post (r04f A/B: 1.4 ms slower)
 #endif
 constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
 static_assert(W_LOP + 4 <= RECW, "line-op words");
