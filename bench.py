@@ -265,6 +265,8 @@ def bench_mixed(a, rank, world, local, torch, dist):
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    mx.kernel_time(reset=True)
+    mx.profile(True)   # HIP events around each code's decode launch (on its own stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -275,6 +277,8 @@ def bench_mixed(a, rank, world, local, torch, dist):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    kt = mx.kernel_time(reset=True)
+    mx.profile(False)
     h, it = hard.cpu().numpy(), its.cpu().numpy()
     per_rate, alg_bytes, be_tot, fe_tot, bits = [], 0.0, 0, 0, 0
     for c, code in enumerate(codes):
@@ -282,7 +286,9 @@ def bench_mixed(a, rank, world, local, torch, dist):
         e = h[sel][:, :code.k_info].sum(axis=1)          # all-zero codeword: every 1 is an error
         per_rate.append(dict(code=code.name, ebn0_db=MIXED_EBN0[code.name], frames=int(sel.sum()),
                              avg_iters=float(it[sel].mean()), ber=float(e.sum()) / (sel.sum() * code.k_info),
-                             fer=float((e > 0).mean())))
+                             fer=float((e > 0).mean()),
+                             kernel=mx.last_kernels()[c],
+                             kernel_ms=round(kt[c][0] / kt[c][1], 4) if kt[c][1] else None))
         alg_bytes += float((4.0 * code.e * it[sel] + 2.0 * N).sum())
         be_tot += int(e.sum())
         fe_tot += int((e > 0).sum())
@@ -311,7 +317,9 @@ def bench_mixed(a, rank, world, local, torch, dist):
             # whole-step rate (several kernels on concurrent streams): no single dominant launch;
             # traffic = HBM bytes per step over all its kernels (PMC, profiles/traffic.json)
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": hbm_peak_gbs(), "unit": "GB/s",
-                         "frac": round(achieved / hbm_peak_gbs(), 4), "traffic": None, "kernel_ms": None,
+                         "frac": round(achieved / hbm_peak_gbs(), 4), "traffic": None,
+                         # the longest per-rate decode launch (they run concurrently; per_rate has each)
+                         "kernel_ms": max((r["kernel_ms"] for r in per_rate if r["kernel_ms"]), default=None),
                          "algorithmic_bytes_per_step": alg_bytes},
             "cpu_baseline": None,
         }

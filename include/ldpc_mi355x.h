@@ -258,6 +258,10 @@ int ldpc_decode_i8_mixed_async(ldpc_mixed *mx, void *hip_stream, const int8_t *d
 /* Kernel family the last mixed decode ran for code `code_index` (numbering of
  * ldpc_ctx_last_kernel; 0 if that code had no codewords in any decode yet). */
 int ldpc_mixed_last_kernel(ldpc_mixed *mx, int code_index, int *kernel);
+/* Per-code decode-kernel timing (ldpc_ctx_profile / ldpc_ctx_kernel_time of
+ * the code's context): the decode launches only, not the gather / scatter. */
+int ldpc_mixed_profile(ldpc_mixed *mx, int enable);
+int ldpc_mixed_kernel_time(ldpc_mixed *mx, int code_index, double *total_ms, int *launches, int reset);
 
 /* DVB-S2 IRA encoder (codes built from an Annex-B table), as the
  * reference's GenericEncoder::encode (code/x86/CEncoder/GenericEncoder.cpp:38-78):

@@ -70,6 +70,8 @@ SIGNATURES = {
     "ldpc_mixed_destroy": (None, [P]),
     "ldpc_decode_i8_mixed_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params)]),
     "ldpc_mixed_last_kernel": (I, [P, I, C.POINTER(I)]),
+    "ldpc_mixed_profile": (I, [P, I]),
+    "ldpc_mixed_kernel_time": (I, [P, I, C.POINTER(C.c_double), C.POINTER(I), I]),
     "ldpc_dvbs2_encode": (I, [P, P, P, I]),
     "ldpc_awgn_sigma": (C.c_double, [C.c_double, C.c_double]),
     "ldpc_awgn_i8_table": (I, [C.c_double, I, I, P]),

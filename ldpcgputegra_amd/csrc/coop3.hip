@@ -109,6 +109,10 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 #ifndef LDPC_C3_EARLY_PRE
 #define LDPC_C3_EARLY_PRE 0   // experiment switch: 1 = slab waves 1..5 issue the pre's LDS reads before the post (r04f A/B: 1.4 ms slower)
 #endif
+#ifndef LDPC_C3_MORDER
+#define LDPC_C3_MORDER 0      // memory wave's period order: 0 = slot writes, gathers, loads, writebacks, stores,
+                              // vmcnt(42); 1 = loads, gathers, slot writes, writebacks, stores, vmcnt(36)
+#endif
 constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
 static_assert(W_LOP + 4 <= RECW, "line-op words");
 
@@ -876,6 +880,15 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 if (STAMP) tx = stampL();
                 uint32_t gix[WS];
                 uint4 wbd[WS], std_[WS];
+                if constexpr (LDPC_C3_MORDER == 1) {
+                    // the line loads first (their addresses are in VGPRs): the
+                    // memory wave's LDS burst then starts after the slab waves'
+                    // chain-input reads of the period start were served
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                        constexpr int w = decltype(wc)::value;
+                        pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w].x + lq), 0, 0));
+                    });
+                }
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
                     gix[w] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
@@ -885,18 +898,27 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     wbd[w] = *(const uint4 *)(lcb + lop[w].w + lq);
                     std_[w] = sm.mst[(p - 2) & 1][w][kl][qp];
                 });
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
-                    constexpr int w = decltype(wc)::value;
-                    *(uint4 *)(lcb + lop[w].z + lq) = pend[(s + 1) % NPD][w];
-                });
+                if constexpr (LDPC_C3_MORDER == 0) {
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
+                        constexpr int w = decltype(wc)::value;
+                        *(uint4 *)(lcb + lop[w].z + lq) = pend[(s + 1) % NPD][w];
+                    });
+                }
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
                     if (lane < 40) dma16_buf(vr, (gix[w] << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
                 });
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
-                    constexpr int w = decltype(wc)::value;
-                    pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w].x + lq), 0, 0));
-                });
+                if constexpr (LDPC_C3_MORDER == 0) {
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                        constexpr int w = decltype(wc)::value;
+                        pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w].x + lq), 0, 0));
+                    });
+                } else {
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
+                        constexpr int w = decltype(wc)::value;
+                        *(uint4 *)(lcb + lop[w].z + lq) = pend[(s + 1) % NPD][w];
+                    });
+                }
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // writebacks of period p
                     constexpr int w = decltype(wc)::value;
                     rbuf_store_v4(__builtin_bit_cast(i32x4, wbd[w]), vr, (int)(lop[w].y + lq), 0, 0);
@@ -912,7 +934,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     lop[w] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][W_LOP];
                 });
                 if (STAMP) sP[1] += stampL() - tx;
-                asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+                if constexpr (LDPC_C3_MORDER == 1)
+                    asm volatile("s_waitcnt vmcnt(36)" ::: "memory");   // the gathers of p-1: 12 + 24 ops after them
+                else
+                    asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
                 if (STAMP) sA += stampL() - tx;
                 __syncthreads();
                 uS = (uS + 1 == a.nw) ? 0 : uS + 1;
@@ -1018,7 +1043,13 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs), then reads and runs its pre
                 if (fair) __builtin_amdgcn_s_setprio(P0);
-                if (LDPC_C3_EARLY_PRE && sl.w != 0) {
+                if (LDPC_C3_EARLY_PRE == 2 && sl.w != 0) {
+                    // the chain inputs first (the post waits for them alone:
+                    // LDS returns in order), then the pre's reads under the post
+                    const uint32_t xr = sl.read_x(p - 1, sp);
+                    sl.read_pre((s + 1) % NI, rcn, in);
+                    sl.template post<false, ET, MP1>(p - 1, xr, sp);
+                } else if (LDPC_C3_EARLY_PRE == 1 && sl.w != 0) {
                     // no distance-2 reader outside slab wave 0: the pre's LDS
                     // reads are issued first and land under the post
                     sl.read_pre((s + 1) % NI, rcn, in);
@@ -1026,11 +1057,15 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     sl.template post<false, ET, MP1>(p - 1, xr, sp);
                 } else {
                     const uint32_t xr = sl.read_x(p - 1, sp);
+                    if (STAMP) {   // the chain inputs' arrival (the empty asm makes the wave wait for them)
+                        asm volatile("" ::"v"(xr));
+                        t2 = stampL();
+                    }
                     sl.template post<false, ET, MP1>(p - 1, xr, sp);
                     sl.read_pre((s + 1) % NI, rcn, in);
                 }
                 rcn = sl.read_rec(p + 2);
-                if (STAMP) t1 = t2 = stampL();
+                if (STAMP) t1 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(P1);
                 sl.template pre<false, ET, MP2>(p + 1, in, sn);
                 if (STAMP) t3 = stampL();
@@ -1055,10 +1090,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             if (STAMP) {
                 const unsigned long long t5 = stampL();
                 sA += t5 - tx;
-                if (fast) {
-                    sP[0] += t1 - tx;
-                    sP[1] += t2 - t1;
-                    sP[2] += t3 - t2;
+                if (fast) {   // x wait, post (+ the pre's read issue), pre
+                    sP[0] += (t2 ? t2 : t1) - tx;
+                    sP[1] += t1 - (t2 ? t2 : t1);
+                    sP[2] += t3 - t1;
                 }
             }
             __syncthreads();
@@ -1130,9 +1165,11 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
         const double *x = &v[w * 8];
         if (w == CHW)
             fprintf(stderr, "  chain %d: busy %.0f steps %.0f\n", w, x[0], x[1]);
-        else
-            fprintf(stderr, "  slab %d: busy %.0f | vmcnt %.0f %s %.0f %s %.0f mem %.0f\n", w, x[0], x[1],
-                    w == 0 ? "post" : "pre", x[2], w == 0 ? "pre" : "post", x[3], x[0] - x[1] - x[2] - x[3]);
+        else if (w == WS + 1)
+            fprintf(stderr, "  memory %d: busy %.0f | issue %.0f vmcnt %.0f\n", w, x[0], x[2], x[0] - x[2]);
+        else   // fast periods: x-input wait, post, pre; rest = guarded periods' share and the stamps
+            fprintf(stderr, "  slab %d: busy %.0f | x wait %.0f post %.0f pre %.0f rest %.0f\n", w, x[0], x[1], x[2],
+                    x[3], x[0] - x[1] - x[2] - x[3]);
     }
 }
 

@@ -199,3 +199,20 @@ extern "C" int ldpc_mixed_last_kernel(ldpc_mixed *mx, int code_index, int *kerne
         return ldpc_set_error(LDPC_EINVAL, "mixed last kernel: bad arguments");
     return ldpc_ctx_last_kernel(mx->ctx[code_index], kernel);
 }
+
+extern "C" int ldpc_mixed_profile(ldpc_mixed *mx, int enable)
+{
+    if (!mx) return ldpc_set_error(LDPC_EINVAL, "mixed profile: NULL");
+    for (auto *c : mx->ctx) {
+        const int rc = ldpc_ctx_profile(c, enable);
+        if (rc != LDPC_OK) return rc;
+    }
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_mixed_kernel_time(ldpc_mixed *mx, int code_index, double *total_ms, int *launches, int reset)
+{
+    if (!mx || code_index < 0 || code_index >= (int)mx->ctx.size())
+        return ldpc_set_error(LDPC_EINVAL, "mixed kernel time: bad arguments");
+    return ldpc_ctx_kernel_time(mx->ctx[code_index], total_ms, launches, reset);
+}

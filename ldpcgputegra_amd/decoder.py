@@ -245,6 +245,19 @@ class MixedDecoder:
             out.append(Decoder.KERNEL_NAMES.get(k.value, str(k.value)))
         return out
 
+    def profile(self, enable=True):
+        """Record each code's decode-kernel launches with HIP events."""
+        _lib.check(_lib.lib().ldpc_mixed_profile(self._mx, int(bool(enable))))
+
+    def kernel_time(self, reset=True):
+        """[(total_ms, launches)] per code since the last reset (profile() on)."""
+        out = []
+        for c in range(len(self.codes)):
+            ms, n = C.c_double(), C.c_int()
+            _lib.check(_lib.lib().ldpc_mixed_kernel_time(self._mx, c, C.byref(ms), C.byref(n), int(reset)))
+            out.append((ms.value, n.value))
+        return out
+
     def close(self):
         if getattr(self, "_mx", None) is not None and _lib._lib is not None:
             _lib._lib.ldpc_mixed_destroy(self._mx)
