@@ -80,8 +80,9 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
 
 // ---- linecache.cpp: coop3's LDS line cache (info rows as 128-B lines) ----
 constexpr int LC_GAP = 10;    // accesses of a line >= LC_GAP periods apart: separate residencies
-constexpr int LC_LEAD = 4;   // a line is loaded (into VGPRs) >= 4 periods before its first access
-constexpr int LC_PUT = 3;    // ... and written to its slot 3 periods after its load
+constexpr int LC_LEAD = 3;   // a line is loaded (into VGPRs) >= 3 periods before its first access
+constexpr int LC_PUT = 2;    // ... and written to its slot 2 periods after its load (coop3: loads first in a
+                             // period, vmcnt(36) at its end completes those of the period before)
 constexpr int LC_OPS = 48;   // line loads / writebacks per period: 6 slab waves x 8 lane groups
 struct LcPlan {
     int slots = 0;                 // LDS line slots used, the sink (slot 0) included

@@ -110,7 +110,7 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 #define LDPC_C3_EARLY_PRE 0   // experiment switch: 1 = slab waves 1..5 issue the pre's LDS reads before the post (r04f A/B: 1.4 ms slower)
 #endif
 #ifndef LDPC_C3_MORDER
-#define LDPC_C3_MORDER 0      // memory wave's period order: 0 = slot writes, gathers, loads, writebacks, stores,
+#define LDPC_C3_MORDER 1      // memory wave's period order: 0 = slot writes, gathers, loads, writebacks, stores,
                               // vmcnt(42); 1 = loads, gathers, slot writes, writebacks, stores, vmcnt(36)
 #endif
 constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
@@ -560,6 +560,11 @@ LDPC_DEV uint32_t high_bits16(uint4 x)   // byte high bits -> 16-bit codeword ma
     auto c4 = [](uint32_t v) { return ((v >> 7) & 1u) | ((v >> 14) & 2u) | ((v >> 21) & 4u) | ((v >> 28) & 8u); };
     return c4(x.x) | c4(x.y) << 4 | c4(x.z) << 8 | c4(x.w) << 12;
 }
+// the hard-bit word of a V row piece (16 codewords): bit j = (V_j > 0)
+LDPC_DEV uint32_t row_hbits(uint4 y)
+{
+    return high_bits16(make_uint4(pos_bits(y.x), pos_bits(y.y), pos_bits(y.z), pos_bits(y.w)));
+}
 // Wave CHW: the chain; the others: slab waves (slab index w: slots 8w .. 8w+7).
 // ET: in-kernel early termination -- the decode runs one iteration per
 // segment (pipeline drained and the line cache written back at its end), then
@@ -597,6 +602,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         __syncthreads();
         if (et_sh[0] == 0) return;   // padding columns only
     }
+    // ET (slab waves): sP[3] = segment prologues, sD = epilogues + syndromes;
+    // elapsed from the first segment's start, G x segments periods
+    unsigned long long sA = 0, sP[4] = {0, 0, 0, 0}, sD = 0, t0 = 0, tx = 0, tseg = 0;
+    int nseg = 1;
     // after iteration `it` (ET): syndrome and decision -- every thread,
     // uniform result (true: decode another iteration).  Codewords converged
     // earlier are frozen by the slab waves (Slab3::fm: their V rows are
@@ -647,7 +656,18 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         __syncthreads();
         return (fail & live) == live;
     };
+    // stamps (chain wave): sP[1] cycles of round 0 (from the entry), sP[2]
+    // cycles of full syndromes, sD their count
+    auto et_stamp = [&](int k, unsigned long long &t) {
+        if (STAMP && wave == CHW) {
+            const unsigned long long u = stamp3();
+            if (k > 0) sP[k] += u - t;
+            t = u;
+        }
+    };
     auto et_after = [&](int it) -> bool {
+        unsigned long long te = 0;
+        et_stamp(0, te);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the iteration's stores, writebacks and table DMAs
         __syncthreads();
         const uint32_t live = et_sh[0];
@@ -660,25 +680,28 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                                            : (int)((threadIdx.x + (size_t)it * NT * 5) % (size_t)a.m);
             const uint32_t x = high_bits16(et_check(c)) & live;
             et_note(x, c);
-            if (et_round(x, live)) goto et_done;
+            const bool settled = et_round(x, live);
+            et_stamp(1, te);
+            if (settled) goto et_done;
         }
         {
+            if (STAMP && wave == CHW) sD++;
             // the full syndrome: every variable's hard bits staged in LDS (the
             // pipeline's LDS is idle between segments; the launch checks n
             // fits), then the checks, 8 per thread and round with an exit
             // test after each; loads unconditional (clamped index) so a
             // round's loads are in flight together
             uint16_t *hb = reinterpret_cast<uint16_t *>(&sm);
-            auto hbits = [](uint4 y) {
-                return (uint16_t)high_bits16(make_uint4(pos_bits(y.x), pos_bits(y.y), pos_bits(y.z), pos_bits(y.w)));
-            };
-            for (int r0 = 0; r0 < a.n; r0 += NT * 8) {
-                uint4 y[8];
+            // HB rows per thread in flight at once: the staging of 1 MB is
+            // latency-bound (16 rounds of 8 took ~124k cycles)
+            constexpr int HB = 16;
+            for (int r0 = 0; r0 < a.n; r0 += NT * HB) {
+                uint4 y[HB];
 #pragma unroll
-                for (int i = 0; i < 8; i++) y[i] = *et_row((uint32_t)min(r0 + i * NT + (int)threadIdx.x, a.n - 1));
+                for (int i = 0; i < HB; i++) y[i] = *et_row((uint32_t)min(r0 + i * NT + (int)threadIdx.x, a.n - 1));
 #pragma unroll
-                for (int i = 0; i < 8; i++)
-                    if (r0 + i * NT + (int)threadIdx.x < a.n) hb[r0 + i * NT + threadIdx.x] = hbits(y[i]);
+                for (int i = 0; i < HB; i++)
+                    if (r0 + i * NT + (int)threadIdx.x < a.n) hb[r0 + i * NT + threadIdx.x] = (uint16_t)row_hbits(y[i]);
             }
             __syncthreads();
             bool done = false;
@@ -715,6 +738,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 }
                 et_round(f, live);
             }
+            et_stamp(2, te);
         }
     et_done:
         const uint32_t fresh = live & ~et_sh[1];   // converged after this iteration
@@ -729,7 +753,6 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     };
     // stamps (diagnostic build): per wave 8 words: busy, phases 1..3 (slab:
     // vmcnt, first and second half), -, elapsed, -, G
-    unsigned long long sA = 0, sP[4] = {0, 0, 0, 0}, sD = 0, t0 = 0, tx = 0;
     auto write_stamps = [&]() {
         if (STAMP && lane == 0) {
             unsigned long long *o = a.stamps + ((size_t)id * (WS + 2) + wave) * 8;
@@ -737,7 +760,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             for (int i = 0; i < 4; i++) o[1 + i] = sP[i];
             o[5] = stamp3() - t0;
             o[6] = sD;
-            o[7] = (unsigned long long)G;
+            o[7] = (unsigned long long)G * (unsigned long long)nseg;
         }
     };
 
@@ -767,7 +790,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             __syncthreads();   // prologue 1: tables of windows 0 .. KAHEAD-1 and the resident lines in LDS
             __syncthreads();   // prologue 1b: the memory wave's first gathers landed
             __syncthreads();   // prologue 2: constants of window 0 in LDS
-            if (STAMP) t0 = stamp3();
+            if (STAMP && it == 0) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
                 if (STAMP) tx = stamp3();
                 if (p < G && cl) chain_window3<WS, R, 0, NB, NMS>(sm, p & 1, c, w4);
@@ -780,6 +803,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             }
             __syncthreads();   // epilogue: the slab waves' line writebacks read the cache
             if (!ET || !et_after(it)) break;
+            nseg++;
         }
         write_stamps();
         return;
@@ -844,7 +868,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();   // prologue 1b: the first windows' gathers landed
             __syncthreads();   // prologue 2
-            if (STAMP) t0 = stamp3();
+            if (STAMP && it == 0) t0 = stamp3();
             constexpr int NPD = LC_PUT + 1;
             uint4 pend[NPD][WS];   // line loads of periods p-LC_PUT .. p (written to their slots LC_PUT periods on)
 #pragma unroll
@@ -880,44 +904,58 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 if (STAMP) tx = stampL();
                 uint32_t gix[WS];
                 uint4 wbd[WS], std_[WS];
-                if constexpr (LDPC_C3_MORDER == 1) {
+                auto loads = [&]() __attribute__((always_inline)) {   // line loads of period p
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                        constexpr int w = decltype(wc)::value;
+                        pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w].x + lq), 0, 0));
+                    });
+                };
+                auto read_gix = [&]() __attribute__((always_inline)) {   // gather indices of window p+1+R
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                        constexpr int w = decltype(wc)::value;
+                        gix[w] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
+                    });
+                };
+                auto read_out = [&]() __attribute__((always_inline)) {   // writeback and store data
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                        constexpr int w = decltype(wc)::value;
+                        wbd[w] = *(const uint4 *)(lcb + lop[w].w + lq);
+                        std_[w] = sm.mst[(p - 2) & 1][w][kl][qp];
+                    });
+                };
+                auto slot_writes = [&]() __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                        constexpr int w = decltype(wc)::value;
+                        *(uint4 *)(lcb + lop[w].z + lq) = pend[(s + 1) % NPD][w];
+                    });
+                };
+                auto gathers = [&]() __attribute__((always_inline)) {
+                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                        constexpr int w = decltype(wc)::value;
+                        if (lane < 40) dma16_buf(vr, (gix[w] << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
+                    });
+                };
+                if constexpr (LDPC_C3_MORDER == 0) {
+                    read_gix();
+                    read_out();
+                    slot_writes();
+                    gathers();
+                    loads();
+                } else if constexpr (LDPC_C3_MORDER == 1) {
                     // the line loads first (their addresses are in VGPRs): the
-                    // memory wave's LDS burst then starts after the slab waves'
-                    // chain-input reads of the period start were served
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
-                        constexpr int w = decltype(wc)::value;
-                        pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w].x + lq), 0, 0));
-                    });
-                }
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
-                    constexpr int w = decltype(wc)::value;
-                    gix[w] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
-                });
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
-                    constexpr int w = decltype(wc)::value;
-                    wbd[w] = *(const uint4 *)(lcb + lop[w].w + lq);
-                    std_[w] = sm.mst[(p - 2) & 1][w][kl][qp];
-                });
-                if constexpr (LDPC_C3_MORDER == 0) {
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
-                        constexpr int w = decltype(wc)::value;
-                        *(uint4 *)(lcb + lop[w].z + lq) = pend[(s + 1) % NPD][w];
-                    });
-                }
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
-                    constexpr int w = decltype(wc)::value;
-                    if (lane < 40) dma16_buf(vr, (gix[w] << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
-                });
-                if constexpr (LDPC_C3_MORDER == 0) {
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
-                        constexpr int w = decltype(wc)::value;
-                        pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w].x + lq), 0, 0));
-                    });
-                } else {
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
-                        constexpr int w = decltype(wc)::value;
-                        *(uint4 *)(lcb + lop[w].z + lq) = pend[(s + 1) % NPD][w];
-                    });
+                    // memory wave's LDS burst starts after the slab waves'
+                    // chain-input reads of the period start
+                    loads();
+                    read_gix();
+                    read_out();
+                    gathers();
+                    slot_writes();
+                } else {   // as 1, the slot writes (freeing a pend set) before the output reads
+                    loads();
+                    read_gix();
+                    gathers();
+                    slot_writes();
+                    read_out();
                 }
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // writebacks of period p
                     constexpr int w = decltype(wc)::value;
@@ -934,7 +972,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     lop[w] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][W_LOP];
                 });
                 if (STAMP) sP[1] += stampL() - tx;
-                if constexpr (LDPC_C3_MORDER == 1)
+                if constexpr (LDPC_C3_MORDER != 0)
                     asm volatile("s_waitcnt vmcnt(36)" ::: "memory");   // the gathers of p-1: 12 + 24 ops after them
                 else
                     asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
@@ -957,6 +995,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             });
             __syncthreads();   // epilogue (the slab waves write the resident dirty lines back)
             if (!ET || !et_after(it)) break;
+            nseg++;
         }
         write_stamps();
         return;
@@ -989,12 +1028,25 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     (uint32_t)((32 + kl) * 16 + 4 * (q >> 1))};
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
-        // line cache prologue: the lines resident at a segment start (LcPlan::pro)
-        for (int i = st_id; i < 8 * a.n_pro; i += NSL) {
-            const uint32_t pw = a.lc_pro[i >> 3];
-            const uint32_t piece = (uint32_t)(i & 7) * 16u;
-            *(uint4 *)((char *)&sm.lc[0][0] + (pw >> 16) * 128u + piece) =
-                *(const uint4 *)(Vg + (size_t)(pw & 0xFFFFu) * 128 + piece);
+        if (STAMP) tseg = stamp3();
+        // line cache prologue: the lines resident at a segment start
+        // (LcPlan::pro), PB pieces per thread in flight at once (ET runs it
+        // every iteration: one HBM round trip per batch, not per piece)
+        {
+            constexpr int PB = 12;
+            for (int i0 = st_id; i0 < 8 * a.n_pro; i0 += PB * NSL) {
+                uint32_t pw[PB];
+                uint4 d[PB];
+#pragma unroll
+                for (int j = 0; j < PB; j++) pw[j] = a.lc_pro[min(i0 + j * NSL, 8 * a.n_pro - 1) >> 3];
+#pragma unroll
+                for (int j = 0; j < PB; j++)
+                    d[j] = *(const uint4 *)(Vg + (size_t)(pw[j] & 0xFFFFu) * 128 + (uint32_t)((i0 + j * NSL) & 7) * 16u);
+#pragma unroll
+                for (int j = 0; j < PB; j++)
+                    if (i0 + j * NSL < 8 * a.n_pro)
+                        *(uint4 *)((char *)&sm.lc[0][0] + (pw[j] >> 16) * 128u + (uint32_t)((i0 + j * NSL) & 7) * 16u) = d[j];
+            }
         }
         __syncthreads();   // prologue 1: tables and resident lines in LDS
         if constexpr (ET) {   // codewords 2q (low half) and 2q+1 (high half) of this lane: converged?
@@ -1013,7 +1065,11 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         else
             sl.template pre<false, ET>(0, in, st[0]);
         __syncthreads();   // prologue 2
-        if (STAMP) t0 = stamp3();
+        if (STAMP) {
+            const unsigned long long t = stamp3();
+            if (it == 0) t0 = t;
+            sP[3] += t - tseg;
+        }
         int uA = a.nw - 1;   // local index of window p-1 (post)
         int uB = 1 % a.nw;   // local index of window p+1 (pre)
         // Period p: post of window p-1 (state st[(p-1) % NS], x inputs from the
@@ -1118,14 +1174,30 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 period(std::integral_constant<int, (1 + decltype(jc)::value) % U>{}, T{}, p + decltype(jc)::value);
         });
         // line cache epilogue: the dirty lines still resident (LcPlan::epi)
+        if (STAMP) tseg = stamp3();
         __syncthreads();
-        for (int i = st_id; i < 8 * a.n_epi; i += NSL) {
-            const uint32_t pw = a.lc_epi[i >> 3];
-            const uint32_t piece = (uint32_t)(i & 7) * 16u;
-            *(uint4 *)(Vg + (size_t)(pw & 0xFFFFu) * 128 + piece) =
-                *(const uint4 *)((const char *)&sm.lc[0][0] + (pw >> 16) * 128u + piece);
+        {
+            constexpr int PB = 8;
+            for (int i0 = st_id; i0 < 8 * a.n_epi; i0 += PB * NSL) {
+                uint32_t pw[PB];
+                uint4 d[PB];
+#pragma unroll
+                for (int j = 0; j < PB; j++) pw[j] = a.lc_epi[min(i0 + j * NSL, 8 * a.n_epi - 1) >> 3];
+#pragma unroll
+                for (int j = 0; j < PB; j++)
+                    d[j] = *(const uint4 *)((const char *)&sm.lc[0][0] + (pw[j] >> 16) * 128u + (uint32_t)((i0 + j * NSL) & 7) * 16u);
+#pragma unroll
+                for (int j = 0; j < PB; j++)
+                    if (i0 + j * NSL < 8 * a.n_epi) {
+                        const uint32_t row = (pw[j] & 0xFFFFu) * 8u + (uint32_t)((i0 + j * NSL) & 7);
+                        *(uint4 *)(Vg + (size_t)row * 16u) = d[j];
+                    }
+            }
         }
-        if (!ET || !et_after(it)) break;
+        const bool more = ET && et_after(it);
+        if (STAMP) sD += stamp3() - tseg;
+        if (!more) break;
+        nseg++;
     }
     write_stamps();
 }
@@ -1157,19 +1229,21 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
             const unsigned long long *o = &h[((size_t)b * nwaves + w) * 8];
             const double G = o[7] ? (double)o[7] : 1.0;
             for (int i = 0; i < 6; i++) v[w * 8 + i] += o[i] / G / grid;
-            v[w * 8 + 6] += ((o[6] >> 16) & 0xffff) / G / grid;
-            v[w * 8 + 7] += (o[6] & 0xffff) / G / grid;
+            v[w * 8 + 6] += o[6] / G / grid;
+            v[w * 8 + 7] += G / grid;
         }
-    fprintf(stderr, "coop3 stamps [cycles per period]: elapsed %.0f\n", v[5]);
+    fprintf(stderr, "coop3 stamps [cycles per period]: elapsed %.0f (%.0f periods per workgroup)\n", v[5], v[7]);
     for (int w = 0; w < nwaves; w++) {
         const double *x = &v[w * 8];
         if (w == CHW)
-            fprintf(stderr, "  chain %d: busy %.0f steps %.0f\n", w, x[0], x[1]);
+            fprintf(stderr, "  chain %d: busy %.0f steps %.0f | ET round 0 %.1f, full syndromes %.1f (%.4f per period)\n",
+                    w, x[0], x[1], x[2], x[3], x[6]);
         else if (w == WS + 1)
             fprintf(stderr, "  memory %d: busy %.0f | issue %.0f vmcnt %.0f\n", w, x[0], x[2], x[0] - x[2]);
         else   // fast periods: x-input wait, post, pre; rest = guarded periods' share and the stamps
-            fprintf(stderr, "  slab %d: busy %.0f | x wait %.0f post %.0f pre %.0f rest %.0f\n", w, x[0], x[1], x[2],
-                    x[3], x[0] - x[1] - x[2] - x[3]);
+            fprintf(stderr, "  slab %d: busy %.0f | x wait %.0f post %.0f pre %.0f rest %.0f | ET segment prologue %.1f "
+                            "epilogue + syndrome %.1f\n", w, x[0], x[1], x[2], x[3], x[0] - x[1] - x[2] - x[3], x[4],
+                    x[6]);
     }
 }
 
@@ -1409,24 +1483,27 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 0 none, 1 static (second waves), 2 fair by phase
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups
-    if (et) {
-        if (nms)
-            hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 8), 0, s, a);
-        else
-            hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-    if (nms) {
-        hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-    const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0;
+    const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0 && !nms;
     if (stamped) {
         const size_t bytes = (size_t)grid * 8 * 8 * sizeof(unsigned long long);
         if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
-    const int rc = launch_wsr<6, 2>(a, grid, stamped, s);
+    int rc;
+    if (et) {
+        if (nms)
+            hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 8), 0, s, a);
+        else if (stamped)
+            hipLaunchKernelGGL((coop3_decode<6, 2, true, true>), dim3(grid), dim3(64 * 8), 0, s, a);
+        else
+            hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
+        rc = hipGetLastError() == hipSuccess ? 0 : -1;
+    } else if (nms) {
+        hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    } else {
+        rc = launch_wsr<6, 2>(a, grid, stamped, s);
+    }
     if (stamped) {
         if (rc == 0) report_stamps3<6>(a.stamps, grid, s);
         (void)hipFree(a.stamps);

@@ -1,20 +1,24 @@
 #!/usr/bin/env python3
-"""Build-time guard for coop3's hand-counted `s_waitcnt vmcnt(42)`.
+"""Build-time guard for coop3's hand-counted `s_waitcnt vmcnt(36)`.
 
 coop3's memory wave (csrc/coop3.hip, `mperiod`) issues, per period, for each of
-the WS = 6 slab-wave sets: one LDS-DMA gather (`buffer_load_dwordx4 ... lds`,
-inline asm the compiler does not count), one line load, one line writeback and
-one store -- 4 * WS = 24 vector-memory instructions -- and closes the period
-with vmcnt(24 + 3 * WS = 42): everything up to the previous period's gathers
-has landed.  That count is only right while the compiler emits exactly those
-24 instructions per period (no split, no extra load, no scratch spill).  This
+the WS = 6 slab-wave sets, in this order: one line load, one LDS-DMA gather
+(`buffer_load_dwordx4 ... lds`, inline asm the compiler does not count), one
+line writeback and one store -- 4 * WS = 24 vector-memory instructions -- and
+closes the period with vmcnt(24 + 2 * WS = 36) right before its barrier:
+everything up to the previous period's gathers (and so its line loads) has
+landed.  That count is only right while the compiler emits exactly those 24
+instructions per period (no split, no extra load, no scratch spill).  This
 script disassembles the built coop3 kernels and checks it: every straight-line
-region between two consecutive `s_waitcnt vmcnt(42)` (no scalar / VCC branch
-inside: those are the guarded first / last periods) must hold exactly
---ops vector-memory instructions, at least --min-regions such regions must
-exist per kernel, and no coop3 kernel may touch scratch.
+region between two consecutive period-closing waits (`s_waitcnt vmcnt(36)`
+followed by the `s_barrier` with no vector-memory instruction between; no
+scalar / VCC branch inside the region: those are the guarded first / last
+periods) must hold exactly --ops vector-memory instructions, at least
+--min-regions such regions must exist per kernel, and no coop3 kernel may touch
+scratch.  (The compiler's own waits for the line loads it tracks are stricter
+than needed and not period boundaries.)
 
-usage: check_vmcnt.py [--ops 24] [--vmcnt 42] <coop3.o | libldpc_mi355x.so | file.s>
+usage: check_vmcnt.py [--ops 24] [--vmcnt 36] <coop3.o | libldpc_mi355x.so | file.s>
 exit 0 = ok, 1 = mismatch (the message names the kernel and region).
 """
 import argparse
@@ -66,17 +70,35 @@ def functions(isa):
     return funcs
 
 
-def check(isa, ops, vmcnt, min_regions=3, pattern="coop3_decode"):
-    """List of error strings (empty = ok) and the number of regions checked."""
+def closes_period(lines, i, reach=8):
+    """The wait at line i is followed by an s_barrier within `reach` lines,
+    with no vector-memory instruction or branch before it."""
+    for l in lines[i + 1:i + 1 + reach]:
+        if re.match(r"^\s*s_barrier\b", l):
+            return True
+        if VMEM.match(l) or BRANCH.match(l):
+            return False
+    return False
+
+
+ET_NAME = re.compile(r"coop3_decodeILi\d+ELi\d+ELb[01]ELb1E")
+
+
+def check(isa, ops, vmcnt, min_regions=1, pattern="coop3_decode", et_ops=24, et_vmcnt=36):
+    """List of error strings (empty = ok) and the number of regions checked.
+    Early-termination kernels (template flag ET) are checked against
+    et_ops / et_vmcnt (the same counts today)."""
     errs, checked = [], 0
-    wait = re.compile(r"^\s*s_waitcnt\s+.*vmcnt\(%d\)" % vmcnt)
     kernels = {k: v for k, v in functions(isa).items() if pattern in k}
     if not kernels:
         return ["no %s kernel in the disassembly" % pattern], 0
+    base_ops, base_vmcnt = ops, vmcnt
     for name, lines in kernels.items():
+        ops, vmcnt = (et_ops, et_vmcnt) if ET_NAME.search(name) else (base_ops, base_vmcnt)
+        wait = re.compile(r"^\s*s_waitcnt\s+.*vmcnt\(%d\)" % vmcnt)
         if any(re.match(r"^\s*scratch_", l) for l in lines):
             errs.append("%s: scratch access (a spill adds vector-memory ops the vmcnt does not count)" % name)
-        marks = [i for i, l in enumerate(lines) if wait.match(l)]
+        marks = [i for i, l in enumerate(lines) if wait.match(l) and closes_period(lines, i)]
         if not marks:
             errs.append("%s: no s_waitcnt vmcnt(%d)" % (name, vmcnt))
             continue
@@ -101,15 +123,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
     ap.add_argument("--ops", type=int, default=24, help="vector-memory ops per memory-wave period (4 * WS)")
-    ap.add_argument("--vmcnt", type=int, default=42, help="the period's closing wait (4 * WS + 3 * WS)")
-    ap.add_argument("--min-regions", type=int, default=3)
+    ap.add_argument("--vmcnt", type=int, default=36, help="the period's closing wait (4 * WS + 2 * WS)")
+    ap.add_argument("--et-ops", type=int, default=24, help="ET kernels' vector-memory ops per period")
+    ap.add_argument("--et-vmcnt", type=int, default=36, help="ET kernels' period-closing wait")
+    ap.add_argument("--min-regions", type=int, default=1)
     a = ap.parse_args()
-    errs, n = check(disassemble(a.path), a.ops, a.vmcnt, a.min_regions)
+    errs, n = check(disassemble(a.path), a.ops, a.vmcnt, a.min_regions, et_ops=a.et_ops, et_vmcnt=a.et_vmcnt)
     if errs:
         for e in errs:
             print("check_vmcnt: " + e, file=sys.stderr)
         return 1
-    print("check_vmcnt: ok (%d memory-wave periods of %d vector-memory ops, vmcnt(%d))" % (n, a.ops, a.vmcnt))
+    print("check_vmcnt: ok (%d memory-wave periods of %d / %d vector-memory ops, vmcnt(%d) / vmcnt(%d) with ET)"
+          % (n, a.ops, a.et_ops, a.vmcnt, a.et_vmcnt))
     return 0
 
 

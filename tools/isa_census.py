@@ -48,7 +48,7 @@ def coop3_census(funcs, kernel="coop3_decodeILi6ELi2ELb0ELb0ELb0E"):
     """One steady period of coop3 (DVB-S2 r1/2, WS = 6): the slab waves' fast
     period split at its branches (the shared prefix, the post variants for
     slab wave 0 / the others, the pre), a memory-wave period (between two
-    vmcnt(42)) and a chain block of 8 steps; VALU also as lane-ops per
+    period-closing vmcnt waits) and a chain block of 8 steps; VALU also as lane-ops per
     check x codeword (a slab lane = one check x 2 codewords; the memory and
     chain waves serve a window's 48 checks x 16 codewords)."""
     name = next(k for k in funcs if kernel in k)
@@ -69,7 +69,7 @@ def coop3_census(funcs, kernel="coop3_decodeILi6ELi2ELb0ELb0ELb0E"):
         c = collections.Counter(classify(m) for m in mn[x + 1:y])
         parts.append(dict(lines=[x, y], valu=c["valu"], salu=c["salu"], lds=c["lds"], nop=c["nop"]))
     out["slab_fast_period_blocks"] = parts
-    w = [i for i, l in enumerate(L) if "vmcnt(42)" in l]
+    w = [i for i, l in enumerate(L) if "vmcnt(" in l and check_vmcnt.closes_period(L, i)]
     for x, y in zip(w, w[1:]):
         if not any(mn[i].startswith(("s_cbranch_scc", "s_cbranch_vcc", "s_branch")) for i in range(x + 1, y)):
             c = collections.Counter(classify(m) for m in mn[x + 1:y])
@@ -96,7 +96,7 @@ def main():
     funcs = check_vmcnt.functions(check_vmcnt.disassemble(a.path))
     if a.coop3:
         import json
-        print(json.dumps(coop3_census(funcs), indent=1))
+        print(json.dumps(coop3_census(funcs, a.kernel), indent=1))
         return
     for name, lines in funcs.items():
         if a.kernel not in name:
