@@ -113,6 +113,16 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 #define LDPC_C3_MORDER 1      // memory wave's period order: 0 = slot writes, gathers, loads, writebacks, stores,
                               // vmcnt(42); 1 = loads, gathers, slot writes, writebacks, stores, vmcnt(36)
 #endif
+#ifndef LDPC_C3_MSLEEP
+#define LDPC_C3_MSLEEP 4      // memory wave: s_sleep (x 64 cycles) after its line loads, before its LDS burst
+#endif
+#ifndef LDPC_C3_BPRIO
+#define LDPC_C3_BPRIO 0
+#endif
+#ifndef LDPC_C3_SWROT
+#define LDPC_C3_SWROT 3       // slab index = (the wave's slab position + SWROT) % WS: slab 0 (the distance-2
+                              // writers and readers) on the second wave of a SIMD (A/B: -0.8 %)
+#endif
 constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
 static_assert(W_LOP + 4 <= RECW, "line-op words");
 
@@ -946,6 +956,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     // memory wave's LDS burst starts after the slab waves'
                     // chain-input reads of the period start
                     loads();
+                    // then a pause before the LDS burst: the slab waves' chain-input
+                    // reads of the period start go first (same-box A/B: 35.7 -> 35.3 ms
+                    // with 4 x 64 cycles; 8 was slower again)
+                    if constexpr (LDPC_C3_MSLEEP > 0) __builtin_amdgcn_s_sleep(LDPC_C3_MSLEEP);
                     read_gix();
                     read_out();
                     gathers();
@@ -1002,7 +1016,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     }
 
     // ------------------------------------------------------------ slab waves
-    const int sw = wave - (wave > CHW ? 1 : 0);   // slab index
+    const int sw = (wave - (wave > CHW ? 1 : 0) + LDPC_C3_SWROT) % WS;   // slab index
     constexpr int NSL = 64 * WS;                  // slab threads
     const int st_id = sw * 64 + lane;
     // the second-dispatched half of the slab waves loses VALU arbitration to
@@ -1098,7 +1112,12 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs), then reads and runs its pre
-                if (fair) __builtin_amdgcn_s_setprio(P0);
+                if (fair) {
+                    if (LDPC_C3_BPRIO && wave > CHW)   // experiment: second-dispatched waves ahead in the post
+                        __builtin_amdgcn_s_setprio(P0 + 1);
+                    else
+                        __builtin_amdgcn_s_setprio(P0);
+                }
                 if (LDPC_C3_EARLY_PRE == 2 && sl.w != 0) {
                     // the chain inputs first (the post waits for them alone:
                     // LDS returns in order), then the pre's reads under the post
