@@ -120,8 +120,8 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 #define LDPC_C3_BPRIO 0
 #endif
 #ifndef LDPC_C3_SWROT
-#define LDPC_C3_SWROT 3       // slab index = (the wave's slab position + SWROT) % WS: slab 0 (the distance-2
-                              // writers and readers) on the second wave of a SIMD (A/B: -0.8 %)
+#define LDPC_C3_SWROT 0       // experiment: slab index = (the wave's slab position + SWROT) % WS (same-box
+                              // A/B of 3 vs 0: -0.8 % on one box, +0.5 % on another)
 #endif
 constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
 static_assert(W_LOP + 4 <= RECW, "line-op words");
