@@ -106,9 +106,6 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 // (LcPlan::ops) as byte offsets: 8 the line loaded, 9 the line written back
 // (from the group's V block), 10 the slot written with the load of LC_PUT
 // periods earlier, 11 the slot written back (from the line cache)
-#ifndef LDPC_C3_EARLY_PRE
-#define LDPC_C3_EARLY_PRE 0   // experiment switch: 1 = slab waves 1..5 issue the pre's LDS reads before the post (r04f A/B: 1.4 ms slower)
-#endif
 #ifndef LDPC_C3_MORDER
 #define LDPC_C3_MORDER 1      // memory wave's period order: 0 = slot writes, gathers, loads, writebacks, stores,
                               // vmcnt(42); 1 = loads, gathers, slot writes, writebacks, stores, vmcnt(36)
@@ -1118,19 +1115,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     else
                         __builtin_amdgcn_s_setprio(P0);
                 }
-                if (LDPC_C3_EARLY_PRE == 2 && sl.w != 0) {
-                    // the chain inputs first (the post waits for them alone:
-                    // LDS returns in order), then the pre's reads under the post
-                    const uint32_t xr = sl.read_x(p - 1, sp);
-                    sl.read_pre((s + 1) % NI, rcn, in);
-                    sl.template post<false, ET, MP1>(p - 1, xr, sp);
-                } else if (LDPC_C3_EARLY_PRE == 1 && sl.w != 0) {
-                    // no distance-2 reader outside slab wave 0: the pre's LDS
-                    // reads are issued first and land under the post
-                    sl.read_pre((s + 1) % NI, rcn, in);
-                    const uint32_t xr = sl.read_x(p - 1, sp);
-                    sl.template post<false, ET, MP1>(p - 1, xr, sp);
-                } else {
+                {
                     const uint32_t xr = sl.read_x(p - 1, sp);
                     if (STAMP) {   // the chain inputs' arrival (the empty asm makes the wave wait for them)
                         asm volatile("" ::"v"(xr));
