@@ -29,7 +29,7 @@
 // * V lives in the grouped layout Vg[group][row][16 codewords] and the
 //   information rows move between HBM and the workgroup's LDS as whole 128-B
 //   lines (8 rows x 16 codewords) through a line cache planned on the host
-//   (linecache.cpp: each line is loaded 4 periods before its first use and
+//   (linecache.cpp: each line is loaded 3 periods before its first use and
 //   written back after its last, one residency serving ~8 checks) -- whole
 //   lines, no scattered 16-B V pieces (on MI355X the CU's texture path stalled
 //   on those: 47 ms per launch, 18 % of it on the info-row stores alone,
@@ -48,7 +48,7 @@
 // Period p (one s_barrier): chain = steps of window p; slab waves = post of
 // window p-1, pre of window p+1; memory wave = stores of window p-2, gathers
 // of window p+1+R, the line cache's writebacks / loads of period p and the
-// slot writes of the lines loaded in period p-3.
+// slot writes of the lines loaded in period p-2.
 //
 // The chain recurrence (check i, x edge input Y = V[p_{i-1}]):
 //   V[p_i] = clamp(c_o + eps * sign(c_x) * min(max(|c_x| - off, 0), T), +-127)
@@ -106,12 +106,11 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 // (LcPlan::ops) as byte offsets: 8 the line loaded, 9 the line written back
 // (from the group's V block), 10 the slot written with the load of LC_PUT
 // periods earlier, 11 the slot written back (from the line cache)
-#ifndef LDPC_C3_MORDER
-#define LDPC_C3_MORDER 1      // memory wave's period order: 0 = slot writes, gathers, loads, writebacks, stores,
-                              // vmcnt(42); 1 = loads, gathers, slot writes, writebacks, stores, vmcnt(36)
-#endif
 #ifndef LDPC_C3_MSLEEP
 #define LDPC_C3_MSLEEP 4      // memory wave: s_sleep (x 64 cycles) after its line loads, before its LDS burst
+#endif
+#ifndef LDPC_C3_MPRIO
+#define LDPC_C3_MPRIO 2        // memory wave priority (chain wave: 3; same-box A/B: 2 vs 0 -0.35 %)
 #endif
 #ifndef LDPC_C3_BPRIO
 #define LDPC_C3_BPRIO 0
@@ -822,14 +821,16 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     const int kl = lane >> 3, q = lane & 7;
 
     if (wave == MW) {
+        if (LDPC_C3_MPRIO > 0) __builtin_amdgcn_s_setprio(LDPC_C3_MPRIO);
         // ------------------------------------------------------------ memory wave
         // Every vector-memory operation of the workgroup, per period p for each
-        // slab wave's set of 8 slots (w = 0..WS-1), in this order: the slot
-        // writes of the lines loaded in period p-LC_PUT; the LDS-DMA gathers of
-        // window p+1+R (messages + o-edge parity rows); the line loads of period
-        // p (8 lines per set); the line writebacks of period p (slot -> VGPRs ->
-        // HBM); the stores of window p-2 (messages + x-edge parity rows).  Then
-        // vmcnt(42) (see mperiod).  Unused ops go to the sink row / line / slot,
+        // slab wave's set of 8 slots (w = 0..WS-1), in this order: the line
+        // loads of period p (8 lines per set, into VGPRs); the LDS-DMA gathers
+        // of window p+1+R (messages + o-edge parity rows); the line writebacks
+        // of period p (slot -> VGPRs -> HBM); the stores of window p-2
+        // (messages + x-edge parity rows); between them (LDS only) the slot
+        // writes of the lines loaded in period p-LC_PUT.  Then vmcnt(36) (see
+        // mperiod).  Unused ops go to the sink row / line / slot,
         // so the counts are static; tools/check_vmcnt.py checks the emitted ISA
         // against them at build time.
         char *lcb = (char *)&sm.lc[0][0];
@@ -890,22 +891,19 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 sidx[w] = (uint32_t)a.m;
                 lop[w] = *(const uint4 *)&sm.tab[0][8 * w + kl][W_LOP];
             }
-            // period p: gathers of window p+1+R, line loads of period p, line
-            // writebacks of period p, stores of window p-2 (4 WS = 24 ops);
-            // vmcnt(42) = 24 + 3 WS at its end completes everything up to the
-            // gathers of period p-1 (the pre of window p+2 reads them next
-            // period), hence the line loads of period p-2 and earlier (the
-            // slot writes of period p+1 take those of period p+1-LC_PUT), and
-            // a writeback two periods after its issue (its line is loaded
-            // again >= 3 periods later, linecache.cpp).  The count holds only
-            // while the compiler emits exactly these 24 vector-memory
-            // instructions per period: tools/check_vmcnt.py (run by
-            // __graft_entry__.build) checks the ISA
-            // Latency: every LDS read the period's vector-memory ops need is
-            // issued at its start -- the gather indices, and the writeback and
-            // store data (their writers ran before the barrier) -- so the
-            // round trips overlap the slot writes, gathers and loads issued
-            // meanwhile instead of each preceding its store
+            // period p, vector memory in this order: the line loads of period
+            // p, the gathers of window p+1+R, the line writebacks of period p,
+            // the stores of window p-2 (4 WS = 24 ops); vmcnt(36) = 24 + 2 WS
+            // at its end completes everything up to the gathers of period p-1
+            // (the pre of window p+2 reads them next period) and so the line
+            // loads of period p-1 (the slot writes of period p+1 take those of
+            // period p+1-LC_PUT = p-1), and a writeback two periods after its
+            // issue (its line is loaded again >= 3 periods later,
+            // linecache.cpp).  The count holds only while the compiler emits
+            // exactly these 24 vector-memory instructions per period:
+            // tools/check_vmcnt.py (run by __graft_entry__.build) checks the
+            // ISA.  The compiler's own waits for the line loads it tracks (it
+            // does not see the LDS-DMA gathers) are stricter than needed.
             auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
                 constexpr int s = decltype(sc_)::value;   // p % NPD
                 if (STAMP) tx = stampL();
@@ -942,32 +940,16 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                         if (lane < 40) dma16_buf(vr, (gix[w] << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
                     });
                 };
-                if constexpr (LDPC_C3_MORDER == 0) {
-                    read_gix();
-                    read_out();
-                    slot_writes();
-                    gathers();
-                    loads();
-                } else if constexpr (LDPC_C3_MORDER == 1) {
-                    // the line loads first (their addresses are in VGPRs): the
-                    // memory wave's LDS burst starts after the slab waves'
-                    // chain-input reads of the period start
-                    loads();
-                    // then a pause before the LDS burst: the slab waves' chain-input
-                    // reads of the period start go first (same-box A/B: 35.7 -> 35.3 ms
-                    // with 4 x 64 cycles; 8 was slower again)
-                    if constexpr (LDPC_C3_MSLEEP > 0) __builtin_amdgcn_s_sleep(LDPC_C3_MSLEEP);
-                    read_gix();
-                    read_out();
-                    gathers();
-                    slot_writes();
-                } else {   // as 1, the slot writes (freeing a pend set) before the output reads
-                    loads();
-                    read_gix();
-                    gathers();
-                    slot_writes();
-                    read_out();
-                }
+                // the line loads first (their addresses are in VGPRs), then a
+                // pause, so that the slab waves' chain-input reads of the period
+                // start are served before the memory wave's LDS burst (same-box
+                // A/B: 35.7 -> 35.3 ms with 4 x 64 cycles; 8 was slower again)
+                loads();
+                if constexpr (LDPC_C3_MSLEEP > 0) __builtin_amdgcn_s_sleep(LDPC_C3_MSLEEP);
+                read_gix();
+                read_out();
+                gathers();
+                slot_writes();
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // writebacks of period p
                     constexpr int w = decltype(wc)::value;
                     rbuf_store_v4(__builtin_bit_cast(i32x4, wbd[w]), vr, (int)(lop[w].y + lq), 0, 0);
@@ -983,10 +965,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     lop[w] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][W_LOP];
                 });
                 if (STAMP) sP[1] += stampL() - tx;
-                if constexpr (LDPC_C3_MORDER != 0)
-                    asm volatile("s_waitcnt vmcnt(36)" ::: "memory");   // the gathers of p-1: 12 + 24 ops after them
-                else
-                    asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(36)" ::: "memory");   // the gathers of p-1: 12 + 24 ops after them
                 if (STAMP) sA += stampL() - tx;
                 __syncthreads();
                 uS = (uS + 1 == a.nw) ? 0 : uS + 1;
