@@ -429,9 +429,14 @@ def test_mixed_rate_batch_with_early_termination():
         llr[sel] = channel.awgn_i8_host(code.n, sel.size, seed=31 + c, table=table, codeword=cw)
     d_hard = torch.empty((B, 64800), dtype=torch.uint8, device="cuda")
     d_its = torch.empty(B, dtype=torch.int32, device="cuda")
+    mx.profile(True)   # per-code decode-kernel timing (ldpc_mixed_kernel_time)
     mx.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, ids, 20, params=default_params(early_term=1),
                         iters_used=d_its)
     torch.cuda.synchronize()
+    kt = mx.kernel_time(reset=True)
+    assert [n for _, n in kt] == [1, 1, 1, 1] and all(ms > 0 for ms, _ in kt), kt
+    assert [n for _, n in mx.kernel_time()] == [0, 0, 0, 0]   # reset
+    mx.profile(False)
     hard, its = d_hard.cpu().numpy(), d_its.cpu().numpy()
     for c, name in enumerate(names):
         sel = np.where(ids == c)[0]
