@@ -38,11 +38,17 @@ struct Scratch {
     size_t msg_bytes = 0;
     void *d_early = nullptr;        // coop early termination: live[stride] u8, bad[stride] u32, iters[stride]
     size_t early_bytes = 0;
+    void *d_V2 = nullptr;           // coop3 staged early termination: compacted state, map | iterations | count
+    size_t V2_bytes = 0;
+    void *d_et2 = nullptr;
+    size_t et2_bytes = 0;
     void release()
     {
         (void)hipFree(d_V);
         (void)hipFree(d_msg);
         (void)hipFree(d_early);
+        (void)hipFree(d_V2);
+        (void)hipFree(d_et2);
         *this = Scratch{};
     }
 };
@@ -444,6 +450,10 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     // early termination: live u8 | bad u32 | iterations used i32 (when the caller passed none)
     const bool et_state = (kern == 5 || kern == 8) && p->early_term;
     if (et_state && (rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
+    const bool et_staged = kern == 8 && p->early_term && coop3_et_stage_iters(batch, n_iter) > 0;
+    if (et_staged && ((rc = ensure(&sc.d_V2, &sc.V2_bytes, 2 * v_bytes)) != LDPC_OK ||
+                      (rc = ensure(&sc.d_et2, &sc.et2_bytes, (size_t)stride * 20 + 256)) != LDPC_OK))
+        return rc;
     if (alloc_only) return LDPC_OK;
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
@@ -491,6 +501,8 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
     L.iters_used = d_iters;
     L.lds_pad = c->lds_pad;
+    L.V2 = et_staged ? sc.d_V2 : nullptr;
+    L.et2 = et_staged ? (int32_t *)sc.d_et2 : nullptr;
     if (et_state) {
         L.bad = (uint32_t *)sc.d_early;
         if (!L.iters_used) L.iters_used = (int32_t *)((char *)sc.d_early + (size_t)stride * 4);

@@ -77,6 +77,8 @@ struct LcPlan;
 // the schedule and its line-cache plan (linecache.cpp): 0 ok, 1 none for this code, < 0 error
 int coop3_plan_lc(const ldpc_code *h, Coop3Host &ho, LcPlan &lp);
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s);
+// first-stage iterations of a staged early-termination decode (0: one launch)
+int coop3_et_stage_iters(int batch, int iters);
 
 // ---- linecache.cpp: coop3's LDS line cache (info rows as 128-B lines) ----
 constexpr int LC_GAP = 10;    // accesses of a line >= LC_GAP periods apart: separate residencies

@@ -166,6 +166,12 @@ struct Coop3Args {
     const uint32_t *ev;
     int32_t *iters_used;
     int iters, batch, m0, d1, n_pro, n_epi;
+    // ET stages (launch_coop3): iterations done before this launch (added to
+    // the iterations recorded), the value recorded for codewords still
+    // decoding at its end, and the batch read from device memory (a compacted
+    // stage's codeword count) when batch_dev is set
+    int iter_base, fill;
+    const int *batch_dev;
     int G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
     uint32_t nmsf;                    // NMS factor per half (value form)
     size_t gstride;                   // bytes between two codeword groups' V
@@ -591,6 +597,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     const int lane = threadIdx.x & 63;
     const int nb = gridDim.x, id = blockIdx.x;
     const int wg = a.remap ? (id & 7) * (nb >> 3) + (id >> 3) : id;   // XCD-aware codeword groups
+    const int batch = (ET && a.batch_dev) ? *a.batch_dev : a.batch;
     const int G = ET ? a.nw : a.G;   // periods per segment (ET: one iteration)
     if (G == 0) return;
     char *Vg = (char *)a.V + (size_t)wg * a.gstride;
@@ -600,11 +607,11 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     auto et_row = [&](uint32_t v) -> const uint4 * { return (const uint4 *)(Vg + (size_t)v * 16); };
     if constexpr (ET) {
         if (threadIdx.x == 0) {
-            const int valid = min(CW, max(0, a.batch - wg * CW));
+            const int valid = min(CW, max(0, batch - wg * CW));
             et_sh[0] = (1u << valid) - 1u;
             et_sh[1] = 0;
         }
-        if (threadIdx.x < CW && wg * CW + (int)threadIdx.x < a.batch) a.iters_used[wg * CW + threadIdx.x] = a.iters;
+        if (threadIdx.x < CW && wg * CW + (int)threadIdx.x < batch) a.iters_used[wg * CW + threadIdx.x] = a.fill;
         __syncthreads();
         if (et_sh[0] == 0) return;   // padding columns only
     }
@@ -753,7 +760,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             et_sh[0] = live & ~fresh;
             et_sh[1] = 0;
         }
-        if (fresh && threadIdx.x < CW && ((fresh >> threadIdx.x) & 1u)) a.iters_used[wg * CW + threadIdx.x] = it + 1;
+        if (fresh && threadIdx.x < CW && ((fresh >> threadIdx.x) & 1u))
+            a.iters_used[wg * CW + threadIdx.x] = a.iter_base + it + 1;
         __syncthreads();
         return (live & ~fresh) != 0 && it + 1 < a.iters;
     };
@@ -1040,7 +1048,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         }
         __syncthreads();   // prologue 1: tables and resident lines in LDS
         if constexpr (ET) {   // codewords 2q (low half) and 2q+1 (high half) of this lane: converged?
-            const int valid = min(CW, max(0, a.batch - wg * CW));
+            const int valid = min(CW, max(0, batch - wg * CW));
             const uint32_t conv = (((1u << valid) - 1u) & ~et_sh[0]) >> (2 * q);
             sl.fm = ((conv & 1u) ? 0x0000FFFFu : 0u) | ((conv & 2u) ? 0xFFFF0000u : 0u);
             sl.psel = 0x0c0c0000u | ((conv & 2u) ? 0x0300u : 0x0700u) | ((conv & 1u) ? 0x01u : 0x05u);
@@ -1404,6 +1412,14 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
 // number of 128-B lines in all (groups spread over the L2 channels).  One
 // block per group lets the memory wave address all of it with 32-bit buffer
 // offsets from one resource
+void coop3_group_layout_nm(int n, int m, size_t *vpart, size_t *block)
+{
+    const size_t vlines = ((size_t)n + 8 + 7) / 8, mlines = ((size_t)(m + 1) * MREC + 127) / 128;
+    size_t lines = vlines + mlines;
+    if (lines % 2 == 0) lines++;
+    *vpart = vlines * 128;
+    *block = lines * 128;
+}
 void coop3_group_layout(const ldpc_code *h, size_t *vpart, size_t *block)
 {
     const size_t vlines = ((size_t)h->n + 8 + 7) / 8, mlines = ((size_t)(h->m + 1) * MREC + 127) / 128;
@@ -1422,6 +1438,107 @@ size_t coop3_group_bytes(const ldpc_code *h)
 // the workgroup's LDS (the ET kernel stages the hard bits of all n variables,
 // u16 each, in it between segments)
 bool coop3_et_in_kernel(const CoopCode &cc, int n) { return cc.S == 48 && (size_t)n * 2 <= sizeof(Smem3<6, 2>); }
+
+// ---- staged early termination (batches of more than one workgroup per CU):
+// after a first launch of K iterations the codewords still decoding are
+// compacted into dense 16-codeword groups of a second state buffer (V byte,
+// message code and constant halves of each codeword: its slot in the pair
+// words), decoded on from there (iterations K+1 ..), and their V moved back.
+// A workgroup leaves only when all its 16 codewords have converged, so
+// without compaction one slow codeword holds 15 converged ones in its
+// workgroup's pipeline until the last iteration.
+constexpr int ET_LIVE = -1;   // iters_used of a codeword still decoding after a stage
+
+// the codewords of a stage still decoding (its[j] == ET_LIVE, j < n or
+// *n_dev): their stage index -> sel, their batch slot (through prev, the
+// stage's own map; none: the identity) -> map, their number -> *count
+__global__ void et_select_k(const int32_t *its, int n, const int *n_dev, const int32_t *prev, int32_t *sel,
+                            int32_t *map, int *count)
+{
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nn = n_dev ? *n_dev : n;
+    const bool live = j < nn && its[j] == ET_LIVE;
+    const unsigned long long m = __ballot(live);
+    int base = 0;
+    if ((threadIdx.x & 63) == 0 && m) base = atomicAdd(count, __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (live) {
+        const int k = base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1ull));
+        sel[k] = j;
+        map[k] = prev ? prev[j] : j;
+    }
+}
+
+// dst group g2 (blockIdx.y), rows / checks of the group (x): V bytes and the
+// message halves of the codewords map[16 g2 + i] (i < 16; the padding past
+// count gets zeros)
+__global__ void et_gather_k(const char *Vs, char *Vd, const int32_t *map, const int *count, int vrows, int mrows,
+                            size_t gstride, size_t vpart)
+{
+    const int g2 = blockIdx.y, nlive = *count;
+    if (16 * g2 >= nlive) return;
+    int src[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) src[i] = 16 * g2 + i < nlive ? map[16 * g2 + i] : -1;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < vrows + mrows; r += gridDim.x * blockDim.x) {
+        char *d = Vd + (size_t)g2 * gstride;
+        if (r < vrows) {   // V row r: byte i = codeword i
+            uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                if (src[i] >= 0) {
+                    const uint8_t v = (uint8_t)Vs[(size_t)(src[i] >> 4) * gstride + (size_t)r * 16 + (src[i] & 15)];
+                    w[i >> 2] |= (uint32_t)v << (8 * (i & 3));
+                }
+            *(uint4 *)(d + (size_t)r * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {   // message record of check c: pair q's (MA, MB) words, codeword 2q + h in half h of each
+            const int c = r - vrows;
+            uint32_t w[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) w[i] = 0;
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                if (src[i] >= 0) {
+                    const char *rec = Vs + (size_t)(src[i] >> 4) * gstride + vpart + (size_t)c * MREC;
+                    const int qs = (src[i] & 15) >> 1, hs = src[i] & 1, qd = i >> 1, hd = i & 1;
+                    const uint32_t ma = ((const uint16_t *)(rec + 8 * qs))[hs], mb = ((const uint16_t *)(rec + 8 * qs + 4))[hs];
+                    w[2 * qd] |= ma << (16 * hd);
+                    w[2 * qd + 1] |= mb << (16 * hd);
+                }
+            uint4 *o = (uint4 *)(d + vpart + (size_t)c * MREC);
+#pragma unroll
+            for (int k = 0; k < 4; k++) o[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        }
+    }
+}
+
+// the compacted codewords' V rows and iterations back to their batch slots
+__global__ void et_scatter_k(const char *Vs, char *Vd, const int32_t *map, const int *count, const int32_t *its2,
+                             int32_t *iters_used, int vrows, size_t gstride)
+{
+    const int g2 = blockIdx.y, nlive = *count;
+    if (16 * g2 >= nlive) return;
+    if (blockIdx.x == 0 && threadIdx.x < 16 && 16 * g2 + (int)threadIdx.x < nlive)
+        iters_used[map[16 * g2 + threadIdx.x]] = its2[16 * g2 + threadIdx.x];
+    int dst[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) dst[i] = 16 * g2 + i < nlive ? map[16 * g2 + i] : -1;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < vrows; r += gridDim.x * blockDim.x) {
+        const uint4 v = *(const uint4 *)(Vs + (size_t)g2 * gstride + (size_t)r * 16);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            if (dst[i] >= 0)
+                Vd[(size_t)(dst[i] >> 4) * gstride + (size_t)r * 16 + (dst[i] & 15)] = (char)(w[i >> 2] >> (8 * (i & 3)));
+    }
+}
+
+// first-stage iterations of a staged early-termination decode (0: one stage)
+int coop3_et_stage_iters(int batch, int iters)
+{
+    const int k = env_int3("LDPC_COOP3_ET_K", 20), min_batch = env_int3("LDPC_COOP3_ET_STAGE_MIN", 8192);
+    return (k > 0 && k < iters && batch >= min_batch) ? k : 0;
+}
 
 int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
 {
@@ -1455,6 +1572,9 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.iters_used = L.iters_used;
     a.iters = L.iters;
     a.batch = L.batch;
+    a.iter_base = 0;
+    a.fill = L.iters;
+    a.batch_dev = nullptr;
     a.m0 = cc.m0;
     a.d1 = cc.d1;
     a.rmm = (uint32_t)(L.msg_max * 256 + 255) * 0x00010001u;
@@ -1473,14 +1593,72 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
     int rc;
-    if (et) {
+    auto launch_et = [&](const Coop3Args &x) -> int {
         if (nms)
-            hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 8), 0, s, a);
+            hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 8), 0, s, x);
         else if (stamped)
-            hipLaunchKernelGGL((coop3_decode<6, 2, true, true>), dim3(grid), dim3(64 * 8), 0, s, a);
+            hipLaunchKernelGGL((coop3_decode<6, 2, true, true>), dim3(grid), dim3(64 * 8), 0, s, x);
         else
-            hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
-        rc = hipGetLastError() == hipSuccess ? 0 : -1;
+            hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 8), 0, s, x);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    };
+    const int k1 = et && L.V2 && L.et2 ? coop3_et_stage_iters(L.batch, L.iters) : 0;
+    if (et && k1 > 0 && !stamped) {
+        // stage 0: K iterations on the whole batch (codewords still decoding
+        // record ET_LIVE); then, every ET_STEP iterations, the live codewords
+        // are compacted into the other of two dense buffers and decoded on
+        // from there; each stage's codewords go back to their batch slots
+        // (V rows and iterations) after it
+        const int step = std::max(1, env_int3("LDPC_COOP3_ET_STEP", 5));
+        size_t vpart = 0, block = 0;
+        coop3_group_layout_nm(L.n, L.m, &vpart, &block);
+        const size_t vbytes = (size_t)grid * L.vgroup;
+        char *buf[2] = {(char *)L.V2, (char *)L.V2 + vbytes};
+        const int S = L.stride;
+        int32_t *sel = L.et2, *map[2] = {L.et2 + S, L.et2 + 2 * S}, *its[2] = {L.et2 + 3 * S, L.et2 + 4 * S};
+        int *count = (int *)(L.et2 + 5 * S);   // one counter per stage (<= 64 stages)
+        Coop3Args a0 = a;
+        a0.iters = k1;
+        a0.fill = ET_LIVE;
+        if (launch_et(a0)) return -1;
+        const char *src = (const char *)L.V;
+        const int32_t *src_its = L.iters_used, *src_map = nullptr;
+        const int *src_n = nullptr;
+        int done = k1;
+        for (int st = 0; done < L.iters && st < 64; st++) {
+            const int k = std::min(step, L.iters - done), b = st & 1;
+            const bool last = done + k >= L.iters;
+            if (hipMemsetAsync(count + st, 0, sizeof(int), s) != hipSuccess) return -1;
+            hipLaunchKernelGGL(et_select_k, dim3((S + 255) / 256), dim3(256), 0, s, src_its, L.batch, src_n, src_map,
+                               sel, map[b], count + st);
+            hipLaunchKernelGGL(et_gather_k, dim3(64, grid), dim3(256), 0, s, src, buf[b], sel, count + st, L.n + 8,
+                               L.m + 1, L.vgroup, vpart);
+            if (hipGetLastError() != hipSuccess) return -1;
+            // the compacted codewords from iteration `done` on: no XCD remap
+            // (the live groups are the first ones), the batch read on the device
+            Coop3Args as = a;
+            as.V = (int8_t *)buf[b];
+            as.Mc = (uint8_t *)buf[b] + vpart;
+            as.iters = k;
+            as.iter_base = done;
+            as.fill = last ? L.iters : ET_LIVE;
+            as.batch_dev = count + st;
+            as.iters_used = its[b];
+            as.remap = false;
+            if (launch_et(as)) return -1;
+            hipLaunchKernelGGL(et_scatter_k, dim3(64, grid), dim3(256), 0, s, (const char *)buf[b], (char *)L.V, map[b],
+                               count + st, its[b], L.iters_used, L.n, L.vgroup);
+            if (hipGetLastError() != hipSuccess) return -1;
+            src = buf[b];
+            src_its = its[b];
+            src_map = map[b];
+            src_n = count + st;
+            done += k;
+        }
+        return 0;
+    }
+    if (et) {
+        rc = launch_et(a);
     } else if (nms) {
         hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
         return hipGetLastError() == hipSuccess ? 0 : -1;

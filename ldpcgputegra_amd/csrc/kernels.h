@@ -31,6 +31,11 @@ struct DecodeLaunch {
     // coop3: V in the grouped layout Vg[stride / 16][rows][16 codewords],
     // vgroup bytes between groups (0: the row layout V[N][vpitch])
     size_t vgroup;
+    // coop3 staged early termination: two more grouped state buffers (each
+    // the size of V) and int32 scratch: selection | 2 maps | 2 iteration
+    // arrays ([stride] each) | per-stage counts
+    void *V2;
+    int32_t *et2;
     // dynamic LDS bytes added to the windowed2 launch (mixed batches: keeps its
     // waves off the CUs of a concurrent coop3 decode, see ldpc_ctx_set_lds_pad)
     int lds_pad;

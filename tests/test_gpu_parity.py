@@ -238,6 +238,38 @@ def test_early_termination_vs_oracle(code):
         assert np.array_equal(d_soft.cpu().numpy(), ref_soft), "kernel %d" % k
 
 
+@pytest.mark.parametrize("q,nms,step,ebn0", [(20, False, 10, 1.0), (40, False, 2, 1.0), (30, True, 3, 1.6)])
+def test_coop3_staged_early_termination_vs_oracle(monkeypatch, q, nms, step, ebn0):
+    """Staged early termination (launch_coop3: K iterations on the whole
+    batch, then every `step` iterations the codewords still decoding
+    compacted into dense groups of the other of two state buffers and
+    decoded on from there, each stage's codewords moved back), forced at a
+    small batch (LDPC_COOP3_ET_STAGE_MIN=0): hard and soft outputs and
+    iterations equal the oracle's per-codeword early termination."""
+    torch = _torch()
+    code, batch, iters = "dvbs2_r1_2", 200, 30
+    t = load_table(code)
+    sigma = channel.sigma_from_ebn0(ebn0, t.k_info / t.n)
+    llr = channel.awgn_i8_host(t.n, batch, seed=17, table=channel.i8_table(sigma))
+    algo, param = (O.NMS, 26) if nms else (O.OMS, 1)
+    ref_hard, ref_soft, ref_its = O.decode_i8(t, llr, iters, algo, param, early_term=True, return_soft=True)
+    k1 = int(np.percentile(ref_its, q))   # the first stage: some codewords converge in it, some after it
+    assert 0 < k1 < iters and (ref_its > k1).any() and (ref_its <= k1).any()
+    monkeypatch.setenv("LDPC_COOP3_ET_STAGE_MIN", "0")
+    monkeypatch.setenv("LDPC_COOP3_ET_K", str(k1))
+    monkeypatch.setenv("LDPC_COOP3_ET_STEP", str(step))   # step 2 / 3: several compactions
+    dec = decoder(code, 8, max_batch=256)
+    d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+    d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
+    d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
+    p = default_params(early_term=1, algo=ALGO_NMS, factor=param) if nms else default_params(early_term=1)
+    dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=p, soft=d_soft, iters_used=d_its)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_its.cpu().numpy(), ref_its)
+    assert np.array_equal(d_soft.cpu().numpy(), ref_soft)
+    assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
+
+
 def has_kernel(code, k):
     try:
         decoder(code, k, 64)
