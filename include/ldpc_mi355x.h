@@ -87,7 +87,10 @@ typedef struct {
     int var_max;
     int msg_min;     /* setMsgRange(min, max)                   default -31, 31  */
     int msg_max;
-    int early_term;  /* stop a codeword once H*x == 0 (0 = exact n_iter) */
+    int early_term;  /* stop a codeword once H*x == 0 (0 = exact n_iter); the
+                        DVB-S2 r1/2 kernel decodes batches >= 8192 in stages,
+                        compacting the codewords still decoding every few
+                        iterations (LDPC_COOP3_ET_K / _STEP / _STAGE_MIN) */
 } ldpc_params;
 
 /* ---- errors / version ------------------------------------------------ */
