@@ -20,6 +20,7 @@
 #include "ldpc_internal.h"
 #include "windowed.h"
 #include "coop.h"
+#include "stairf.h"
 #include "lds.h"
 #include "host.h"
 
@@ -81,6 +82,7 @@ struct ldpc_ctx {
     CoopCode coop{};                // coop.hip tables (workgroup-cooperative DVB-S2 path)
     CoopCode coop3{};               // coop3.hip tables (pre + post slab waves, i16 chain, D0 = 7)
     LdsCode lds{};                  // lds.hip tables (LDS-resident short-code decoder)
+    StairfCode stairf{};            // stairf.hip table (float staircase codes)
     Scratch sc;                     // device-API decodes and the unchunked host path
     void *d_io = nullptr;           // staging for the quantiser's host-buffer API
     size_t io_bytes = 0;
@@ -180,6 +182,7 @@ extern "C" int ldpc_ctx_create(const ldpc_code *h, int device, int max_batch, ld
     if ((rc = coop_upload(h, &c->coop)) != LDPC_OK) return fail(rc);
     if ((rc = coop3_upload(h, &c->coop3)) != LDPC_OK) return fail(rc);
     if ((rc = lds_upload(h, &c->lds)) != LDPC_OK) return fail(rc);
+    if ((rc = stairf_upload(h, &c->stairf)) != LDPC_OK) return fail(rc);
     *out = c;
     return LDPC_OK;
 }
@@ -199,6 +202,7 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     coop_free(&c->coop);
     coop_free(&c->coop3);
     lds_free(&c->lds);
+    stairf_free(&c->stairf);
     for (auto &pr : c->events) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -228,16 +232,16 @@ extern "C" int ldpc_ctx_stream(ldpc_ctx *c, void **s)
 
 bool ldpc_ctx_has_kernel(const ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 9) return false;
+    if (!c || k < 0 || k > 11 || k == 10) return false;
     if (c->device < 0) return k == 0;
     return !((k == 2 && !windowed_supported(c->code)) || (k == 3 && !c->w16.valid) || k == 4 ||
              (k == 5 && !c->coop.valid) || k == 6 || (k == 7 && !c->lds.valid) || (k == 8 && !c->coop3.valid) ||
-             (k == 9 && !c->lds.ep_valid));
+             (k == 9 && !c->lds.ep_valid) || (k == 11 && !c->stairf.valid));
 }
 
 extern "C" int ldpc_ctx_set_kernel(ldpc_ctx *c, int k)
 {
-    if (!c || k < 0 || k > 9) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 9");
+    if (!c || k < 0 || k > 11 || k == 10) return ldpc_set_error(LDPC_EINVAL, "kernel must be 0 (auto) .. 9 or 11");
     if (!ldpc_ctx_has_kernel(c, k)) return ldpc_set_error(LDPC_EUNSUPPORTED, "kernel %d cannot schedule this code", k);
     c->kernel = k;
     return LDPC_OK;
@@ -342,8 +346,14 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
     const bool ld = lds_applicable(c->code, c->lds, is_float);
     if (c->kernel == 7) return ld ? 7 : -1;
     if (c->kernel == 9) return ldsep_applicable(c->code, c->lds, is_float) ? 9 : -1;
+    const bool sf = c->stairf.valid && stairf_stride_ok(c->stairf, c->code->n, stride);
+    if (c->kernel == 11) return (is_float && sf && !p->early_term) ? 11 : -1;
     if (is_float) {
         if (c->kernel == 0 && ldsep_applicable(c->code, c->lds, true)) return 9;
+        if (c->kernel == 0 && sf) {
+            if (!p->early_term) return 11;
+            c->last_skipped = 11;
+        }
         return (c->kernel == 0 && lds_preferred(c->code, c->lds, true)) ? 7 : (c->kernel <= 1 ? 1 : -1);
     }
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
@@ -425,10 +435,11 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         if (lr) return ldpc_set_error(LDPC_EDEVICE, "lds decode launch: %s", hipGetErrorString(hipGetLastError()));
         return LDPC_OK;
     }
-    const bool win = kern >= 2;
+    const bool win = kern >= 2 && kern != 11;
     // + a sink row / sink words for the masked stores of the coop kernel
-    const size_t msg_zero = (kern == 8   ? coop3_msg_bytes(h, stride)
-                             : win    ? windowed_msg_bytes(h, stride)
+    const size_t msg_zero = (kern == 8    ? coop3_msg_bytes(h, stride)
+                             : kern == 11 ? stairf_msg_bytes(c->stairf, stride)
+                             : win        ? windowed_msg_bytes(h, stride)
                                       : (size_t)h->e * stride * esz) +
                             4096;
     // V row pitch (codewords): the coop kernel pads it by LDPC_VPITCH_PAD
@@ -516,6 +527,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     }
     int lr = kern == 8   ? launch_coop3(L, c->coop3, s)
              : kern == 5 ? launch_coop(L, c->coop, s)
+             : kern == 11 ? launch_stairf(L, c->stairf, s)
              : kern == 3 ? launch_windowed2(L, c->w16, s)
              : kern == 2 ? launch_windowed(L, c->wcode, s)
                          : launch_generic(L, s);

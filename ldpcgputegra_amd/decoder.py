@@ -58,8 +58,10 @@ class Decoder:
         windowed2 (S = 16), 5 = workgroup-cooperative DVB-S2 kernel (coop),
         7 = LDS-resident short-code kernel (int8 and float), 8 = coop3 (slab waves
         doing pre + post, i16 chain; the DVB-S2 r1/2 default), 9 = ldsep
-        (edge-parallel float for short QC codes; the float default where it fits).  4 and 6
-        (windowed2 S = 32, coop2) were superseded and removed."""
+        (edge-parallel float for short QC codes; the float default where it fits),
+        11 = stairf (float staircase codes, DVB-S2: the float default for them
+        without early termination).  4 and 6 (windowed2 S = 32, coop2) were
+        superseded and removed."""
         _lib.check(_lib.lib().ldpc_ctx_set_kernel(self._ctx, int(kernel)))
 
     @property
@@ -78,7 +80,7 @@ class Decoder:
         _lib.check(_lib.lib().ldpc_ctx_kernel_time(self._ctx, C.byref(ms), C.byref(n), int(reset)))
         return ms.value, n.value
 
-    KERNEL_NAMES = {0: "none", 1: "generic", 2: "windowed", 3: "windowed2_s16", 4: "windowed2_s32", 5: "coop", 6: "coop2", 7: "lds", 8: "coop3", 9: "ldsep", 10: "host"}
+    KERNEL_NAMES = {0: "none", 1: "generic", 2: "windowed", 3: "windowed2_s16", 4: "windowed2_s32", 5: "coop", 6: "coop2", 7: "lds", 8: "coop3", 9: "ldsep", 10: "host", 11: "stairf"}
 
     @property
     def last_kernel(self):

@@ -307,6 +307,42 @@ def test_float_decoder_vs_oracle(code, algo, beta, batch):
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard), "kernel %d" % k
 
 
+@pytest.mark.parametrize("code,algo,beta,batch,iters", [
+    ("dvbs2_r1_2", ALGO_MS, 0.0, 40, 6), ("dvbs2_r1_2", ALGO_OMS, 0.15, 17, 3), ("dvbs2_r1_2", ALGO_NMS, 0.75, 64, 4),
+    ("dvbs2_r2_3", ALGO_MS, 0.0, 33, 3), ("dvbs2shape_r3_4", ALGO_NMS, 0.75, 20, 3),
+    ("dvbs2shape_r5_6", ALGO_MS, 0.0, 20, 3), ("dvbs2_r8_9", ALGO_OMS, 0.15, 20, 3), ("dvbs2_r9_10", ALGO_MS, 0.0, 80, 2),
+    ("dvbs2_r1_2", ALGO_MS, 0.0, 3, 1)])
+def test_stairf_vs_oracle(code, algo, beta, batch, iters, monkeypatch):
+    """Float staircase kernel (11, stairf.hip): the float default for the
+    DVB-S2 codes (no early termination) against the oracle's serial float
+    decode (oracle/ldpc_oracle.c), every DVB-S2 check degree it is built for,
+    every group width (LDPC_STAIRF_S 4 / 8 / 16: 16 / 8 / 4 codewords per wave;
+    a code whose check count 16 does not divide runs its fallback width);
+    iteration counts that are not multiples of its prefetch block; batches that
+    leave part of a wave empty; bit-identical soft output."""
+    torch = _torch()
+    t = load_table(code)
+    rng = np.random.default_rng(21)
+    sigma = channel.sigma_from_ebn0(1.0, t.k_info / t.n)
+    llr = (-1.0 + sigma * rng.standard_normal((batch, t.n))).astype(np.float32)
+    o_algo = O.NMS if algo == ALGO_NMS else O.OMS
+    ref_hard, ref_soft, _ = O.decode_f32(t, llr, iters, o_algo, beta)
+    for k, width in ((0, None), (11, 4), (11, 8), (11, 16)):
+        if width:
+            monkeypatch.setenv("LDPC_STAIRF_S", str(width))
+        dec = decoder(code, k, max(64, batch))
+        d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+        d_soft = torch.empty((batch, t.n), dtype=torch.float32, device="cuda")
+        dec.decode_f32_device(torch.from_numpy(llr).cuda(), d_hard, iters,
+                              params=default_params(algo=algo, beta=beta), soft=d_soft)
+        torch.cuda.synchronize()
+        assert dec.last_kernel == "stairf"
+        soft = d_soft.cpu().numpy()
+        assert np.array_equal(soft.view(np.uint32), ref_soft.view(np.uint32)), \
+            "kernel %d width %s: %d values differ" % (k, width, int((soft != ref_soft).sum()))
+        assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
+
+
 @pytest.mark.parametrize("code,batch", [("648x324", 1024), ("576x288", 37)])
 def test_ldsep_auto_early_termination_vs_oracle(code, batch):
     """The float default for the short QC codes is the edge-parallel kernel
