@@ -168,14 +168,18 @@ int ldpc_ctx_stream(ldpc_ctx *ctx, void **hip_stream);
  * 7 = LDS-resident short-code kernel (whole state in LDS; int8 and float),
  * 8 = coop3 (DVB-S2 first-group degree 7: slab waves doing pre + post, i16 chain),
  * 9 = ldsep (float, short QC codes: one wave per codeword, one lane per edge;
- *     the automatic choice for float decodes of the codes it fits).
+ *     the automatic choice for float decodes of the codes it fits),
+ * 11 = stairf (float, DVB-S2 staircase codes: S consecutive checks of 64/S
+ *     codewords per wave, the staircase chain by DPP; the automatic choice for
+ *     float decodes of those codes, early termination by one launch per
+ *     iteration + a syndrome pass).
  * 4 and 6 (windowed2 S = 32, coop2) were superseded and are rejected
  * with LDPC_EUNSUPPORTED. */
 int ldpc_ctx_set_kernel(ldpc_ctx *ctx, int kernel);
 int ldpc_ctx_get_kernel(ldpc_ctx *ctx, int *kernel);
 /* Kernel family the last decode actually ran (1 generic, 2 windowed,
  * 3 windowed2 S=16, 5 coop, 7 lds, 8 coop3, 9 ldsep, 10 the host decoder of a
- * device -1 context; 0 before the first decode). */
+ * device -1 context, 11 stairf; 0 before the first decode). */
 int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
 /* The fastest kernel of this code that the last automatic selection could
  * not use for the call's parameters (8: coop3, 5: coop -- they take OMS / MS

@@ -347,13 +347,10 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
     if (c->kernel == 7) return ld ? 7 : -1;
     if (c->kernel == 9) return ldsep_applicable(c->code, c->lds, is_float) ? 9 : -1;
     const bool sf = c->stairf.valid && stairf_stride_ok(c->stairf, c->code->n, stride);
-    if (c->kernel == 11) return (is_float && sf && !p->early_term) ? 11 : -1;
+    if (c->kernel == 11) return (is_float && sf) ? 11 : -1;
     if (is_float) {
         if (c->kernel == 0 && ldsep_applicable(c->code, c->lds, true)) return 9;
-        if (c->kernel == 0 && sf) {
-            if (!p->early_term) return 11;
-            c->last_skipped = 11;
-        }
+        if (c->kernel == 0 && sf) return 11;
         return (c->kernel == 0 && lds_preferred(c->code, c->lds, true)) ? 7 : (c->kernel <= 1 ? 1 : -1);
     }
     const bool w1 = windowed_supported(c->code) && windowed_params_ok(p);
@@ -459,7 +456,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     if ((rc = ensure(&sc.d_V, &sc.V_bytes, v_bytes)) != LDPC_OK) return rc;
     if (kern != 8 && (rc = ensure(&sc.d_msg, &sc.msg_bytes, msg_zero)) != LDPC_OK) return rc;
     // early termination: live u8 | bad u32 | iterations used i32 (when the caller passed none)
-    const bool et_state = (kern == 5 || kern == 8) && p->early_term;
+    const bool et_state = (kern == 5 || kern == 8 || kern == 11) && p->early_term;
     if (et_state && (rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
     const bool et_staged = kern == 8 && p->early_term && coop3_et_stage_iters(batch, n_iter) > 0;
     if (et_staged && ((rc = ensure(&sc.d_V2, &sc.V2_bytes, 2 * v_bytes)) != LDPC_OK ||

@@ -11,9 +11,9 @@ struct StairfCode {
     int X = 0;               // information edges per check (check degree - 2)
     int m = 0;               // checks
     int x0 = 0;              // node of check 0's chain input (the tail check's parity edge)
-    // per group width S = 4, 8, 16 (null: not usable for this code):
+    // per group width S = 4, 8, 16, 2 (null: not usable for this code):
     // [M / S][(X + 3) / 2][S] u32: per check X info nodes, x node, o node (u16 pairs)
-    uint32_t *d_tab[3] = {nullptr, nullptr, nullptr};
+    uint32_t *d_tab[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 // plan + device table; leaves sc->valid false (and returns LDPC_OK) when the

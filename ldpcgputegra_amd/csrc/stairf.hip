@@ -8,8 +8,8 @@
 // kernel splits each check the way the int8 staircase kernels do:
 //
 // * a wave holds 64 / S codewords x S consecutive checks (lane = S *
-//   codeword + slot, slot = check within the group of S; S = 8 by default, 4
-//   and 16 selectable).  The info edges of the S
+//   codeword + slot, slot = check within the group of S; S = 2, 4, 8 or 16
+//   by batch size, stairf_width).  The info edges of the S
 //   checks (no two checks closer than the code's hazard distance share an
 //   info node) and the o edge (the parity node the next check reads; its V
 //   is last iteration's) are independent: each lane reduces its check's info
@@ -47,6 +47,7 @@ struct StairfArgs {
     const uint32_t *tab;
     int G, T, stride, iters, x0;
     float beta;
+    const uint8_t *live;   // early termination: codewords still decoding (stores of the others are off)
 };
 
 template <int X, int S>
@@ -75,15 +76,19 @@ int p_of(int X)
     return 0;
 }
 
-int p_of_s(int X, int S) { return S == 4 ? p_of<4>(X) : S == 8 ? p_of<8>(X) : p_of<16>(X); }
-int s_index(int S) { return S == 4 ? 0 : S == 8 ? 1 : 2; }
+int p_of_s(int X, int S) { return S == 2 ? p_of<2>(X) : S == 4 ? p_of<4>(X) : S == 8 ? p_of<8>(X) : p_of<16>(X); }
+int s_index(int S) { return S == 2 ? 3 : S == 4 ? 0 : S == 8 ? 1 : 2; }
 
-template <bool NMS>
+// A: 0 OMS, 1 NMS, 2 OMS with beta = 0 (plain min-sum)
+template <int A>
 LDPC_DEV float cst(float x, float beta)
 {
-    // generic.hip check_f32: NMS min * beta, OMS max(min - beta, 0)
-    if constexpr (NMS)
+    // generic.hip check_f32: NMS min * beta, OMS max(min - beta, 0); with
+    // beta = 0 that is x itself (x = |c| >= +0: x - 0 = x, max(x, 0) = x)
+    if constexpr (A == 1)
         return x * beta;
+    else if constexpr (A == 2)
+        return x;
     else
         return fmaxf(x - beta, 0.0f);
 }
@@ -98,7 +103,7 @@ LDPC_DEV float rot_chain(float t, int step)
                                     : __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, false));
 }
 
-template <int X, bool NMS, int S>
+template <int X, int A, int S, bool ET>
 __global__ void __launch_bounds__(64) stairf_decode(StairfArgs a)
 {
     constexpr int W = SF<X, S>::W, E = SF<X, S>::E, P = SF<X, S>::P, C = 64 / S;
@@ -113,6 +118,11 @@ __global__ void __launch_bounds__(64) stairf_decode(StairfArgs a)
     char *Vw = (char *)(a.V + (size_t)wv * C);
     char *Mw = (char *)(a.msg + (size_t)wv * a.G * E * 64);
     const uint32_t *tl = a.tab + slot;
+    // early termination: a converged codeword's lanes keep computing (their
+    // loads are shared with live codewords' lanes) but store nothing; a wave
+    // whose codewords have all converged leaves at once
+    const bool alive = !ET || a.live[(size_t)wv * C + cwl];
+    if (ET && !__any(alive)) return;
     const int G = a.G;
     const long total = (long)a.iters * G;
     const float INF = __builtin_huge_valf();
@@ -165,29 +175,31 @@ __global__ void __launch_bounds__(64) stairf_decode(StairfArgs a)
         for (int s = 0; s < S; s++) {
             const float cs = rot_chain<S>(t, s) - mx;
             if (slot == s) cx = cs;
-            const float r = cst<NMS>(fminf(m1, fabsf(cs)), a.beta);
+            const float r = cst<A>(fminf(m1, fabsf(cs)), a.beta);
             t = co + ((sI ^ (cs < 0.0f)) ? -r : r);
         }
         const float ax = fabsf(cx);
         const bool nx = cx < 0.0f;
-        const float ro = cst<NMS>(fminf(m1, ax), a.beta);
+        const float ro = cst<A>(fminf(m1, ax), a.beta);
         const float mo = (sI ^ nx) ? -ro : ro;
-        const float rx = cst<NMS>(fminf(m1, ao), a.beta);
+        const float rx = cst<A>(fminf(m1, ao), a.beta);
         const float mxn = (sI ^ no) ? -rx : rx;
         const float mxo = fminf(ax, ao);
         const bool sx = sI ^ nx ^ no;
         char *mg = Mw + (size_t)gg * E * 256 + lm;
+        if (alive) {
 #pragma unroll
-        for (int j = 0; j < X; j++) {
-            const float r = cst<NMS>(fminf(av[j] == m1 ? m2 : m1, mxo), a.beta);
-            const float mj = (sx ^ (cv[j] < 0.0f)) ? -r : r;
-            *(float *)(mg + j * 256) = mj;
-            vref(node(ids, j)) = cv[j] + mj;
+            for (int j = 0; j < X; j++) {
+                const float r = cst<A>(fminf(av[j] == m1 ? m2 : m1, mxo), a.beta);
+                const float mj = (sx ^ (cv[j] < 0.0f)) ? -r : r;
+                *(float *)(mg + j * 256) = mj;
+                vref(node(ids, j)) = cv[j] + mj;
+            }
+            *(float *)(mg + X * 256) = mxn;
+            *(float *)(mg + (X + 1) * 256) = mo;
+            if (hasx) vref(node(ids, X)) = cx + mxn;
+            if (sto) vref(node(ids, X + 1)) = co + mo;
         }
-        *(float *)(mg + X * 256) = mxn;
-        *(float *)(mg + (X + 1) * 256) = mo;
-        if (hasx) vref(node(ids, X)) = cx + mxn;
-        if (sto) vref(node(ids, X + 1)) = co + mo;
     };
 
     // prologue: ids of groups 0 .. 2P-1, data of groups 0 .. P-1
@@ -211,22 +223,78 @@ __global__ void __launch_bounds__(64) stairf_decode(StairfArgs a)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the prefetches past the end
 }
 
-template <int X, int S>
-int launch_xs(const StairfArgs &a, int blocks, bool nms, hipStream_t s)
+template <int X, int S, bool ET>
+int launch_xse(const StairfArgs &a, int blocks, int algo, hipStream_t s)
 {
-    if (nms)
-        hipLaunchKernelGGL((stairf_decode<X, true, S>), dim3(blocks), dim3(64), 0, s, a);
+    if (algo == 1)
+        hipLaunchKernelGGL((stairf_decode<X, 1, S, ET>), dim3(blocks), dim3(64), 0, s, a);
+    else if (algo == 2)
+        hipLaunchKernelGGL((stairf_decode<X, 2, S, ET>), dim3(blocks), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((stairf_decode<X, false, S>), dim3(blocks), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((stairf_decode<X, 0, S, ET>), dim3(blocks), dim3(64), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int X>
-int launch_x(const StairfArgs &a, int S, int blocks, bool nms, hipStream_t s)
+template <int X, int S>
+int launch_xs(const StairfArgs &a, int blocks, int algo, hipStream_t s)
 {
-    return S == 4 ? launch_xs<X, 4>(a, blocks, nms, s)
-         : S == 8 ? launch_xs<X, 8>(a, blocks, nms, s)
-                  : launch_xs<X, 16>(a, blocks, nms, s);
+    return a.live ? launch_xse<X, S, true>(a, blocks, algo, s) : launch_xse<X, S, false>(a, blocks, algo, s);
+}
+
+// early termination (oracle_decode_f32: stop a codeword after the first
+// iteration whose hard decisions V > 0 satisfy every check): after each
+// one-iteration launch, every check of every live codeword is tested (one
+// lane per codeword, a chunk of checks per workgroup, the check's nodes
+// wave-uniform), any failing check marks the codeword bad; then live
+// codewords without a bad mark stop with that iteration count
+__global__ void __launch_bounds__(64) stairf_et_init_k(uint8_t *live, uint32_t *bad, int32_t *iters_used, int batch,
+                                                       int stride, int iters)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= stride) return;
+    live[b] = b < batch;
+    bad[b] = 0;
+    if (b < batch) iters_used[b] = iters;
+}
+
+__global__ void __launch_bounds__(64) stairf_syndrome_k(const float *V, const uint32_t *ev, const uint8_t *live,
+                                                        uint32_t *bad, int m, int d0, int chunk, int stride)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    const bool on = live[b] != 0;
+    if (!__any(on)) return;
+    const int c0 = blockIdx.y * chunk, c1 = min(m, c0 + chunk);
+    const float *Vb = V + b;
+    int fail = 0;
+    for (int c = c0; c < c1; c++) {
+        const uint32_t *e = ev + (size_t)c * d0;   // layered order: every check d0 edges apart, the tail last
+        const int d = c == m - 1 ? d0 - 1 : d0;
+        int par = 0;
+        for (int j = 0; j < d; j++) par ^= Vb[(size_t)e[j] * stride] > 0.0f;
+        fail |= par;
+    }
+    if (on && fail) bad[b] = 1;
+}
+
+__global__ void __launch_bounds__(64) stairf_et_step_k(uint8_t *live, uint32_t *bad, int32_t *iters_used, int batch,
+                                                       int it)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= batch) return;
+    if (live[b] && !bad[b]) {
+        live[b] = 0;
+        iters_used[b] = it;
+    }
+    bad[b] = 0;
+}
+
+template <int X>
+int launch_x(const StairfArgs &a, int S, int blocks, int algo, hipStream_t s)
+{
+    return S == 2 ? launch_xs<X, 2>(a, blocks, algo, s)
+         : S == 4 ? launch_xs<X, 4>(a, blocks, algo, s)
+         : S == 8 ? launch_xs<X, 8>(a, blocks, algo, s)
+                  : launch_xs<X, 16>(a, blocks, algo, s);
 }
 
 }  // namespace
@@ -249,7 +317,7 @@ int stairf_upload(const ldpc_code *h, StairfCode *sc)
         for (int j = 0; j < X; j++)
             if (par[ev(c, j)]) return LDPC_OK;
     const int W = (X + 3) / 2;
-    for (int S : {4, 8, 16}) {   // one table per group width the code allows
+    for (int S : {2, 4, 8, 16}) {   // one table per group width the code allows
         if (M % S || h->min_hazard < S * p_of_s(X, S)) continue;
         const int G = M / S;
         std::vector<uint32_t> tab((size_t)G * W * S, 0);
@@ -275,11 +343,11 @@ int stairf_upload(const ldpc_code *h, StairfCode *sc)
     sc->X = X;
     sc->m = M;
     sc->x0 = (int)ev(0, X);
-    sc->valid = sc->d_tab[0] || sc->d_tab[1] || sc->d_tab[2];
+    sc->valid = sc->d_tab[0] || sc->d_tab[1] || sc->d_tab[2] || sc->d_tab[3];
     return LDPC_OK;
 }
 
-// group width of a launch: LDPC_STAIRF_S (4 / 8 / 16) if set and the code has
+// group width of a launch: LDPC_STAIRF_S (2 / 4 / 8 / 16) if set and the code has
 // that table; else about one wave per CU: stride / (64 / S) ~ 256 waves.
 // Measured (DVB-S2 r1/2, 20 it, profiles/r04s_float_long.jsonl): batch 1024
 // S = 16 / 8 / 4: 40.9 / 48.6 / 79.0 ms; 4096: 181 / 118 / 84.0 ms; 16384:
@@ -290,7 +358,7 @@ int stairf_width(const StairfCode &sc, int stride)
     const char *e = getenv("LDPC_STAIRF_S");
     const int want = (e && *e) ? atoi(e) : stride >= 4096 ? 4 : stride >= 2048 ? 8 : 16;
     for (int S : {want, 8, 4, 16})
-        if ((S == 4 || S == 8 || S == 16) && sc.d_tab[s_index(S)]) return S;
+        if ((S == 2 || S == 4 || S == 8 || S == 16) && sc.d_tab[s_index(S)]) return S;
     return 0;
 }
 
@@ -313,7 +381,8 @@ size_t stairf_msg_bytes(const StairfCode &sc, int stride)
 
 int launch_stairf(const DecodeLaunch &L, const StairfCode &sc, hipStream_t s)
 {
-    if (!stairf_stride_ok(sc, L.n, L.stride) || L.vpitch != L.stride || L.early) return -1;
+    if (!stairf_stride_ok(sc, L.n, L.stride) || L.vpitch != L.stride) return -1;
+    if (L.early && (!L.live || !L.bad || !L.iters_used || !L.d_edge_var)) return -1;
     const int S = stairf_width(sc, L.stride);
     if (!S) return -1;
     StairfArgs a;
@@ -326,16 +395,35 @@ int launch_stairf(const DecodeLaunch &L, const StairfCode &sc, hipStream_t s)
     a.iters = L.iters;
     a.x0 = sc.x0;
     a.beta = L.beta;
-    const bool nms = L.algo == 1;
+    a.live = nullptr;
+    const int algo = L.algo == 1 ? 1 : L.beta == 0.0f ? 2 : 0;
     const int blocks = L.stride / (64 / S);
-    if (L.iters <= 0) return 0;
-    switch (sc.X) {
-    case 5: return launch_x<5>(a, S, blocks, nms, s);
-    case 8: return launch_x<8>(a, S, blocks, nms, s);
-    case 12: return launch_x<12>(a, S, blocks, nms, s);
-    case 20: return launch_x<20>(a, S, blocks, nms, s);
-    case 25: return launch_x<25>(a, S, blocks, nms, s);
-    case 28: return launch_x<28>(a, S, blocks, nms, s);
+    auto run = [&]() {
+        switch (sc.X) {
+        case 5: return launch_x<5>(a, S, blocks, algo, s);
+        case 8: return launch_x<8>(a, S, blocks, algo, s);
+        case 12: return launch_x<12>(a, S, blocks, algo, s);
+        case 20: return launch_x<20>(a, S, blocks, algo, s);
+        case 25: return launch_x<25>(a, S, blocks, algo, s);
+        case 28: return launch_x<28>(a, S, blocks, algo, s);
+        }
+        return -1;
+    };
+    if (!L.early) return L.iters <= 0 ? 0 : run();
+    // early termination: one launch per iteration, then the syndrome
+    const int cb = L.stride / 64;
+    hipLaunchKernelGGL(stairf_et_init_k, dim3(cb), dim3(64), 0, s, L.live, L.bad, L.iters_used, L.batch, L.stride,
+                       L.iters);
+    if (hipGetLastError() != hipSuccess) return -1;
+    const int chunks = std::max(1, std::min(sc.m, 4096 / cb)), chunk = (sc.m + chunks - 1) / chunks;
+    a.iters = 1;
+    a.live = L.live;
+    for (int it = 1; it <= L.iters; it++) {
+        if (run()) return -1;
+        hipLaunchKernelGGL(stairf_syndrome_k, dim3(cb, (sc.m + chunk - 1) / chunk), dim3(64), 0, s, (const float *)L.V,
+                           L.d_edge_var, L.live, L.bad, sc.m, sc.X + 2, chunk, L.stride);
+        hipLaunchKernelGGL(stairf_et_step_k, dim3(cb), dim3(64), 0, s, L.live, L.bad, L.iters_used, L.batch, it);
+        if (hipGetLastError() != hipSuccess) return -1;
     }
-    return -1;
+    return 0;
 }

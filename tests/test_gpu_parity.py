@@ -316,7 +316,7 @@ def test_stairf_vs_oracle(code, algo, beta, batch, iters, monkeypatch):
     """Float staircase kernel (11, stairf.hip): the float default for the
     DVB-S2 codes (no early termination) against the oracle's serial float
     decode (oracle/ldpc_oracle.c), every DVB-S2 check degree it is built for,
-    every group width (LDPC_STAIRF_S 4 / 8 / 16: 16 / 8 / 4 codewords per wave;
+    every group width (LDPC_STAIRF_S 2 / 4 / 8 / 16: 32 / 16 / 8 / 4 codewords per wave;
     a code whose check count 16 does not divide runs its fallback width);
     iteration counts that are not multiples of its prefetch block; batches that
     leave part of a wave empty; bit-identical soft output."""
@@ -327,7 +327,7 @@ def test_stairf_vs_oracle(code, algo, beta, batch, iters, monkeypatch):
     llr = (-1.0 + sigma * rng.standard_normal((batch, t.n))).astype(np.float32)
     o_algo = O.NMS if algo == ALGO_NMS else O.OMS
     ref_hard, ref_soft, _ = O.decode_f32(t, llr, iters, o_algo, beta)
-    for k, width in ((0, None), (11, 4), (11, 8), (11, 16)):
+    for k, width in ((0, None), (11, 2), (11, 4), (11, 8), (11, 16)):
         if width:
             monkeypatch.setenv("LDPC_STAIRF_S", str(width))
         dec = decoder(code, k, max(64, batch))
@@ -341,6 +341,40 @@ def test_stairf_vs_oracle(code, algo, beta, batch, iters, monkeypatch):
         assert np.array_equal(soft.view(np.uint32), ref_soft.view(np.uint32)), \
             "kernel %d width %s: %d values differ" % (k, width, int((soft != ref_soft).sum()))
         assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
+
+
+@pytest.mark.parametrize("code,algo,beta,ebn0,iters", [("dvbs2_r1_2", ALGO_MS, 0.0, 2.0, 9),
+                                                       ("dvbs2_r1_2", ALGO_NMS, 0.75, 2.0, 12),
+                                                       ("dvbs2_r2_3", ALGO_OMS, 0.15, 2.6, 12)])
+def test_stairf_early_termination_vs_oracle(code, algo, beta, ebn0, iters, monkeypatch):
+    """Float staircase kernel with early termination (one launch per
+    iteration, then a syndrome pass over the live codewords): iterations used,
+    soft output and hard decisions equal the oracle's per-codeword stop
+    (oracle/ldpc_oracle.c: syndrome after every iteration), at every group
+    width; some codewords stop early, some run to the limit."""
+    torch = _torch()
+    t = load_table(code)
+    batch = 70
+    rng = np.random.default_rng(23)
+    llr = (-1.0 + channel.sigma_from_ebn0(ebn0, t.k_info / t.n) * rng.standard_normal((batch, t.n))).astype(np.float32)
+    o_algo = O.NMS if algo == ALGO_NMS else O.OMS
+    ref_hard, ref_soft, ref_its = O.decode_f32(t, llr, iters, o_algo, beta, early_term=True, threads=O.host_threads())
+    assert ref_its.min() < iters
+    for k, width in ((0, None), (11, 2), (11, 4), (11, 8), (11, 16)):
+        if width:
+            monkeypatch.setenv("LDPC_STAIRF_S", str(width))
+        dec = decoder(code, k, 128)
+        d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+        d_soft = torch.empty((batch, t.n), dtype=torch.float32, device="cuda")
+        d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
+        dec.decode_f32_device(torch.from_numpy(llr).cuda(), d_hard, iters,
+                              params=default_params(algo=algo, beta=beta, early_term=1), soft=d_soft, iters_used=d_its)
+        torch.cuda.synchronize()
+        assert dec.last_kernel == "stairf"
+        assert np.array_equal(d_its.cpu().numpy(), ref_its), "width %s" % width
+        soft = d_soft.cpu().numpy()
+        assert np.array_equal(soft.view(np.uint32), ref_soft.view(np.uint32)), "width %s" % width
+        assert np.array_equal(d_hard.cpu().numpy(), ref_hard), "width %s" % width
 
 
 @pytest.mark.parametrize("code,batch", [("648x324", 1024), ("576x288", 37)])
