@@ -348,15 +348,18 @@ int stairf_upload(const ldpc_code *h, StairfCode *sc)
 }
 
 // group width of a launch: LDPC_STAIRF_S (2 / 4 / 8 / 16) if set and the code has
-// that table; else about one wave per CU: stride / (64 / S) ~ 256 waves.
-// Measured (DVB-S2 r1/2, 20 it, profiles/r04s_float_long.jsonl): batch 1024
-// S = 16 / 8 / 4: 40.9 / 48.6 / 79.0 ms; 4096: 181 / 118 / 84.0 ms; 16384:
-// 839 / 507 / 357 ms (narrower pieces of V cost HBM efficiency once the
-// chip is full: 64-B pieces at S = 4, 16-B at S = 16)
+// that table; else by batch: the widest pieces of V (S = 2: 32 codewords =
+// whole 128-B lines) once there are enough waves to fill the chip, narrower
+// groups (more waves per codeword) below that.  Measured (DVB-S2 r1/2, 20 it,
+// plain min-sum, profiles/r04t_float_long.jsonl), S = 2 / 4 / 8 / 16:
+//   batch  1024: 131.4 / 73.3 / 45.9 / 40.2 ms
+//   batch  2048: 132.8 / 74.9 / 53.7 / 67.1
+//   batch  4096: 137.5 / 80.1 / 117.8 / 179.9
+//   batch 16384: 234.3 / 356.1 / 507.2 / 830.3 (S = 2: 4.73 TB/s of HBM traffic)
 int stairf_width(const StairfCode &sc, int stride)
 {
     const char *e = getenv("LDPC_STAIRF_S");
-    const int want = (e && *e) ? atoi(e) : stride >= 4096 ? 4 : stride >= 2048 ? 8 : 16;
+    const int want = (e && *e) ? atoi(e) : stride >= 8192 ? 2 : stride >= 4096 ? 4 : stride >= 2048 ? 8 : 16;
     for (int S : {want, 8, 4, 16})
         if ((S == 2 || S == 4 || S == 8 || S == 16) && sc.d_tab[s_index(S)]) return S;
     return 0;
