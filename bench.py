@@ -472,7 +472,8 @@ def main():
         except (OSError, ValueError):
             pass
         out = {
-            "metric": ("decoded Mbit/s, configs[1]: %s float min-sum, %d iters" % (a.code, a.iters) if f32 else
+            "metric": (("decoded Mbit/s, configs[1]: %s float min-sum, %d iters" if a.code == "648x324" else
+                        "decoded Mbit/s, %s float min-sum, %d iters") % (a.code, a.iters) if f32 else
                        "decoded Mbit/s + BER@SNR, DVB-S2 N=64800 r=1/2, 50 iters, 1/2/4/8 MI355X"),
             "value": round(value, 3),
             "unit": "Mbit/s",
@@ -511,6 +512,10 @@ def main():
             out["roofline"]["note"] = ("HBM is not the limiter: real traffic (PMC) is ~0.66x the algorithmic bytes "
                                        "at ~3.5 TB/s; the period is set by VALU issue + LDS latency of the slab "
                                        "waves, the chain wave's serial steps and the memory wave's issue")
+        if dec.last_kernel == "stairf":
+            out["roofline"]["note"] = ("float staircase kernel: HBM-bound once the chip is full (16384 codewords at "
+                                       "width 2: 4.73 TB/s of real traffic); below that per-wave VALU issue and the "
+                                       "chain's dependent steps (DESIGN.md, stairf)")
         if dec.last_kernel in ("lds", "ldsep"):
             # the LDS-resident kernel keeps V and the messages in LDS: HBM sees
             # only LLRs in / hard decisions out (the measured traffic), so the
