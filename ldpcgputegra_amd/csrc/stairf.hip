@@ -98,9 +98,12 @@ LDPC_DEV float cst(float x, float beta)
 template <int S>
 LDPC_DEV float rot_chain(float t, int step)
 {
+    // bound_ctrl: lanes whose source is outside the row read 0 (none of them is
+    // the step's valid slot), which lets the move fold into the subtract that
+    // consumes it (v_sub_f32_dpp): one dependent instruction less per step
     const int v = __float_as_int(t);
-    return __int_as_float(step == 0 ? __builtin_amdgcn_mov_dpp(v, 0x100 + S - 1, 0xF, 0xF, false)
-                                    : __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, false));
+    return __int_as_float(step == 0 ? __builtin_amdgcn_update_dpp(0, v, 0x100 + S - 1, 0xF, 0xF, true)
+                                    : __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true));
 }
 
 template <int X, int A, int S, bool ET>
