@@ -26,6 +26,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+def source_hash():
+    from ldpcgputegra_amd._lib import source_hash as h
+    return h()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,6 +139,47 @@ def cpu_baseline(code_name, iters, budget_s, threads, seed):
                        "%s logical CPUs); the all-core figure is per-thread rate x physical cores, a projection, "
                        "not a measurement" % (code_name, iters, done, threads, el, done1, el1, host["cpu_quota"],
                                               host["logical_cpus"]))
+
+
+def cpu_baseline_product_host(code_name, iters, budget_s, threads, seed):
+    """The product's own host decoder (a device -1 context of the C-ABI,
+    csrc/host.cpp: AVX2, 32 codewords per block, one block per thread at a
+    time) on the same threads and inputs as cpu_baseline -- the drop-in for a
+    machine without a GPU, timed like the reference's per-thread loop
+    (code/x86/main_p.cpp:664-765).  Product code, not the oracle."""
+    from ldpcgputegra_amd import Code, Decoder, channel, load_table
+    t = load_table(code_name)
+    table = channel.i8_table(channel.sigma_from_ebn0(1.0, t.k_info / t.n))
+
+    def rate(thr, budget):
+        os.environ["LDPC_HOST_THREADS"] = str(thr)
+        blk = 32 * thr                     # one 32-codeword block per thread per round
+        llr = channel.awgn_i8_host(t.n, blk, seed, table)
+        dec = Decoder(Code(code_name), device=-1, max_batch=blk)
+        dec.decode_i8(llr[:32], 1)         # untimed: first touch
+        done, t0 = 0, time.perf_counter()
+        while True:
+            dec.decode_i8(llr, iters)
+            done += blk
+            el = time.perf_counter() - t0
+            if el >= budget:
+                dec.close()
+                return done, el
+
+    old = os.environ.get("LDPC_HOST_THREADS")
+    try:
+        done1, el1 = rate(1, max(1.0, budget_s * 0.25))
+        done, el = rate(threads, budget_s)
+    finally:
+        if old is None:
+            os.environ.pop("LDPC_HOST_THREADS", None)
+        else:
+            os.environ["LDPC_HOST_THREADS"] = old
+    return dict(value=round(done * t.n / el / 1e6, 3), unit="Mbit/s", cores=threads, kind="product-host",
+                threads=threads, per_thread_mbps=round(done1 * t.n / el1 / 1e6, 3),
+                sample="%s %d it int8 OMS offset 1 on the product's device -1 host decoder: %d codewords "
+                       "(%d threads x 32-codeword blocks) in %.2f s; 1 thread: %d codewords in %.2f s"
+                       % (code_name, iters, done, threads, el, done1, el1))
 
 
 def cpu_baseline_f32(code_name, iters, budget_s, threads, seed):
@@ -288,6 +334,7 @@ def bench_mixed(a, rank, world, local, torch, dist):
                              avg_iters=float(it[sel].mean()), ber=float(e.sum()) / (sel.sum() * code.k_info),
                              fer=float((e > 0).mean()),
                              kernel=mx.last_kernels()[c],
+                             et_first_stage=mx.last_et_stages()[c],   # > 0: staged early termination (coop3)
                              kernel_ms=round(kt[c][0] / kt[c][1], 4) if kt[c][1] else None))
         alg_bytes += float((4.0 * code.e * it[sel] + 2.0 * N).sum())
         be_tot += int(e.sum())
@@ -303,7 +350,10 @@ def bench_mixed(a, rank, world, local, torch, dist):
                       % ", ".join(n.split("_", 1)[1].replace("_", "/") for n in names),
             "value": round(value, 3), "unit": "Mbit/s", "n_gpus": world,
             "ranks_seen": dist.get_world_size() if dist.is_initialized() else 1, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(el / a.steps * 1e3, 4),
+            # per 4096 codewords: comparable with the fixed-50 configs[2] step at batch 4096
+            "ms_per_4096_codewords": round(el / a.steps * 1e3 * 4096 / B, 4),
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int8",
             "data": "synthetic (device AWGN generator, all-zero codeword per rate)" + (
                 "; r3/4 and r5/6 are DVB-S2-shaped stand-ins (Annex-B structure, seeded random addresses: "
@@ -323,10 +373,13 @@ def bench_mixed(a, rank, world, local, torch, dist):
                          "algorithmic_bytes_per_step": alg_bytes},
             "cpu_baseline": None,
         }
+        src = source_hash()
+        out["build"] = {"src_sha16": src}
         try:
             tr = json.load(open(a.traffic_file))
-            out["roofline"]["traffic"] = tr.get("mixed_%s_b%d_it%d" % (a.mixed_codes, B, a.iters),
-                                                {}).get("hbm_bytes_per_step")
+            ent = tr.get("mixed_%s_b%d_it%d" % (a.mixed_codes, B, a.iters), {})
+            if ent.get("src_sha16") == src:
+                out["roofline"]["traffic"] = ent.get("hbm_bytes_per_step")
         except (OSError, ValueError):
             pass
         if world == 1 and a.cpu_seconds > 0:
@@ -464,11 +517,21 @@ def main():
             alg_bytes = B * (4.0 * E * a.iters + 2.0 * N)
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9     # GB/s
         peak = hbm_peak_gbs()
-        traffic = None
+        # PMC traffic of this exact build: profiles/traffic.json entries carry
+        # the source hash of the library they were measured on (tools/
+        # summarize_profiles.py); a different build gets null, not a stale number
+        traffic, traffic_note = None, None
+        src = source_hash()
         try:
             tr = json.load(open(a.traffic_file))
             key = "%s_b%d_it%d_%s" % (a.code, B, a.iters, dec.last_kernel)
-            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+            ent = tr.get(key, {})
+            if ent.get("src_sha16") == src:
+                traffic = ent.get("hbm_bytes_per_launch")
+                traffic_note = "PMC FETCH/WRITE passes on this build: %s" % ent.get("source")
+            elif ent:
+                traffic_note = ("no PMC pass for this build (src %s); last measured on src %s: %s"
+                                % (src, ent.get("src_sha16"), ent.get("source")))
         except (OSError, ValueError):
             pass
         out = {
@@ -501,9 +564,10 @@ def main():
             "info_mbps": round(value * code.k_info / N, 3),
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": peak, "unit": "GB/s",
-                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_note,
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": alg_bytes,
             },
+            "build": {"src_sha16": src},
         }
         if dec.last_kernel == "coop3":
             # priced against HBM as the contract asks; what limits the kernel is
@@ -526,7 +590,7 @@ def main():
             lds_peak = lds_peak_gbs()
             out["roofline"] = {
                 "bound": "lds", "achieved": round(achieved, 2), "peak": lds_peak, "unit": "GB/s",
-                "frac": round(achieved / lds_peak, 4), "traffic": traffic,
+                "frac": round(achieved / lds_peak, 4), "traffic": traffic, "traffic_source": traffic_note,
                 "hbm_achieved": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic else None,
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": alg_bytes,
                 "note": ("algorithmic bytes are on-chip traffic (V in LDS, messages in VGPRs: neither leaves the CU); "
@@ -541,6 +605,9 @@ def main():
             thr = a.cpu_threads or O.host_threads()
             out["cpu_baseline"] = (cpu_baseline_f32(a.code, a.iters, a.cpu_seconds, thr, a.seed) if f32 else
                                    cpu_baseline(a.code, a.iters, a.cpu_seconds, thr, a.seed))
+            if not f32:   # beside the reference: the product's own host decoder (device -1)
+                out["cpu_baseline_product_host"] = cpu_baseline_product_host(a.code, a.iters, a.cpu_seconds * 0.5,
+                                                                             thr, a.seed)
         else:
             out["cpu_baseline"] = None
         if world > 1:   # one entry per rank: its device and its own decode-kernel time

@@ -185,6 +185,11 @@ int ldpc_ctx_last_kernel(ldpc_ctx *ctx, int *kernel);
  * not use for the call's parameters (8: coop3, 5: coop -- they take OMS / MS
  * with msg_max <= 63 and var range +-127), 0 when none was skipped. */
 int ldpc_ctx_last_skipped(ldpc_ctx *ctx, int *kernel);
+/* Early termination of the last decode on coop3 (kernel 8): the iterations of
+ * its first stage when it ran staged (batches >= LDPC_COOP3_ET_STAGE_MIN, default
+ * 8192 codewords: the codewords still decoding compacted every
+ * LDPC_COOP3_ET_STEP iterations), 0 when it ran as one launch. */
+int ldpc_ctx_last_et_stage(ldpc_ctx *ctx, int *first_stage_iters);
 /* Kernel timing (bench / profiling): when enabled, every decode records HIP
  * events around the decode kernel on the stream it is launched on;
  * ldpc_ctx_kernel_time returns the summed kernel time and launch count since
@@ -210,10 +215,13 @@ int ldpc_decode_f32(ldpc_ctx *ctx, const float *llr, uint8_t *hard, int batch, i
  * CGPU_Decoder_MS_SIMD.cu:219-275, without its blocking copies).  llr / hard
  * should be page-locked (ldpc_host_alloc): pageable buffers make the copies
  * synchronous.  The context's device staging and scratch are reused by its
- * next call, so the calls on one context must use one stream; two contexts
- * keep two batches in flight (H2D of batch k+1 and D2H of batch k-1 under the
- * decode of batch k).  ldpc_ctx_synchronize waits for the context's last
- * host_async call; hard is valid after it. */
+ * next call: each call records an event of the context's own after its D2H
+ * copy, and the next call's stream waits for that event before reusing them
+ * (so calls on one context may use different streams, but they serialise);
+ * two contexts keep two batches in flight (H2D of batch k+1 and D2H of batch
+ * k-1 under the decode of batch k).  ldpc_ctx_synchronize (and
+ * ldpc_ctx_destroy) wait on that event, never on the caller's stream; hard is
+ * valid after it. */
 int ldpc_decode_i8_host_async(ldpc_ctx *ctx, void *hip_stream, const int8_t *llr, uint8_t *hard, int batch,
                               int n_iter, const ldpc_params *p);
 int ldpc_decode_f32_host_async(ldpc_ctx *ctx, void *hip_stream, const float *llr, uint8_t *hard, int batch,
@@ -265,6 +273,8 @@ int ldpc_decode_i8_mixed_async(ldpc_mixed *mx, void *hip_stream, const int8_t *d
 /* Kernel family the last mixed decode ran for code `code_index` (numbering of
  * ldpc_ctx_last_kernel; 0 if that code had no codewords in any decode yet). */
 int ldpc_mixed_last_kernel(ldpc_mixed *mx, int code_index, int *kernel);
+/* ldpc_ctx_last_et_stage of code `code_index`'s context. */
+int ldpc_mixed_last_et_stage(ldpc_mixed *mx, int code_index, int *first_stage_iters);
 /* Per-code decode-kernel timing (ldpc_ctx_profile / ldpc_ctx_kernel_time of
  * the code's context): the decode launches only, not the gather / scatter. */
 int ldpc_mixed_profile(ldpc_mixed *mx, int enable);

@@ -16,6 +16,23 @@ LDPC_OK, LDPC_EINVAL, LDPC_EUNSUPPORTED, LDPC_EDEVICE, LDPC_ENOMEM, LDPC_EIO = 0
 ALGO_OMS, ALGO_NMS, ALGO_MS = 0, 1, 2
 
 
+def source_hash():
+    """sha256 (16 hex digits) over the sources the library is built from
+    (csrc/* and include/*): ties a committed measurement (profiles/traffic.json)
+    to the exact kernel code it was taken on."""
+    import hashlib
+    root = os.path.dirname(_HERE)
+    h = hashlib.sha256()
+    for d in (os.path.join(_HERE, "csrc"), os.path.join(root, "include")):
+        for f in sorted(os.listdir(d)):
+            fp = os.path.join(d, f)
+            if os.path.isfile(fp):
+                h.update(f.encode())
+                with open(fp, "rb") as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 class LdpcError(RuntimeError):
     def __init__(self, status, msg):
         super().__init__("%s (%d): %s" % (_strerror(status), status, msg))
@@ -59,6 +76,7 @@ SIGNATURES = {
     "ldpc_ctx_get_kernel": (I, [P, C.POINTER(I)]),
     "ldpc_ctx_last_kernel": (I, [P, C.POINTER(I)]),
     "ldpc_ctx_last_skipped": (I, [P, C.POINTER(I)]),
+    "ldpc_ctx_last_et_stage": (I, [P, C.POINTER(I)]),
     "ldpc_ctx_profile": (I, [P, I]),
     "ldpc_ctx_kernel_time": (I, [P, C.POINTER(C.c_double), C.POINTER(I), I]),
     "ldpc_decode_i8": (I, [P, P, P, I, I, C.POINTER(ldpc_params)]),
@@ -70,6 +88,7 @@ SIGNATURES = {
     "ldpc_mixed_destroy": (None, [P]),
     "ldpc_decode_i8_mixed_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params)]),
     "ldpc_mixed_last_kernel": (I, [P, I, C.POINTER(I)]),
+    "ldpc_mixed_last_et_stage": (I, [P, I, C.POINTER(I)]),
     "ldpc_mixed_profile": (I, [P, I]),
     "ldpc_mixed_kernel_time": (I, [P, I, C.POINTER(C.c_double), C.POINTER(I), I]),
     "ldpc_dvbs2_encode": (I, [P, P, P, I]),

@@ -71,6 +71,7 @@ struct ldpc_ctx {
                                     // 9 ldsep (edge-parallel float)
                                     // (4 and 6, windowed2 S32 and coop2, were superseded and removed)
     int last_kernel = 0;
+    int last_et_stage = 0;          // coop3 staged early termination: first-stage iterations (0: one launch)
     int last_skipped = 0;   // the preferred kernel the last decode could not use at its batch size (0: none)
     int lds_pad = 0;        // extra dynamic LDS per windowed2 workgroup (ldpc_ctx_set_lds_pad)
     hipStream_t stream = nullptr;
@@ -89,8 +90,11 @@ struct ldpc_ctx {
     // host-buffer API pipeline (decode_host): chunk i of a batch runs on lane
     // i % lanes.size(): its own stream, scratch and input / output staging
     std::vector<Lane> lanes;
-    // asynchronous host-buffer API: the stream of the last call (ldpc_ctx_synchronize)
-    hipStream_t host_stream = nullptr;
+    // asynchronous host-buffer API: an event of the context's own, recorded
+    // after each call's D2H copy (ldpc_ctx_synchronize / destroy wait on it,
+    // never on the caller's stream, which may be gone by then; a call on
+    // another stream waits on it before reusing d_io and the scratch)
+    hipEvent_t host_done = nullptr;
     bool host_pending = false;
     // kernel timing (ldpc_ctx_profile)
     bool profile = false;
@@ -196,7 +200,8 @@ extern "C" void ldpc_ctx_destroy(ldpc_ctx *c)
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->host_pending) (void)hipStreamSynchronize(c->host_stream);
+    if (c->host_pending) (void)hipEventSynchronize(c->host_done);
+    if (c->host_done) (void)hipEventDestroy(c->host_done);
     windowed_code_free(&c->wcode);
     windowed2_free(&c->w16);
     coop_free(&c->coop);
@@ -305,6 +310,13 @@ extern "C" int ldpc_ctx_last_skipped(ldpc_ctx *c, int *k)
 {
     if (!c || !k) return ldpc_set_error(LDPC_EINVAL, "NULL");
     *k = c->last_skipped;
+    return LDPC_OK;
+}
+
+extern "C" int ldpc_ctx_last_et_stage(ldpc_ctx *c, int *k)
+{
+    if (!c || !k) return ldpc_set_error(LDPC_EINVAL, "NULL");
+    *k = c->last_et_stage;
     return LDPC_OK;
 }
 
@@ -459,6 +471,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     const bool et_state = (kern == 5 || kern == 8 || kern == 11) && p->early_term;
     if (et_state && (rc = ensure(&sc.d_early, &sc.early_bytes, (size_t)stride * 12)) != LDPC_OK) return rc;
     const bool et_staged = kern == 8 && p->early_term && coop3_et_stage_iters(batch, n_iter) > 0;
+    if (!alloc_only) c->last_et_stage = et_staged ? coop3_et_stage_iters(batch, n_iter) : 0;
     if (et_staged && ((rc = ensure(&sc.d_V2, &sc.V2_bytes, 2 * v_bytes)) != LDPC_OK ||
                       (rc = ensure(&sc.d_et2, &sc.et2_bytes, (size_t)stride * 20 + 256)) != LDPC_OK))
         return rc;
@@ -724,17 +737,24 @@ static int decode_host_async(ldpc_ctx *c, void *sv, const void *llr, uint8_t *ha
     const size_t in_al = ((size_t)batch * n * esz + 255) / 256 * 256;
     // size the staging and the scratch before anything is queued (a hipFree of
     // a buffer the previous call still uses would wait for the device anyway)
+    if (!c->host_done) HIP_TRY(hipEventCreateWithFlags(&c->host_done, hipEventDisableTiming));
+    // a previous call (possibly on another stream) still using d_io / the scratch:
+    // resizing frees them, so wait for it on the host; otherwise order this
+    // stream after it on the device
+    const bool grow = c->io_bytes < in_al + (size_t)batch * n;
+    if (c->host_pending && grow) HIP_TRY(hipEventSynchronize(c->host_done));
     if ((rc = ensure(&c->d_io, &c->io_bytes, in_al + (size_t)batch * n)) != LDPC_OK) return rc;
     if ((rc = decode_device(c, c->sc, s, c->d_io, nullptr, nullptr, nullptr, batch, n_iter, p, is_float, true)) !=
         LDPC_OK)
         return rc;
+    if (c->host_pending) HIP_TRY(hipStreamWaitEvent(s, c->host_done, 0));
     char *d_in = (char *)c->d_io, *d_out = d_in + in_al;
     HIP_TRY(hipMemcpyAsync(d_in, llr, (size_t)batch * n * esz, hipMemcpyHostToDevice, s));
     if ((rc = decode_device(c, c->sc, s, d_in, (uint8_t *)d_out, nullptr, nullptr, batch, n_iter, p, is_float)) !=
         LDPC_OK)
         return rc;
     HIP_TRY(hipMemcpyAsync(hard, d_out, (size_t)batch * n, hipMemcpyDeviceToHost, s));
-    c->host_stream = s;
+    HIP_TRY(hipEventRecord(c->host_done, s));
     c->host_pending = true;
     return LDPC_OK;
 }
@@ -757,7 +777,7 @@ extern "C" int ldpc_ctx_synchronize(ldpc_ctx *c)
     if (!c->host_pending) return LDPC_OK;
     HIP_TRY(hipSetDevice(c->device));
     c->host_pending = false;
-    HIP_TRY(hipStreamSynchronize(c->host_stream));
+    HIP_TRY(hipEventSynchronize(c->host_done));
     return LDPC_OK;
 }
 

@@ -1625,8 +1625,11 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
         const int32_t *src_its = L.iters_used, *src_map = nullptr;
         const int *src_n = nullptr;
         int done = k1;
-        for (int st = 0; done < L.iters && st < 64; st++) {
-            const int k = std::min(step, L.iters - done), b = st & 1;
+        // at most 64 stages (one counter each in et2): the 64th takes every
+        // iteration left, so the decode always reaches L.iters
+        constexpr int MAX_STAGES = 64;
+        for (int st = 0; done < L.iters; st++) {
+            const int k = st == MAX_STAGES - 1 ? L.iters - done : std::min(step, L.iters - done), b = st & 1;
             const bool last = done + k >= L.iters;
             if (hipMemsetAsync(count + st, 0, sizeof(int), s) != hipSuccess) return -1;
             hipLaunchKernelGGL(et_select_k, dim3((S + 255) / 256), dim3(256), 0, s, src_its, L.batch, src_n, src_map,

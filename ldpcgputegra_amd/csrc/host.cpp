@@ -7,9 +7,9 @@
 // CDecoder_NMS_fixed_SSE.cpp:125-368), bit-exact for
 // int8.  Written for the host's wide vector unit: 32 codewords per AVX2
 // register (the reference's SSE decoder does 16), V[N][32] and msg[E][32]
-// interleaved per block of 32 codewords, blocks spread over host threads.  A
-// portable loop over the 32 lanes (the same operations, one byte at a time)
-// runs where AVX2 is absent.  The float path is scalar per codeword.
+// interleaved per block of 32 codewords (16 where only SSE4.1 is present),
+// blocks spread over host threads.  A portable loop over the lanes (the same operations, one byte at
+// a time) runs where neither is available (LDPC_HOST_PORTABLE forces it).  The float path is scalar per codeword.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -22,7 +22,7 @@
 
 namespace {
 
-constexpr int HB = 32;   // codewords per block (one AVX2 register of int8)
+constexpr int HB = 32;   // most codewords per block (one AVX2 register of int8)
 
 struct I8Params {
     int algo, param, var_min, msg_max, early;
@@ -38,16 +38,16 @@ inline int nms8(int mn, int f)   // packs_epi16((u16(min) * factor) >> 5)
     return s > 127 ? 127 : (s < -128 ? -128 : s);
 }
 
-// one check over the 32 lanes of a block, portable
+// one check over the W lanes of a block, portable
 template <bool ET>
 void check_portable(int8_t *V, int8_t *msg, const uint32_t *ev, int d, bool later, const I8Params &p,
-                    const uint8_t *live)
+                    const uint8_t *live, int W)
 {
     int c[64][HB], a[64][HB];
-    for (int l = 0; l < HB; l++) {
+    for (int l = 0; l < W; l++) {
         int sign = 0, min1 = 127, min2 = 127;
         for (int j = 0; j < d; j++) {
-            const int cj = std::max(sat8(V[(size_t)ev[j] * HB + l] - msg[j * HB + l]), p.var_min);
+            const int cj = std::max(sat8(V[(size_t)ev[j] * W + l] - msg[j * W + l]), p.var_min);
             const int aj = (p.algo == LDPC_ALGO_NMS || !later) ? std::min(abs8(cj), p.msg_max)
                                                                : abs8(std::min(cj, p.msg_max));
             sign ^= cj & 0x80;
@@ -71,104 +71,182 @@ void check_portable(int8_t *V, int8_t *msg, const uint32_t *ev, int d, bool late
             const int r = a[j][l] == min1 ? cst1 : cst2;
             const int sig = as_i8(sign ^ (c[j][l] & 0x80));   // never 0: bit 6 is set
             const int m = sig < 0 ? as_i8(-r) : r;
-            msg[j * HB + l] = (int8_t)m;
-            V[(size_t)ev[j] * HB + l] = (int8_t)std::max(sat8(c[j][l] + m), p.var_min);
+            msg[j * W + l] = (int8_t)m;
+            V[(size_t)ev[j] * W + l] = (int8_t)std::max(sat8(c[j][l] + m), p.var_min);
         }
     }
 }
 
-// NMS constants: (u16(min) * f) >> 5, signed-saturated to int8 (unpack / pack
-// stay inside each 128-bit lane, so the byte order is kept)
-__attribute__((target("avx2"))) inline __m256i nms_avx2(__m256i mn, __m256i f)
-{
-    const __m256i z = _mm256_setzero_si256();
-    const __m256i lo = _mm256_srli_epi16(_mm256_mullo_epi16(_mm256_unpacklo_epi8(mn, z), f), 5);
-    const __m256i hi = _mm256_srli_epi16(_mm256_mullo_epi16(_mm256_unpackhi_epi8(mn, z), f), 5);
-    return _mm256_packs_epi16(lo, hi);
-}
+// the SIMD check, written once over a vector-width trait: W = 32 lanes
+// (AVX2) or W = 16 (SSE4.1, the reference's width, where AVX2 is absent).
+// The edge loops are unrolled for the codes' degrees (check_dispatch): with a
+// runtime degree the contributions went through the stack and DVB-S2 r1/2
+// took 0.42 ns per edge and codeword on one thread, 0.31 unrolled.
+struct Avx2 {
+    static constexpr int W = 32;
+    using V = __m256i;
+    __attribute__((target("avx2"))) static V ld(const void *p) { return _mm256_load_si256((const V *)p); }
+    __attribute__((target("avx2"))) static void st(void *p, V v) { _mm256_store_si256((V *)p, v); }
+    __attribute__((target("avx2"))) static V set1(int x) { return _mm256_set1_epi8((char)x); }
+    __attribute__((target("avx2"))) static V zero() { return _mm256_setzero_si256(); }
+    __attribute__((target("avx2"))) static V subs(V a, V b) { return _mm256_subs_epi8(a, b); }
+    __attribute__((target("avx2"))) static V adds(V a, V b) { return _mm256_adds_epi8(a, b); }
+    __attribute__((target("avx2"))) static V subs_u(V a, V b) { return _mm256_subs_epu8(a, b); }
+    __attribute__((target("avx2"))) static V max(V a, V b) { return _mm256_max_epi8(a, b); }
+    __attribute__((target("avx2"))) static V min(V a, V b) { return _mm256_min_epi8(a, b); }
+    __attribute__((target("avx2"))) static V abs(V a) { return _mm256_abs_epi8(a); }
+    __attribute__((target("avx2"))) static V xor_(V a, V b) { return _mm256_xor_si256(a, b); }
+    __attribute__((target("avx2"))) static V and_(V a, V b) { return _mm256_and_si256(a, b); }
+    __attribute__((target("avx2"))) static V eq(V a, V b) { return _mm256_cmpeq_epi8(a, b); }
+    __attribute__((target("avx2"))) static V blend(V a, V b, V m) { return _mm256_blendv_epi8(a, b, m); }
+    __attribute__((target("avx2"))) static V sign(V a, V b) { return _mm256_sign_epi8(a, b); }
+    // NMS constants: (u16(min) * f) >> 5, signed-saturated to int8 (unpack /
+    // pack stay inside each 128-bit lane, so the byte order is kept)
+    __attribute__((target("avx2"))) static V nms(V mn, int f)
+    {
+        const V z = zero(), ff = _mm256_set1_epi16((short)f);
+        const V lo = _mm256_srli_epi16(_mm256_mullo_epi16(_mm256_unpacklo_epi8(mn, z), ff), 5);
+        const V hi = _mm256_srli_epi16(_mm256_mullo_epi16(_mm256_unpackhi_epi8(mn, z), ff), 5);
+        return _mm256_packs_epi16(lo, hi);
+    }
+};
+struct Sse4 {
+    static constexpr int W = 16;
+    using V = __m128i;
+    __attribute__((target("sse4.1"))) static V ld(const void *p) { return _mm_load_si128((const V *)p); }
+    __attribute__((target("sse4.1"))) static void st(void *p, V v) { _mm_store_si128((V *)p, v); }
+    __attribute__((target("sse4.1"))) static V set1(int x) { return _mm_set1_epi8((char)x); }
+    __attribute__((target("sse4.1"))) static V zero() { return _mm_setzero_si128(); }
+    __attribute__((target("sse4.1"))) static V subs(V a, V b) { return _mm_subs_epi8(a, b); }
+    __attribute__((target("sse4.1"))) static V adds(V a, V b) { return _mm_adds_epi8(a, b); }
+    __attribute__((target("sse4.1"))) static V subs_u(V a, V b) { return _mm_subs_epu8(a, b); }
+    __attribute__((target("sse4.1"))) static V max(V a, V b) { return _mm_max_epi8(a, b); }
+    __attribute__((target("sse4.1"))) static V min(V a, V b) { return _mm_min_epi8(a, b); }
+    __attribute__((target("sse4.1"))) static V abs(V a) { return _mm_abs_epi8(a); }
+    __attribute__((target("sse4.1"))) static V xor_(V a, V b) { return _mm_xor_si128(a, b); }
+    __attribute__((target("sse4.1"))) static V and_(V a, V b) { return _mm_and_si128(a, b); }
+    __attribute__((target("sse4.1"))) static V eq(V a, V b) { return _mm_cmpeq_epi8(a, b); }
+    __attribute__((target("sse4.1"))) static V blend(V a, V b, V m) { return _mm_blendv_epi8(a, b, m); }
+    __attribute__((target("sse4.1"))) static V sign(V a, V b) { return _mm_sign_epi8(a, b); }
+    __attribute__((target("sse4.1"))) static V nms(V mn, int f)
+    {
+        const V z = zero(), ff = _mm_set1_epi16((short)f);
+        const V lo = _mm_srli_epi16(_mm_mullo_epi16(_mm_unpacklo_epi8(mn, z), ff), 5);
+        const V hi = _mm_srli_epi16(_mm_mullo_epi16(_mm_unpackhi_epi8(mn, z), ff), 5);
+        return _mm_packs_epi16(lo, hi);
+    }
+};
 
-// the same check on AVX2, 32 lanes per instruction
-template <bool ET>
-__attribute__((target("avx2"))) void check_avx2(int8_t *V, int8_t *msg, const uint32_t *ev, int d, bool later,
-                                                const I8Params &p, const uint8_t *live)
+// one check over the W lanes of a block (OMS_fixed_SSE.cpp:201-254; later
+// groups :293-314; NMS_fixed_SSE.cpp:188-240); D > 0: the degree known at
+// compile time (the edge loops unrolled, contributions in registers), D = 0:
+// runtime degree d
+template <typename S, int D, bool ET>
+__attribute__((target("avx2,sse4.1"))) inline void check_simd(int8_t *V, int8_t *msg, const uint32_t *ev, int d,
+                                                              bool later, const I8Params &p, const uint8_t *live)
 {
-    const __m256i vmin = _mm256_set1_epi8((char)p.var_min), mm = _mm256_set1_epi8((char)p.msg_max);
-    const __m256i s80 = _mm256_set1_epi8((char)0x80);
+    using Vec = typename S::V;
+    constexpr int W = S::W;
+    const int dd = D > 0 ? D : d;
+    const Vec vmin = S::set1(p.var_min), mm = S::set1(p.msg_max), s80 = S::set1(0x80);
     const bool nms = p.algo == LDPC_ALGO_NMS;
-    __m256i c[64], a[64];
-    __m256i sign = _mm256_setzero_si256(), min1 = _mm256_set1_epi8(127), min2 = min1;
-    for (int j = 0; j < d; j++) {
-        const __m256i v = _mm256_load_si256((const __m256i *)(V + (size_t)ev[j] * HB));
-        const __m256i cj = _mm256_max_epi8(_mm256_subs_epi8(v, _mm256_load_si256((const __m256i *)(msg + j * HB))), vmin);
-        const __m256i aj = (nms || !later) ? _mm256_min_epi8(_mm256_abs_epi8(cj), mm)
-                                           : _mm256_abs_epi8(_mm256_min_epi8(cj, mm));
-        sign = _mm256_xor_si256(sign, _mm256_and_si256(cj, s80));
+    Vec c[D > 0 ? D : 64], a[D > 0 ? D : 64];
+    Vec sign = S::zero(), min1 = S::set1(127), min2 = min1;
+#pragma GCC unroll 32
+    for (int j = 0; j < dd; j++) {
+        const Vec v = S::ld(V + (size_t)ev[j] * W);
+        const Vec cj = S::max(S::subs(v, S::ld(msg + j * W)), vmin);
+        const Vec aj = (nms || !later) ? S::min(S::abs(cj), mm) : S::abs(S::min(cj, mm));
+        sign = S::xor_(sign, S::and_(cj, s80));
         c[j] = cj;
         a[j] = aj;
-        min2 = _mm256_min_epi8(min2, _mm256_max_epi8(aj, min1));
-        min1 = _mm256_min_epi8(min1, aj);
+        min2 = S::min(min2, S::max(aj, min1));
+        min1 = S::min(min1, aj);
     }
-    __m256i cst1, cst2;
+    Vec cst1, cst2;
     if (nms) {
-        const __m256i f = _mm256_set1_epi16((short)p.param);
-        cst1 = nms_avx2(min2, f);
-        cst2 = nms_avx2(min1, f);
+        cst1 = S::nms(min2, p.param);
+        cst2 = S::nms(min1, p.param);
     } else {
-        const __m256i off = _mm256_set1_epi8((char)p.param);
-        cst1 = _mm256_min_epi8(_mm256_subs_epu8(min2, off), mm);
-        cst2 = _mm256_min_epi8(_mm256_subs_epu8(min1, off), mm);
+        const Vec off = S::set1(p.param);
+        cst1 = S::min(S::subs_u(min2, off), mm);
+        cst2 = S::min(S::subs_u(min1, off), mm);
     }
-    sign = _mm256_xor_si256(sign, _mm256_set1_epi8((char)((d & 1) ? 0xC0 : 0x40)));
-    const __m256i keep = ET ? _mm256_cmpeq_epi8(_mm256_load_si256((const __m256i *)live), _mm256_setzero_si256())
-                            : _mm256_setzero_si256();
-    for (int j = 0; j < d; j++) {
-        const __m256i r = _mm256_blendv_epi8(cst2, cst1, _mm256_cmpeq_epi8(a[j], min1));
-        const __m256i m = _mm256_sign_epi8(r, _mm256_xor_si256(sign, _mm256_and_si256(c[j], s80)));
-        __m256i nv = _mm256_max_epi8(_mm256_adds_epi8(c[j], m), vmin);
-        int8_t *vp = V + (size_t)ev[j] * HB;
-        if (ET) nv = _mm256_blendv_epi8(nv, _mm256_load_si256((const __m256i *)vp), keep);   // converged: frozen
-        _mm256_store_si256((__m256i *)(msg + j * HB), m);
-        _mm256_store_si256((__m256i *)vp, nv);
+    sign = S::xor_(sign, S::set1((dd & 1) ? 0xC0 : 0x40));
+    const Vec keep = ET ? S::eq(S::ld(live), S::zero()) : S::zero();
+#pragma GCC unroll 32
+    for (int j = 0; j < dd; j++) {
+        const Vec r = S::blend(cst2, cst1, S::eq(a[j], min1));
+        const Vec m = S::sign(r, S::xor_(sign, S::and_(c[j], s80)));
+        Vec nv = S::max(S::adds(c[j], m), vmin);
+        int8_t *vp = V + (size_t)ev[j] * W;
+        if (ET) nv = S::blend(nv, S::ld(vp), keep);   // converged: frozen
+        S::st(msg + j * W, m);
+        S::st(vp, nv);
+    }
+}
+
+template <typename S, bool ET>
+inline void check_dispatch(int8_t *V, int8_t *msg, const uint32_t *ev, int d, bool later, const I8Params &p,
+                           const uint8_t *live)
+{
+    switch (d) {   // the degrees of the reference's codes (DVB-S2: 7, 10, 14, 22, 27, 30 and the tails)
+    case 3: return check_simd<S, 3, ET>(V, msg, ev, d, later, p, live);
+    case 6: return check_simd<S, 6, ET>(V, msg, ev, d, later, p, live);
+    case 7: return check_simd<S, 7, ET>(V, msg, ev, d, later, p, live);
+    case 8: return check_simd<S, 8, ET>(V, msg, ev, d, later, p, live);
+    case 10: return check_simd<S, 10, ET>(V, msg, ev, d, later, p, live);
+    case 14: return check_simd<S, 14, ET>(V, msg, ev, d, later, p, live);
+    case 22: return check_simd<S, 22, ET>(V, msg, ev, d, later, p, live);
+    default: return check_simd<S, 0, ET>(V, msg, ev, d, later, p, live);
     }
 }
 
 // lanes whose hard decisions satisfy every check
-void syndrome_ok(const ldpc_code *h, const int8_t *V, uint8_t *ok)
+void syndrome_ok(const ldpc_code *h, const int8_t *V, uint8_t *ok, int W)
 {
     uint8_t bad[HB] = {0};
     for (int i = 0; i < h->m; i++) {
         const uint32_t *ev = &h->edge_var[h->check_start[i]];
         uint8_t par[HB] = {0};
         for (int j = 0; j < h->check_deg[i]; j++) {
-            const int8_t *v = V + (size_t)ev[j] * HB;
-            for (int l = 0; l < HB; l++) par[l] ^= v[l] > 0;
+            const int8_t *v = V + (size_t)ev[j] * W;
+            for (int l = 0; l < W; l++) par[l] ^= v[l] > 0;
         }
-        for (int l = 0; l < HB; l++) bad[l] |= par[l];
+        for (int l = 0; l < W; l++) bad[l] |= par[l];
     }
-    for (int l = 0; l < HB; l++) ok[l] = !bad[l];
+    for (int l = 0; l < W; l++) ok[l] = !bad[l];
 }
 
 struct Scratch {
-    std::vector<int8_t> V, msg;   // V[N + 1][32] (64-B aligned rows), msg[E][32]
+    std::vector<int8_t> V, msg;   // V[N + 1][W] (64-B aligned), msg[E][W]
     int8_t *v = nullptr, *m = nullptr;
-    void size(const ldpc_code *h)
+    void size(const ldpc_code *h, int W)
     {
-        V.resize(((size_t)h->n + 2) * HB + 64);
-        msg.resize((size_t)h->e * HB + 64);
+        V.resize(((size_t)h->n + 2) * W + 64);
+        msg.resize((size_t)h->e * W + 64);
         v = (int8_t *)(((uintptr_t)V.data() + 63) & ~(uintptr_t)63);
         m = (int8_t *)(((uintptr_t)msg.data() + 63) & ~(uintptr_t)63);
     }
 };
 
-// one block of up to 32 codewords (frame-major in / out)
+#ifndef LDPC_HOST_PF
+#define LDPC_HOST_PF 2
+#endif
+constexpr int PF = LDPC_HOST_PF;   // checks ahead whose V rows are prefetched
+
+// SIMD path of a block: 32-lane AVX2, 16-lane SSE4.1, or the portable loop
+enum class Isa { avx2, sse4, portable };
+
+// one block of up to W codewords (frame-major in / out)
 void decode_block_i8(const ldpc_code *h, const int8_t *llr, uint8_t *hard, int nb, int iters, const I8Params &p,
-                     Scratch &s, bool avx2)
+                     Scratch &s, Isa isa, int W)
 {
     const int n = h->n;
-    s.size(h);
+    s.size(h, W);
     for (int i = 0; i < n; i++)
-        for (int l = 0; l < HB; l++) s.v[(size_t)i * HB + l] = l < nb ? llr[(size_t)l * n + i] : 0;
-    std::memset(s.m, 0, (size_t)h->e * HB);   // CDecoder_OMS_fixed_SSE.cpp:129-131
+        for (int l = 0; l < W; l++) s.v[(size_t)i * W + l] = l < nb ? llr[(size_t)l * n + i] : 0;
+    std::memset(s.m, 0, (size_t)h->e * W);   // CDecoder_OMS_fixed_SSE.cpp:129-131
     alignas(32) uint8_t live[HB];
     for (int l = 0; l < HB; l++) live[l] = l < nb;
     for (int it = 0; it < iters; it++) {
@@ -177,19 +255,27 @@ void decode_block_i8(const ldpc_code *h, const int8_t *llr, uint8_t *hard, int n
             const int d = h->check_deg[i];
             const bool later = h->check_group[i] > 0;
             const uint32_t *ev = &h->edge_var[h->check_start[i]];
-            int8_t *mp = s.m + e0 * HB;
-            if (avx2)
-                p.early ? check_avx2<true>(s.v, mp, ev, d, later, p, live) : check_avx2<false>(s.v, mp, ev, d, later, p, live);
+            int8_t *mp = s.m + e0 * W;
+            if (PF > 0 && i + PF < h->m) {   // the V rows of a check PF ahead (random rows: no HW prefetch)
+                const uint32_t *en = &h->edge_var[h->check_start[i + PF]];
+                for (int j = 0; j < h->check_deg[i + PF]; j++) __builtin_prefetch(s.v + (size_t)en[j] * W, 1, 3);
+            }
+            if (isa == Isa::avx2)
+                p.early ? check_dispatch<Avx2, true>(s.v, mp, ev, d, later, p, live)
+                        : check_dispatch<Avx2, false>(s.v, mp, ev, d, later, p, live);
+            else if (isa == Isa::sse4)
+                p.early ? check_dispatch<Sse4, true>(s.v, mp, ev, d, later, p, live)
+                        : check_dispatch<Sse4, false>(s.v, mp, ev, d, later, p, live);
             else
-                p.early ? check_portable<true>(s.v, mp, ev, d, later, p, live)
-                        : check_portable<false>(s.v, mp, ev, d, later, p, live);
+                p.early ? check_portable<true>(s.v, mp, ev, d, later, p, live, W)
+                        : check_portable<false>(s.v, mp, ev, d, later, p, live, W);
             e0 += (size_t)d;
         }
         if (p.early) {   // per codeword: stop after the first iteration whose hard decisions satisfy H
             uint8_t ok[HB];
-            syndrome_ok(h, s.v, ok);
+            syndrome_ok(h, s.v, ok, W);
             bool any = false;
-            for (int l = 0; l < HB; l++) {
+            for (int l = 0; l < W; l++) {
                 if (ok[l]) live[l] = 0;
                 any |= live[l] != 0;
             }
@@ -197,7 +283,7 @@ void decode_block_i8(const ldpc_code *h, const int8_t *llr, uint8_t *hard, int n
         }
     }
     for (int l = 0; l < nb; l++)
-        for (int i = 0; i < n; i++) hard[(size_t)l * n + i] = s.v[(size_t)i * HB + l] > 0;   // CTools.cpp:370
+        for (int i = 0; i < n; i++) hard[(size_t)l * n + i] = s.v[(size_t)i * W + l] > 0;   // CTools.cpp:370
 }
 
 // one codeword, float (the same schedule; SURVEY.md §8(a) float variant)
@@ -279,12 +365,20 @@ int host_decode_i8(const ldpc_code *h, const int8_t *llr, uint8_t *hard, int bat
     const I8Params ip{p->algo == LDPC_ALGO_NMS ? LDPC_ALGO_NMS : LDPC_ALGO_OMS,
                       p->algo == LDPC_ALGO_NMS ? p->factor : (p->algo == LDPC_ALGO_MS ? 0 : p->offset), p->var_min,
                       p->msg_max, p->early_term};
-    const int nblk = (batch + HB - 1) / HB;
-    const bool avx2 = host_has_avx2() && getenv("LDPC_HOST_PORTABLE") == nullptr;
+    // lanes per block: 32 (AVX2); LDPC_HOST_LANES=16 forces the SSE4.1 width
+    // (measured slower even on DVB-S2, whose 32-lane working set is 10.7 MB:
+    // 0.39 vs 0.31 ns per edge and codeword on one thread)
+    const int forced = getenv("LDPC_HOST_LANES") ? atoi(getenv("LDPC_HOST_LANES")) : 0;
+    const bool avx2 = host_has_avx2();
+    int W = forced == 16 ? 16 : 32;
+    Isa isa = getenv("LDPC_HOST_PORTABLE") ? Isa::portable : W == 32 ? (avx2 ? Isa::avx2 : Isa::sse4) : Isa::sse4;
+    if (isa == Isa::sse4) W = 16;
+    if (isa == Isa::sse4 && !__builtin_cpu_supports("sse4.1")) isa = Isa::portable;
+    const int nblk = (batch + W - 1) / W;
     std::vector<Scratch> sc((size_t)host_threads_for(std::max(nblk, 1)));
     parallel_units(nblk, [&](int b, int k) {
-        const int nb = std::min(HB, batch - b * HB);
-        decode_block_i8(h, llr + (size_t)b * HB * h->n, hard + (size_t)b * HB * h->n, nb, n_iter, ip, sc[k], avx2);
+        const int nb = std::min(W, batch - b * W);
+        decode_block_i8(h, llr + (size_t)b * W * h->n, hard + (size_t)b * W * h->n, nb, n_iter, ip, sc[k], isa, W);
     });
     return LDPC_OK;
 }

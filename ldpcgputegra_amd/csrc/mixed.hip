@@ -200,6 +200,13 @@ extern "C" int ldpc_mixed_last_kernel(ldpc_mixed *mx, int code_index, int *kerne
     return ldpc_ctx_last_kernel(mx->ctx[code_index], kernel);
 }
 
+extern "C" int ldpc_mixed_last_et_stage(ldpc_mixed *mx, int code_index, int *k)
+{
+    if (!mx || !k || code_index < 0 || code_index >= (int)mx->ctx.size())
+        return ldpc_set_error(LDPC_EINVAL, "mixed last et stage: bad arguments");
+    return ldpc_ctx_last_et_stage(mx->ctx[code_index], k);
+}
+
 extern "C" int ldpc_mixed_profile(ldpc_mixed *mx, int enable)
 {
     if (!mx) return ldpc_set_error(LDPC_EINVAL, "mixed profile: NULL");

@@ -59,8 +59,9 @@ class Decoder:
         7 = LDS-resident short-code kernel (int8 and float), 8 = coop3 (slab waves
         doing pre + post, i16 chain; the DVB-S2 r1/2 default), 9 = ldsep
         (edge-parallel float for short QC codes; the float default where it fits),
-        11 = stairf (float staircase codes, DVB-S2: the float default for them
-        without early termination).  4 and 6 (windowed2 S = 32, coop2) were
+        11 = stairf (float staircase codes, DVB-S2: the float default for them,
+        with or without early termination -- with it, one launch per iteration
+        plus a syndrome pass, as include/ldpc_mi355x.h states).  4 and 6 (windowed2 S = 32, coop2) were
         superseded and removed."""
         _lib.check(_lib.lib().ldpc_ctx_set_kernel(self._ctx, int(kernel)))
 
@@ -87,6 +88,14 @@ class Decoder:
         k = C.c_int()
         _lib.check(_lib.lib().ldpc_ctx_last_kernel(self._ctx, C.byref(k)))
         return self.KERNEL_NAMES.get(k.value, str(k.value))
+
+    @property
+    def last_et_stage(self):
+        """First-stage iterations of the last decode's staged early
+        termination on coop3 (0: one launch, or another kernel)."""
+        k = C.c_int()
+        _lib.check(_lib.lib().ldpc_ctx_last_et_stage(self._ctx, C.byref(k)))
+        return k.value
 
     @property
     def last_skipped(self):
@@ -133,10 +142,14 @@ class Decoder:
         p = params or _lib.default_params()
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_decode_i8_host_async(
             self._ctx, s, llr.ctypes.data, hard.ctypes.data, B, n_iter, C.byref(p))), self.device)
+        # the queued copies read llr / write hard until synchronize(): keep the
+        # arrays (and so a pinned_empty buffer's page-locked memory) alive
+        self._pending = (llr, hard)
 
     def synchronize(self):
         """Wait for this context's last decode_i8_host_async."""
         _lib.check(_lib.lib().ldpc_ctx_synchronize(self._ctx))
+        self._pending = None
 
     # -- device tensors (asynchronous on `stream`, default: torch current stream)
     @staticmethod
@@ -245,6 +258,16 @@ class MixedDecoder:
             k = C.c_int()
             _lib.check(_lib.lib().ldpc_mixed_last_kernel(self._mx, c, C.byref(k)))
             out.append(Decoder.KERNEL_NAMES.get(k.value, str(k.value)))
+        return out
+
+    def last_et_stages(self):
+        """Per code: first-stage iterations of its last staged early
+        termination (Decoder.last_et_stage; 0 = one launch)."""
+        out = []
+        for c in range(len(self.codes)):
+            k = C.c_int()
+            _lib.check(_lib.lib().ldpc_mixed_last_et_stage(self._mx, c, C.byref(k)))
+            out.append(k.value)
         return out
 
     def profile(self, enable=True):

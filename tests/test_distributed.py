@@ -1,8 +1,10 @@
 """N > 1 path on the CPU: world_size-2 gloo processes shard a batch of
 codewords exactly as bench.py does (contiguous shards, inputs regenerated from
-(seed, first codeword)), decode their shard (CPU oracle standing in for the
-GPU here), and reduce only counters and time.  Shard invariance: the union of
-the shards equals the single-process decode bit for bit."""
+(seed, first codeword)), decode their shard with the PRODUCT decoder on the
+host (a device -1 context of the C-ABI: csrc/host.cpp, the drop-in on a
+machine without a GPU), and reduce only counters and time.  Shard invariance:
+the union of the shards equals the oracle's single-process decode bit for
+bit (the oracle is only the checker here)."""
 import os
 import socket
 
@@ -25,10 +27,8 @@ def _worker(rank, world, port, total, out_dir):
     import sys
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
     sys.path.insert(0, root)
-    sys.path.insert(0, os.path.join(root, "oracle"))
     import torch.distributed as dist
-    import oracle as O
-    from ldpcgputegra_amd import channel, load_table
+    from ldpcgputegra_amd import Code, Decoder, channel, load_table
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -36,7 +36,10 @@ def _worker(rank, world, port, total, out_dir):
     table = channel.i8_table(channel.sigma_from_ebn0(1.5, 0.5))
     first, count = shard_range(rank, world, total)
     llr = channel.awgn_i8_host(t.n, count, seed=9, table=table, first_cw=first)
-    hard = O.decode_i8(t, llr, 10)
+    dec = Decoder(Code("576x288"), device=-1, max_batch=count)   # product host decoder, one context per rank
+    hard = dec.decode_i8(llr, 10)
+    assert dec.last_kernel == "host"
+    dec.close()
     be = int(hard[:, :t.k_info].sum())
     fe = int((hard[:, :t.k_info].sum(axis=1) > 0).sum())
     el, BE, FE, FR = reduce_results(0.1 * (rank + 1), be, fe, count)

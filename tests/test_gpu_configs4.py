@@ -169,3 +169,94 @@ def test_coop3_nms_vs_oracle(factor, early):
     assert np.array_equal(d_soft.cpu().numpy(), es)
     assert np.array_equal(d_hard.cpu().numpy(), eh)
     dec.close()
+
+
+def _env(**kv):
+    """Set environment variables (the C side reads them per call); returns the
+    restore function."""
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update({k: str(v) for k, v in kv.items()})
+
+    def restore():
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return restore
+
+
+def _mixed_decode(torch, names, llr, ids, iters):
+    from ldpcgputegra_amd.decoder import MixedDecoder
+    B = llr.shape[0]
+    mx = MixedDecoder([Code(n) for n in names], max_batch=B)
+    hard = torch.empty((B, llr.shape[1]), dtype=torch.uint8, device="cuda")
+    its = torch.empty(B, dtype=torch.int32, device="cuda")
+    mx.decode_i8_device(llr, hard, ids, iters, params=default_params(early_term=1), iters_used=its)
+    torch.cuda.synchronize()
+    out = (hard.cpu().numpy(), its.cpu().numpy(), mx.last_kernels(), mx.last_et_stages())
+    mx.close()
+    del hard, its
+    return out
+
+
+def test_configs4_mixed_staged_vs_oracle():
+    """The mixed decoder stages a rate's early termination by the same rule as
+    a single-code decode (coop3 sub-batch >= LDPC_COOP3_ET_STAGE_MIN): with
+    the threshold at 512 and bench.py --mixed's inputs at batch 1536, r1/2's
+    512 codewords run staged (K = 20, then compactions every 5 iterations) and
+    every codeword of every rate equals the oracle's per-codeword early
+    termination (hard decisions and iterations used)."""
+    torch = _torch()
+    import bench
+    names = bench.MIXED_SETS["configs4"]
+    B, iters = 1536, 50
+    ids, llr = _bench_mixed_inputs(torch, names, B, 2024, bench.MIXED_EBN0)
+    restore = _env(LDPC_COOP3_ET_STAGE_MIN=512)
+    try:
+        got_h, got_i, kernels, stages = _mixed_decode(torch, names, llr, ids, iters)
+    finally:
+        restore()
+    assert kernels == ["coop3", "coop", "coop"], kernels
+    assert stages[0] == 20, stages
+    host = llr.cpu().numpy()
+    thr = O.host_threads()
+    for c, name in enumerate(names):
+        sel = np.where(ids == c)[0]
+        eh, _, eit = O.decode_i8(load_table(name), host[sel], iters, early_term=True, return_soft=True, threads=thr)
+        assert np.array_equal(got_i[sel], eit), (name, int((got_i[sel] != eit).sum()))
+        assert np.array_equal(got_h[sel], eh), name
+    assert got_i[ids == 0].max() > 20 and got_i[ids == 0].min() <= 20   # stages before and after K
+
+
+def test_configs4_mixed_staged_batch_as_benched():
+    """bench.py --mixed --batch 24576 (8192 codewords per rate): r1/2 runs
+    staged by default, and the whole batch equals the same mixed decode with
+    staging off (one in-kernel early-termination launch per rate, itself
+    oracle-checked above) bit for bit -- hard decisions and iterations used;
+    a seeded sample of 96 codewords per rate equals the oracle."""
+    torch = _torch()
+    import bench
+    names = bench.MIXED_SETS["configs4"]
+    B, iters = 24576, 50
+    ids, llr = _bench_mixed_inputs(torch, names, B, 2024, bench.MIXED_EBN0)
+    got_h, got_i, kernels, stages = _mixed_decode(torch, names, llr, ids, iters)
+    assert kernels == ["coop3", "coop", "coop"], kernels
+    assert stages[0] > 0, stages
+    restore = _env(LDPC_COOP3_ET_STAGE_MIN=1 << 30)
+    try:
+        ref_h, ref_i, _, stages1 = _mixed_decode(torch, names, llr, ids, iters)
+    finally:
+        restore()
+    assert stages1[0] == 0
+    assert np.array_equal(got_i, ref_i), int((got_i != ref_i).sum())
+    assert np.array_equal(got_h, ref_h)
+    del ref_h
+    host = llr.cpu().numpy()
+    rng = np.random.default_rng(5)
+    thr = O.host_threads()
+    for c, name in enumerate(names):
+        sel = np.sort(rng.choice(np.where(ids == c)[0], 96, replace=False))
+        eh, _, eit = O.decode_i8(load_table(name), host[sel], iters, early_term=True, return_soft=True, threads=thr)
+        assert np.array_equal(got_i[sel], eit), name
+        assert np.array_equal(got_h[sel], eh), name

@@ -270,6 +270,36 @@ def test_coop3_staged_early_termination_vs_oracle(monkeypatch, q, nms, step, ebn
     assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
 
 
+def test_coop3_staged_early_termination_past_64_stages(monkeypatch):
+    """More iterations than 64 stages hold (K = 2, one iteration per stage,
+    90 iterations: K + 64 < 90): the 64th stage takes every iteration left,
+    so codewords still decoding are decoded up to the last iteration and
+    record it (regression: the stage loop used to stop at 64 stages, leaving
+    them under-decoded with iters_used = -1).  Eb/N0 0.9 dB: a quarter of the codewords
+    never converge, one converges only after the 64th stage began."""
+    torch = _torch()
+    code, batch, iters = "dvbs2_r1_2", 48, 90
+    t = load_table(code)
+    llr = channel.awgn_i8_host(t.n, batch, seed=29, table=channel.i8_table(channel.sigma_from_ebn0(0.9, 0.5)))
+    ref_hard, ref_soft, ref_its = O.decode_i8(t, llr, iters, early_term=True, return_soft=True,
+                                              threads=O.host_threads())
+    assert (ref_its == iters).any() and (ref_its < iters).any()
+    monkeypatch.setenv("LDPC_COOP3_ET_STAGE_MIN", "0")
+    monkeypatch.setenv("LDPC_COOP3_ET_K", "2")
+    monkeypatch.setenv("LDPC_COOP3_ET_STEP", "1")
+    dec = decoder(code, 8, max_batch=64)
+    d_hard = torch.empty((batch, t.n), dtype=torch.uint8, device="cuda")
+    d_soft = torch.empty((batch, t.n), dtype=torch.int8, device="cuda")
+    d_its = torch.empty(batch, dtype=torch.int32, device="cuda")
+    dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=default_params(early_term=1),
+                         soft=d_soft, iters_used=d_its)
+    torch.cuda.synchronize()
+    assert dec.last_et_stage == 2
+    assert np.array_equal(d_its.cpu().numpy(), ref_its)
+    assert np.array_equal(d_soft.cpu().numpy(), ref_soft)
+    assert np.array_equal(d_hard.cpu().numpy(), ref_hard)
+
+
 def has_kernel(code, k):
     try:
         decoder(code, k, 64)

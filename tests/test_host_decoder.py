@@ -44,11 +44,29 @@ def test_host_decoder_matches_reference_golden(case):
 @pytest.mark.parametrize("case", [c for c in CASES if c["code"] in ("576x288", "2048x384") or
                                   (c["code"] == "dvbs2_r1_2" and c["iters"] <= 20)][:12],
                          ids=lambda c: c["name"])
-def test_host_portable_path_matches_golden(case, monkeypatch):
-    monkeypatch.setenv("LDPC_HOST_PORTABLE", "1")
+@pytest.mark.parametrize("env", [{"LDPC_HOST_PORTABLE": "1"}, {"LDPC_HOST_LANES": "16"}],
+                         ids=["portable", "sse16"])
+def test_host_portable_path_matches_golden(case, env, monkeypatch):
+    """The per-lane portable loop and the 16-lane SSE4.1 blocks (the paths a
+    host without AVX2 runs) equal the reference's golden vectors too."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     llr, expected = golden_inputs(case)
     got = host(case["code"]).decode_i8(llr, case["iters"], params_of(case))
     assert np.array_equal(got, expected)
+
+
+@pytest.mark.parametrize("lanes", ["16", "32"])
+def test_host_simd_early_termination_ragged(lanes, monkeypatch):
+    """Early termination on both SIMD widths over a ragged batch of 50
+    (blocks of 16 / 32 with a partial last block) equals the oracle."""
+    monkeypatch.setenv("LDPC_HOST_LANES", lanes)
+    t = load_table("576x288")
+    llr = channel.awgn_i8_host(t.n, 50, seed=8, table=channel.i8_table(channel.sigma_from_ebn0(2.0, 0.5)))
+    exp, _, its = O.decode_i8(t, llr, 25, early_term=True, return_soft=True)
+    assert its.min() < 25
+    got = host("576x288").decode_i8(llr, 25, default_params(early_term=1))
+    assert np.array_equal(got, exp)
 
 
 @pytest.mark.parametrize("code,ebn0", [("576x288", 2.0), ("dvbs2_r1_2", 1.1)])

@@ -70,6 +70,15 @@ def functions(isa):
     return funcs
 
 
+def kind(line):
+    """L: a load into VGPRs, G: an LDS-DMA load (`... lds`), S: a store."""
+    if "_store" in line.split("//")[0]:
+        return "S"
+    if re.search(r"\blds\b", line.split("//")[0]):
+        return "G"
+    return "L"
+
+
 def closes_period(lines, i, reach=8):
     """The wait at line i is followed by an s_barrier within `reach` lines,
     with no vector-memory instruction or branch before it."""
@@ -111,6 +120,15 @@ def check(isa, ops, vmcnt, min_regions=1, pattern="coop3_decode", et_ops=24, et_
             if n != ops:
                 errs.append("%s: %d vector-memory instructions between the vmcnt(%d) waits at ISA lines %d and %d, "
                             "the wait assumes %d per period" % (name, n, vmcnt, a, b, ops))
+            else:
+                # the count is right only in this order: WS line loads, WS
+                # LDS-DMA gathers, then the 2 WS writebacks / stores
+                seq = "".join(kind(l) for l in body if VMEM.match(l))
+                ws = ops // 4
+                want = "L" * ws + "G" * ws + "S" * (2 * ws)
+                if seq != want:
+                    errs.append("%s: vector-memory order %s between the waits at ISA lines %d and %d, the vmcnt(%d) "
+                                "argument assumes %s (line loads, gathers, stores)" % (name, seq, a, b, vmcnt, want))
             good += 1
         if good < min_regions:
             errs.append("%s: only %d straight-line memory-wave periods found (want >= %d)" % (name, good,

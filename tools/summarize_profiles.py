@@ -80,8 +80,11 @@ def main():
         if dec:
             tr_path = os.path.join(dst, "traffic.json")
             tr = json.load(open(tr_path)) if os.path.exists(tr_path) else {}
+            # the source hash the bench line reports (the build the passes ran
+            # on): bench.py uses the entry only for that build
             tr[key] = dict(hbm_bytes_per_launch=dec[0]["hbm_bytes"], fetch_kb=dec[0]["fetch_kb"],
-                           write_kb=dec[0]["write_kb"], source="profiles/%s_pmc.json" % tag)
+                           write_kb=dec[0]["write_kb"], source="profiles/%s_pmc.json" % tag,
+                           src_sha16=bench.get("build", {}).get("src_sha16"))
             json.dump(tr, open(tr_path, "w"), indent=1, sort_keys=True)
     print(json.dumps(dict(stats=stats, bench=bool(bench), pmc=list(pmc)), indent=1))
 
