@@ -145,6 +145,12 @@ int ldpc_code_coop_plan_dist(const ldpc_code *h, int S, int R, int dist, int *fi
  * no reference interface.) */
 int ldpc_code_coop3_lc_info(const ldpc_code *h, int *slots, int *max_slots, int *residencies, int *prologue,
                             int *epilogue);
+/* The line cache's modelled LDS bank conflicts: extra LDS cycles per
+ * iteration and workgroup of coop3's pre reads / post writes of the line
+ * cache with the planner's per-residency XOR swizzle (swizzled) and with
+ * every line unswizzled (plain); 0 / 0 when the code has no coop3 schedule.
+ * (Introspection for tests.) */
+int ldpc_code_coop3_lc_banks(const ldpc_code *h, long long *swizzled, long long *plain);
 /* Layer plan of the LDS-resident kernel (kernel 7): maximal runs of
  * consecutive same-group checks sharing no variable (one block row of a
  * quasi-cyclic code).  lds_i8 / lds_f32: 1 if a codeword's state fits the

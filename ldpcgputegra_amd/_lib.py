@@ -68,6 +68,7 @@ SIGNATURES = {
     "ldpc_code_coop_plan": (I, [P, I, I, P, P, I, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "ldpc_code_coop_plan_dist": (I, [P, I, I, I, P, P, I, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "ldpc_code_coop3_lc_info": (I, [P] + [C.POINTER(I)] * 5),
+    "ldpc_code_coop3_lc_banks": (I, [P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     "ldpc_code_destroy": (None, [P]),
     "ldpc_ctx_create": (I, [P, I, I, C.POINTER(P)]),
     "ldpc_ctx_destroy": (None, [P]),

@@ -234,6 +234,14 @@ class Code:
             return None
         return dict(zip(("slots", "max_slots", "residencies", "prologue", "epilogue"), (x.value for x in v)))
 
+    def coop3_lc_banks(self):
+        """Modelled extra LDS cycles per iteration and workgroup of coop3's
+        line-cache pre reads / post writes: dict(swizzled=..., plain=...)
+        (the planner's XOR swizzle vs every line unswizzled)."""
+        a, b = C.c_longlong(), C.c_longlong()
+        _lib.check(_lib.lib().ldpc_code_coop3_lc_banks(self._h, C.byref(a), C.byref(b)))
+        return dict(swizzled=a.value, plain=b.value)
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and _lib._lib is not None:

@@ -86,14 +86,27 @@ constexpr int LC_LEAD = 3;   // a line is loaded (into VGPRs) >= 3 periods befor
 constexpr int LC_PUT = 2;    // ... and written to its slot 2 periods after its load (coop3: loads first in a
                              // period, vmcnt(36) at its end completes those of the period before)
 constexpr int LC_OPS = 48;   // line loads / writebacks per period: 6 slab waves x 8 lane groups
+// A line's 8 rows sit in its slot XOR-swizzled: row i at piece position i ^ z
+// (z = 0..7 per residency, chosen by the planner so that the 4 pieces one
+// 32-lane half of a pre read / post write touches fall in distinct bank
+// groups: the LDS serves a ds_read_b32 / ds_write_b16 half in one cycle only
+// if its addresses hit distinct banks, and a piece's bank group is its
+// position in the 128-B slot).  Slot fields carry z beside the slot index.
+constexpr int LC_SLOT_BITS = 10;                       // slot index < 1024
+constexpr uint32_t LC_SLOT_MASK = (1u << LC_SLOT_BITS) - 1;
 struct LcPlan {
     int slots = 0;                 // LDS line slots used, the sink (slot 0) included
     int residencies = 0;           // line residencies per iteration
     std::vector<uint32_t> ops;     // [nw][LC_OPS][2]: load line | writeback line << 16,
                                    //   slot written (the load of 2 periods earlier) | writeback slot << 16
+                                   //   (each 16-bit slot field: slot | z << LC_SLOT_BITS)
     std::vector<uint32_t> piece;   // [nw][S][D0 - 2]: LDS byte offset (from the cache) of each info entry's piece
-    std::vector<uint32_t> pro;     // slot << 16 | line: lines resident at a segment start
-    std::vector<uint32_t> epi;     // slot << 16 | line: dirty lines written back at a segment end
+    std::vector<uint32_t> pro;     // z << 26 | slot << 16 | line: lines resident at a segment start
+    std::vector<uint32_t> epi;     // z << 26 | slot << 16 | line: dirty lines written back at a segment end
+    // modelled extra LDS cycles of the pre reads + post writes per iteration
+    // and workgroup (bank conflicts, lc_bank_extra), with the planner's
+    // swizzle and with z = 0 everywhere
+    long bank_extra = 0, bank_extra_plain = 0;
 };
 // tab: coop3's permuted slot records (Coop3Host::pl.tab); 0 = ok (plan self-checked), -1 = no plan
 int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int n, int k, int max_slots,

@@ -540,6 +540,13 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
     }
 }
 
+// LDS byte offset of row i of the line of a prologue / epilogue entry
+// (z << 26 | slot << 16 | line): piece i ^ z of its slot (LcPlan swizzle)
+LDPC_DEV uint32_t lc_piece(uint32_t pw, uint32_t i)
+{
+    return ((pw >> 16) & LC_SLOT_MASK) * 128u + ((i ^ (pw >> 26)) & 7u) * 16u;
+}
+
 // diagnostic stamps that do not wait: the compiler waits for s_memtime only
 // where the value is used (the end of a period)
 LDPC_DEV unsigned long long stampL()
@@ -932,14 +939,14 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 auto read_out = [&]() __attribute__((always_inline)) {   // writeback and store data
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
-                        wbd[w] = *(const uint4 *)(lcb + lop[w].w + lq);
+                        wbd[w] = *(const uint4 *)(lcb + (lop[w].w ^ lq));   // row q of the swizzled slot
                         std_[w] = sm.mst[(p - 2) & 1][w][kl][qp];
                     });
                 };
                 auto slot_writes = [&]() __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
-                        *(uint4 *)(lcb + lop[w].z + lq) = pend[(s + 1) % NPD][w];
+                        *(uint4 *)(lcb + (lop[w].z ^ lq)) = pend[(s + 1) % NPD][w];
                     });
                 };
                 auto gathers = [&]() __attribute__((always_inline)) {
@@ -1043,7 +1050,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 #pragma unroll
                 for (int j = 0; j < PB; j++)
                     if (i0 + j * NSL < 8 * a.n_pro)
-                        *(uint4 *)((char *)&sm.lc[0][0] + (pw[j] >> 16) * 128u + (uint32_t)((i0 + j * NSL) & 7) * 16u) = d[j];
+                        *(uint4 *)((char *)&sm.lc[0][0] + lc_piece(pw[j], (uint32_t)((i0 + j * NSL) & 7))) = d[j];
             }
         }
         __syncthreads();   // prologue 1: tables and resident lines in LDS
@@ -1176,7 +1183,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 for (int j = 0; j < PB; j++) pw[j] = a.lc_epi[min(i0 + j * NSL, 8 * a.n_epi - 1) >> 3];
 #pragma unroll
                 for (int j = 0; j < PB; j++)
-                    d[j] = *(const uint4 *)((const char *)&sm.lc[0][0] + (pw[j] >> 16) * 128u + (uint32_t)((i0 + j * NSL) & 7) * 16u);
+                    d[j] = *(const uint4 *)((const char *)&sm.lc[0][0] + lc_piece(pw[j], (uint32_t)((i0 + j * NSL) & 7)));
 #pragma unroll
                 for (int j = 0; j < PB; j++)
                     if (i0 + j * NSL < 8 * a.n_epi) {
@@ -1353,8 +1360,11 @@ static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vec
             const uint32_t lines = lp.ops[((size_t)u * LC_OPS + kk) * 2], slots = lp.ops[((size_t)u * LC_OPS + kk) * 2 + 1];
             rec[W_LOP] = (lines & 0xFFFFu) * 128u;        // line loaded (byte offset in the group's V block)
             rec[W_LOP + 1] = (lines >> 16) * 128u;        // line written back
-            rec[W_LOP + 2] = (slots & 0xFFFFu) * 128u;    // slot written with the load of LC_PUT periods earlier
-            rec[W_LOP + 3] = (slots >> 16) * 128u;        // slot written back
+            // slot byte offsets with the line's swizzle z in bits 4..6: lane q's
+            // piece is at (offset ^ 16 q) (LcPlan, coop.h)
+            auto slot_off = [](uint32_t f) { return (f & LC_SLOT_MASK) * 128u + (f >> LC_SLOT_BITS) * 16u; };
+            rec[W_LOP + 2] = slot_off(slots & 0xFFFFu);   // slot written with the load of LC_PUT periods earlier
+            rec[W_LOP + 3] = slot_off(slots >> 16);       // slot written back
         }
 }
 
@@ -1673,6 +1683,18 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
         (void)hipFree(a.stamps);
     }
     return rc;
+}
+
+extern "C" int ldpc_code_coop3_lc_banks(const ldpc_code *h, long long *swizzled, long long *plain)
+{
+    if (!h || !swizzled || !plain) return ldpc_set_error(LDPC_EINVAL, "coop3 lc banks args");
+    Coop3Host ho;
+    LcPlan lp;
+    const int rc = coop3_plan_lc(h, ho, lp);
+    if (rc < 0) return rc;
+    *swizzled = rc == 0 ? lp.bank_extra : 0;
+    *plain = rc == 0 ? lp.bank_extra_plain : 0;
+    return LDPC_OK;
 }
 
 // line-cache statistics of a code's coop3 schedule (tests, tools)

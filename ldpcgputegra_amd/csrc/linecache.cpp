@@ -49,6 +49,7 @@ struct Res {
     bool dirty, whole;   // written to; resident for the whole iteration
     int fw = 1 << 30;    // first write period (unrolled like e)
     int slot = -1;
+    int z = 0;              // XOR swizzle of its rows in the slot (LcPlan)
     int li = -1, wi = -1;   // index of its load / writeback in the period's op list
 };
 
@@ -284,7 +285,107 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     const int used = assign(best_p0);
     o.slots = used + 1;
     o.residencies = (int)rs.size();
-    if (o.slots > max_slots) return lc_fail(__LINE__);
+    if (o.slots > max_slots || o.slots > (int)LC_SLOT_MASK + 1) return lc_fail(__LINE__);
+    // residency holding line L at access period p (cyclic)
+    auto res_id_at = [&](uint32_t L, int p) -> int {
+        for (int id : res_of[L]) {
+            const Res &R = rs[id];
+            if (R.whole || cmod(p - R.f, nw) <= R.e - R.f) return id;
+        }
+        return -1;
+    };
+    // bank groups: a pre read (ds_read_b32) / post write (ds_write_b16) of info
+    // entry j serves slab wave w's slots 8w + 4h .. 8w + 4h + 3 in one 32-lane
+    // half h; a piece's bank group is its position in its 128-B slot (slots are
+    // 32 dwords = the 32 banks those instructions use), so 4 distinct pieces
+    // in one position cost 3 extra cycles.  Access = residency, row (-1: the
+    // sink piece of an inactive slot)
+    struct Acc {
+        int res, row;
+    };
+    std::vector<std::vector<Acc>> groups;
+    for (int u = 0; u < nw; u++)
+        for (int w = 0; w < S / 8; w++)
+            for (int hh = 0; hh < 2; hh++)
+                for (int j = 0; j < X; j++) {
+                    std::vector<Acc> g;
+                    for (int i = 0; i < 4; i++) {
+                        const uint32_t *r = rec_at(u, 8 * w + 4 * hh + i);
+                        if (!(r[D0] & COOP_M_ACT)) {
+                            g.push_back({-1, 0});
+                            continue;
+                        }
+                        const int id = res_id_at(r[j] / 8, cmod(u - 1, nw));
+                        if (id < 0) return lc_fail(__LINE__);
+                        g.push_back({id, (int)(r[j] % 8)});
+                    }
+                    groups.push_back(g);
+                }
+    auto pos_of = [&](const Acc &a) { return a.res < 0 ? 0 : (a.row ^ rs[a.res].z); };
+    // extra LDS cycles of one group: the most distinct pieces in one position, minus 1
+    auto extra = [&](const std::vector<Acc> &g) -> int {
+        int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (size_t i = 0; i < g.size(); i++) {
+            bool dup = false;
+            for (size_t k2 = 0; k2 < i; k2++) dup |= g[k2].res == g[i].res && g[k2].row == g[i].row;
+            if (!dup) cnt[pos_of(g[i])]++;
+        }
+        int mx = 0;
+        for (int c : cnt) mx = std::max(mx, c);
+        return mx - 1;
+    };
+    auto total = [&]() {
+        long t = 0;
+        for (const auto &g : groups) t += extra(g);
+        return 2 * t;   // the pre read and the post write
+    };
+    o.bank_extra_plain = total();
+    // local search over z: each residency takes the z that minimises the
+    // extra cycles of its groups (pairwise same-position count as the
+    // smoother objective), a few sweeps (LDPC_LC_SWIZZLE=0: z = 0)
+    const char *sz = getenv("LDPC_LC_SWIZZLE");
+    if (!(sz && *sz && atoi(sz) == 0)) {
+        std::vector<std::vector<int>> gof(rs.size());
+        for (int gi = 0; gi < (int)groups.size(); gi++)
+            for (const Acc &a : groups[gi])
+                if (a.res >= 0 && (gof[a.res].empty() || gof[a.res].back() != gi)) gof[a.res].push_back(gi);
+        auto pairs = [&](const std::vector<Acc> &g) -> int {
+            int c = 0;
+            for (size_t i = 0; i < g.size(); i++)
+                for (size_t k2 = 0; k2 < i; k2++)
+                    if (!(g[k2].res == g[i].res && g[k2].row == g[i].row) && pos_of(g[k2]) == pos_of(g[i])) c++;
+            return c;
+        };
+        for (int sweep = 0; sweep < 12; sweep++) {
+            int changed = 0;
+            for (int id = 0; id < (int)rs.size(); id++) {
+                if (gof[id].empty()) continue;
+                const int z0 = rs[id].z;
+                int bz = z0, bc = 1 << 30;
+                for (int z = 0; z < 8; z++) {
+                    rs[id].z = (z0 + z) & 7;   // ties keep the current z
+                    int c = 0;
+                    for (int gi : gof[id]) c += 4 * extra(groups[gi]) + pairs(groups[gi]);
+                    if (c < bc) {
+                        bc = c;
+                        bz = rs[id].z;
+                    }
+                }
+                rs[id].z = bz;
+                changed += bz != z0;
+            }
+            if (!changed) break;
+        }
+    }
+    o.bank_extra = total();
+    {
+        const char *dbg = getenv("LDPC_LC_DEBUG");
+        if (dbg && *dbg == '2')
+            fprintf(stderr, "coop3 line cache: %d slots, %d residencies; modelled pre/post bank-conflict cycles per "
+                            "iteration and workgroup: %ld (z = 0: %ld)\n", o.slots, o.residencies, o.bank_extra,
+                    o.bank_extra_plain);
+    }
+    auto sfield = [&](const Res &R) { return (uint32_t)R.slot | (uint32_t)R.z << LC_SLOT_BITS; };
     // per-period op lists
     std::vector<std::vector<int>> lp(nw), wp(nw);
     for (int i = 0; i < (int)rs.size(); i++) {
@@ -307,20 +408,16 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
         uint32_t *ld = &o.ops[((size_t)cmod(R.tl, nw) * LC_OPS + R.li) * 2];
         ld[0] = (ld[0] & 0xFFFF0000u) | R.line;
         uint32_t *dw = &o.ops[((size_t)cmod(R.tl + LC_PUT, nw) * LC_OPS + R.li) * 2];
-        dw[1] = (dw[1] & 0xFFFF0000u) | (uint32_t)R.slot;
+        dw[1] = (dw[1] & 0xFFFF0000u) | sfield(R);
         if (R.dirty) {
             uint32_t *wb = &o.ops[((size_t)cmod(R.tw, nw) * LC_OPS + R.wi) * 2];
             wb[0] = (wb[0] & 0xFFFFu) | R.line << 16;
-            wb[1] = (wb[1] & 0xFFFFu) | (uint32_t)R.slot << 16;
+            wb[1] = (wb[1] & 0xFFFFu) | sfield(R) << 16;
         }
     }
-    // residency holding line L at access period p (cyclic)
     auto res_at = [&](uint32_t L, int p) -> const Res * {
-        for (int id : res_of[L]) {
-            const Res &R = rs[id];
-            if (R.whole || cmod(p - R.f, nw) <= R.e - R.f) return &R;
-        }
-        return nullptr;
+        const int id = res_id_at(L, p);
+        return id < 0 ? nullptr : &rs[id];
     };
     o.piece.assign((size_t)nw * S * X, 0);
     for (int u = 0; u < nw; u++)
@@ -330,12 +427,12 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
             for (int j = 0; j < X; j++) {
                 const Res *R = res_at(r[j] / 8, cmod(u - 1, nw));
                 if (!R || R != res_at(r[j] / 8, cmod(u + 1, nw))) return lc_fail(__LINE__);
-                o.piece[((size_t)u * S + kk) * X + j] = (uint32_t)R->slot * 128u + (r[j] % 8) * 16u;
+                o.piece[((size_t)u * S + kk) * X + j] = (uint32_t)R->slot * 128u + ((r[j] % 8) ^ (uint32_t)R->z) * 16u;
             }
         }
     // segment prologue / epilogue: holds across the iteration boundary
     for (const Res &R : rs) {
-        const uint32_t w = (uint32_t)R.slot << 16 | R.line;
+        const uint32_t w = (uint32_t)R.z << 26 | (uint32_t)R.slot << 16 | R.line;
         if (R.whole) {
             o.pro.push_back(w);
             if (R.dirty) o.epi.push_back(w);
@@ -366,7 +463,7 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
     const int X = D0 - 2;
     const uint32_t sink_line = (uint32_t)(n / 8);
     const int NSL = o.slots;
-    std::vector<int> line_of(NSL, -1);
+    std::vector<int> line_of(NSL, -1), z_of(NSL, 0);
     std::vector<char> dirty(NSL, 0);
     std::vector<long> last_store((size_t)k / 8, -1000000);
     std::vector<int> dirty_copies((size_t)k / 8, 0);
@@ -375,9 +472,10 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
         return -1;
     };
     for (uint32_t w : o.pro) {
-        const int s = (int)(w >> 16), L = (int)(w & 0xFFFFu);
+        const int s = (int)((w >> 16) & LC_SLOT_MASK), L = (int)(w & 0xFFFFu);
         if (s <= 0 || s >= NSL || line_of[s] >= 0) return fail("prologue slot", -1, s, L);
         line_of[s] = L;
+        z_of[s] = (int)(w >> 26) & 7;
     }
     auto rec_at = [&](int u, int kk) { return &tab[((size_t)u * S + kk) * recw]; };
     std::vector<long> put_at(NSL, -1000000);   // period of the slot's last write by the memory wave
@@ -389,7 +487,8 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
             for (int j = 0; j < X; j++) {
                 const uint32_t off = o.piece[((size_t)u * S + kk) * X + j];
                 const int s = (int)(off / 128);
-                if (off % 128 != (r[j] % 8) * 16 || s <= 0 || s >= NSL || line_of[s] != (int)(r[j] / 8))
+                if (s <= 0 || s >= NSL || off % 128 != ((r[j] % 8) ^ (uint32_t)z_of[s]) * 16 ||
+                    line_of[s] != (int)(r[j] / 8))
                     return fail(wr ? "post finds another line" : "pre finds another line", P, s, (int)r[j]);
                 if (put_at[s] == P)
                     return fail(wr ? "post of a line written to its slot this period"
@@ -436,12 +535,12 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
         std::vector<char> wb_slot(NSL, 0);
         for (int i = 0; i < LC_OPS; i++)
             if ((ops[2 * i] >> 16) != sink_line) {
-                const int s = (int)(ops[2 * i + 1] >> 16);
+                const int s = (int)((ops[2 * i + 1] >> 16) & LC_SLOT_MASK);
                 if (s > 0 && s < NSL) wb_slot[s] = 1;
             }
         // slot writes of the loads of period P - LC_PUT (first in the memory wave's period)
         for (int i = 0; i < LC_OPS; i++) {
-            const int s = (int)(ops[2 * i + 1] & 0xFFFFu);
+            const int s = (int)(ops[2 * i + 1] & LC_SLOT_MASK);
             const uint32_t L = pend[(size_t)((P + 1) % NPD) * LC_OPS + i];   // the load of period P - LC_PUT
             if (s == 0) {
                 if (L != sink_line && P >= LC_PUT) return fail("load without a slot", P, s, (int)L);
@@ -453,15 +552,17 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
             if (wb_slot[s]) return fail("slot written and written back in one period", P, s, (int)L);
             if (used_slot[s]) return fail("slot refilled in a period whose post / pre access it", P, s, line_of[s]);
             line_of[s] = (int)L;
+            z_of[s] = (int)((ops[2 * i + 1] & 0xFFFFu) >> LC_SLOT_BITS);
             put_at[s] = P;
         }
         // writebacks (concurrent with the post / pre below)
         for (int i = 0; i < LC_OPS; i++) {
             const uint32_t L = ops[2 * i] >> 16;
-            const int s = (int)(ops[2 * i + 1] >> 16);
+            const int s = (int)((ops[2 * i + 1] >> 16) & LC_SLOT_MASK);
             if (L == sink_line) continue;
-            if (L >= (uint32_t)k / 8 || s <= 0 || s >= NSL || line_of[s] != (int)L)
-                return fail("writeback of a line not in its slot", P, s, (int)L);
+            if (L >= (uint32_t)k / 8 || s <= 0 || s >= NSL || line_of[s] != (int)L ||
+                (int)(ops[2 * i + 1] >> (16 + LC_SLOT_BITS)) != z_of[s])
+                return fail("writeback of a line not in its slot (or with another swizzle)", P, s, (int)L);
             if (touched[L]) return fail("writeback in a period accessing the line", P, s, (int)L);
             if (dirty[s]) dirty_copies[L]--;
             dirty[s] = 0;
@@ -483,7 +584,7 @@ int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, i
     // what is left dirty must be the epilogue
     std::vector<uint32_t> left;
     for (int s = 1; s < NSL; s++)
-        if (dirty[s]) left.push_back((uint32_t)s << 16 | (uint32_t)line_of[s]);
+        if (dirty[s]) left.push_back((uint32_t)z_of[s] << 26 | (uint32_t)s << 16 | (uint32_t)line_of[s]);
     std::vector<uint32_t> epi = o.epi;
     std::sort(left.begin(), left.end());
     std::sort(epi.begin(), epi.end());
