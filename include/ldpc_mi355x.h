@@ -330,6 +330,17 @@ int ldpc_quantize_f32_i8(ldpc_ctx *ctx, const float *y, int8_t *q, long count, i
  * (NULL = all-zero); d_counts[0] += bit errors, d_counts[1] += frame errors. */
 int ldpc_count_errors_async(ldpc_ctx *ctx, void *hip_stream, const uint8_t *d_hard, int batch,
                            int k, const uint8_t *d_ref, unsigned long long *d_counts);
+/* Decode and count in one call: ldpc_decode_*_async followed by
+ * ldpc_count_errors_async over d_hard (required) -- the reference's
+ * decode + CErrorAnalyzer::generate pair (code/x86/main_p.cpp:511-540,
+ * CErrorAnalyzer.cpp:123-154).  The edge-parallel float kernel (9) counts in
+ * its own epilogue (no second launch); the others launch the count after. */
+int ldpc_decode_i8_count_async(ldpc_ctx *ctx, void *hip_stream, const int8_t *d_llr, uint8_t *d_hard,
+                               int8_t *d_soft, int32_t *d_iters_used, int batch, int n_iter, const ldpc_params *p,
+                               int k, const uint8_t *d_ref, unsigned long long *d_counts);
+int ldpc_decode_f32_count_async(ldpc_ctx *ctx, void *hip_stream, const float *d_llr, uint8_t *d_hard,
+                                float *d_soft, int32_t *d_iters_used, int batch, int n_iter, const ldpc_params *p,
+                                int k, const uint8_t *d_ref, unsigned long long *d_counts);
 
 #ifdef __cplusplus
 }

@@ -100,6 +100,8 @@ SIGNATURES = {
     "ldpc_awgn_i8_host": (I, [I, I, U64, U64, P, P, P]),
     "ldpc_awgn_i8_async": (I, [P, P, P, I, U64, U64, P, P]),
     "ldpc_count_errors_async": (I, [P, P, P, I, I, P, P]),
+    "ldpc_decode_i8_count_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params), I, P, P]),
+    "ldpc_decode_f32_count_async": (I, [P, P, P, P, P, P, I, I, C.POINTER(ldpc_params), I, P, P]),
     "ldpc_quantize_f32_i8_async": (I, [P, P, P, P, C.c_long, I, I, I]),
     "ldpc_quantize_f32_i8": (I, [P, P, P, C.c_long, I, I, I]),
     "ldpc_decode_i8_host_async": (I, [P, P, P, P, I, I, C.POINTER(ldpc_params)]),

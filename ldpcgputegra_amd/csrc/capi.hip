@@ -393,9 +393,16 @@ static int pick_kernel(ldpc_ctx *c, const ldpc_params *p, bool is_float, int str
 // alloc_only: size the scratch for this decode and return (decode_host sizes
 // every lane before it queues any work: a hipFree mid-pipeline would wait for
 // the device)
+// error count requested with a decode (ldpc_decode_*_count_async)
+struct ErrCount {
+    int k;
+    const uint8_t *ref;
+    unsigned long long *counts;
+};
+
 static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_llr, uint8_t *d_hard, void *d_soft,
                          int32_t *d_iters, int batch, int n_iter, const ldpc_params *p, bool is_float,
-                         bool alloc_only = false, size_t nm_ld = 0)
+                         bool alloc_only = false, size_t nm_ld = 0, const ErrCount *ec = nullptr)
 {
     int rc = check_params(c, batch, n_iter, p, is_float);
     if (rc != LDPC_OK) return rc;
@@ -428,6 +435,11 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         L.early = p->early_term;
         L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
         L.iters_used = d_iters;
+        if (ec && kern == 9) {   // ldsep counts in its epilogue (one wave = one codeword)
+            L.cnt = ec->counts;
+            L.cnt_ref = ec->ref;
+            L.cnt_k = ec->k;
+        }
         hipEvent_t ev0 = nullptr, ev1 = nullptr;
         if (c->profile) {
             HIP_TRY(hipEventCreate(&ev0));
@@ -442,6 +454,8 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
             c->events.emplace_back(ev0, ev1);
         }
         if (lr) return ldpc_set_error(LDPC_EDEVICE, "lds decode launch: %s", hipGetErrorString(hipGetLastError()));
+        if (ec && kern != 9 && launch_count_errors(d_hard, h->n, batch, ec->k, ec->ref, ec->counts, s))
+            return ldpc_set_error(LDPC_EDEVICE, "count_errors: %s", hipGetErrorString(hipGetLastError()));
         return LDPC_OK;
     }
     const bool win = kern >= 2 && kern != 11;
@@ -559,6 +573,8 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
                                                       batch, vpitch, s);
         if (r2) return ldpc_set_error(LDPC_EDEVICE, "deinterleave: %s", hipGetErrorString(hipGetLastError()));
     }
+    if (ec && launch_count_errors(d_hard, h->n, batch, ec->k, ec->ref, ec->counts, s))
+        return ldpc_set_error(LDPC_EDEVICE, "count_errors: %s", hipGetErrorString(hipGetLastError()));
     return LDPC_OK;
 }
 
@@ -591,6 +607,37 @@ extern "C" int ldpc_decode_f32_async(ldpc_ctx *c, void *s, const float *d_llr, u
 {
     if (!c || (!d_llr && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr");
     return decode_device(c, c->sc, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, true);
+}
+
+// decode + error count in one call (the reference's decode followed by
+// CErrorAnalyzer::generate, code/x86/CErrorAnalyzer/CErrorAnalyzer.cpp:123-154;
+// code/x86/main_p.cpp:511-540): fused into the decode kernel's epilogue where
+// the kernel writes the hard decisions itself (ldsep), else one count launch
+// after the decode (it needs d_hard then)
+static int decode_count(ldpc_ctx *c, void *s, const void *d_llr, uint8_t *d_hard, void *d_soft, int32_t *d_iters,
+                        int batch, int n_iter, const ldpc_params *p, bool is_float, int k, const uint8_t *d_ref,
+                        unsigned long long *d_counts)
+{
+    if (!c || (!d_llr && batch > 0)) return ldpc_set_error(LDPC_EINVAL, "NULL ctx/llr");
+    if (!d_counts || k < 0 || k > c->code->n) return ldpc_set_error(LDPC_EINVAL, "count: NULL counts or k %d", k);
+    if (!d_hard) return ldpc_set_error(LDPC_EINVAL, "count: d_hard is required");
+    const ErrCount ec{k, d_ref, d_counts};
+    return decode_device(c, c->sc, (hipStream_t)s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, is_float, false,
+                         0, &ec);
+}
+
+extern "C" int ldpc_decode_i8_count_async(ldpc_ctx *c, void *s, const int8_t *d_llr, uint8_t *d_hard, int8_t *d_soft,
+                                          int32_t *d_iters, int batch, int n_iter, const ldpc_params *p, int k,
+                                          const uint8_t *d_ref, unsigned long long *d_counts)
+{
+    return decode_count(c, s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, false, k, d_ref, d_counts);
+}
+
+extern "C" int ldpc_decode_f32_count_async(ldpc_ctx *c, void *s, const float *d_llr, uint8_t *d_hard, float *d_soft,
+                                           int32_t *d_iters, int batch, int n_iter, const ldpc_params *p, int k,
+                                           const uint8_t *d_ref, unsigned long long *d_counts)
+{
+    return decode_count(c, s, d_llr, d_hard, d_soft, d_iters, batch, n_iter, p, true, k, d_ref, d_counts);
 }
 
 // Chunks of the host-buffer path: whole 64-codeword rows, at least 256

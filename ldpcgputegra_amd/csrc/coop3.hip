@@ -262,7 +262,11 @@ struct Slab3 {
         in.v[3] = *(const uint32_t *)(lcb() + rc.pc.w + lrd);
         in.v[4] = *(const uint32_t *)(lcb() + rc.pm.x + lrd);
         in.v[X] = *(const uint32_t *)(inb + prd);
+#ifdef C3X_BANK_MM   // bank-conflict attribution (timing-only builds, results wrong): conflict-free address
+        const uint2 mm = *(const uint2 *)(inb + 8 * lane);
+#else
         const uint2 mm = *(const uint2 *)(inb + mrd);
+#endif
         in.ma = mm.x;
         in.mb = mm.y;
         in.meta = rc.pm.w;
@@ -272,7 +276,12 @@ struct Slab3 {
     LDPC_DEV uint32_t read_x(int g, const St3 &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
         const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 16 * q;
+#ifdef C3X_BANK_X
+        const unsigned short *xz = (const unsigned short *)&sm.xo[g & 1][0][0] + 2 * lane;
+        const uint32_t x0 = xz[0], x1 = xz[1];
+#else
         const uint32_t x0 = xs[0], x1 = xs[8];
+#endif
         return perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127]
     }
 
@@ -462,7 +471,11 @@ struct Slab3 {
             MA = s.mn1;
             MB = s.mn2;
         }
+#ifdef C3X_BANK_MST
+        *(uint2 *)((char *)&sm.mst[g & 1][w][0][0] + 8 * lane) = make_uint2(MA, MB);
+#else
         *(uint2 *)((char *)&sm.mst[g & 1][w][kl][0] + 8 * q) = make_uint2(MA, MB);
+#endif
     }
 };
 
@@ -939,8 +952,13 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 auto read_out = [&]() __attribute__((always_inline)) {   // writeback and store data
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
+#ifdef C3X_BANK_MEM
+                        wbd[w] = *(const uint4 *)(lcb + 16 * lane);
+                        std_[w] = *(const uint4 *)((const char *)&sm.mst[(p - 2) & 1][w][0][0] + 16 * (lane & 31));
+#else
                         wbd[w] = *(const uint4 *)(lcb + (lop[w].w ^ lq));   // row q of the swizzled slot
                         std_[w] = sm.mst[(p - 2) & 1][w][kl][qp];
+#endif
                     });
                 };
                 auto slot_writes = [&]() __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
@@ -952,7 +970,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 auto gathers = [&]() __attribute__((always_inline)) {
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
+#ifndef C3X_BANK_NODMA
                         if (lane < 40) dma16_buf(vr, (gix[w] << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
+#endif
                     });
                 };
                 // the line loads first (their addresses are in VGPRs), then a

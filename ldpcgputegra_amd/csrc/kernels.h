@@ -39,6 +39,12 @@ struct DecodeLaunch {
     // dynamic LDS bytes added to the windowed2 launch (mixed batches: keeps its
     // waves off the CUs of a concurrent coop3 decode, see ldpc_ctx_set_lds_pad)
     int lds_pad;
+    // fused error count (ldpc_decode_*_count_async; kernels that fuse it, else
+    // a count launch after the decode): bits 0 .. cnt_k-1 of each codeword vs
+    // cnt_ref (NULL: all-zero), bit errors += cnt[0], frame errors += cnt[1]
+    unsigned long long *cnt;
+    const uint8_t *cnt_ref;
+    int cnt_k;
 };
 
 int launch_generic(const DecodeLaunch &L, hipStream_t s);

@@ -50,6 +50,9 @@ struct EpArgs {
     int n, vstride, batch, iters, nl, algo, early;
     float beta;
     int32_t *iters_used;
+    unsigned long long *cnt;   // fused error count (DecodeLaunch::cnt), may be null
+    const uint8_t *cnt_ref;
+    int cnt_k;
 };
 
 // lane permutations inside each group of 8 (every lane written: no old value)
@@ -139,10 +142,21 @@ __global__ void __launch_bounds__(64 * EP_WAVES) ldsep_decode(EpArgs a)
     if (a.iters_used && lane == 0) a.iters_used[b] = it;
     uint8_t *hd = a.hard ? a.hard + (size_t)b * a.n : nullptr;
     float *sd = a.soft ? a.soft + (size_t)b * a.n : nullptr;
+    const uint8_t *rf = a.cnt_ref ? a.cnt_ref + (size_t)b * a.n : nullptr;
+    int errs = 0;
     for (int i = lane; i < a.n; i += 64) {
         const float v = V[i];
-        if (hd) hd[i] = v > 0.0f;   // code/x86/CTools/CTools.cpp:370
+        const uint8_t hb = v > 0.0f;   // code/x86/CTools/CTools.cpp:370
+        if (hd) hd[i] = hb;
         if (sd) sd[i] = v;
+        if (a.cnt && i < a.cnt_k) errs += hb != (rf ? rf[i] : 0);   // CErrorAnalyzer.cpp:123-154
+    }
+    if (a.cnt) {   // the whole wave is this codeword: reduce, one atomic pair per failing codeword
+        for (int o = 32; o > 0; o >>= 1) errs += __shfl_xor(errs, o);
+        if (lane == 0 && errs) {
+            atomicAdd(&a.cnt[0], (unsigned long long)errs);
+            atomicAdd(&a.cnt[1], 1ull);
+        }
     }
 }
 
@@ -216,6 +230,9 @@ int launch_ldsep(const LdsCode &lc, const ldpc_code *h, const float *llr, uint8_
     a.early = L.early;
     a.beta = L.beta;
     a.iters_used = L.iters_used;
+    a.cnt = L.cnt;
+    a.cnt_ref = L.cnt_ref;
+    a.cnt_k = L.cnt_k;
     const bool nms = L.algo == 1;
     const size_t shm = (size_t)EP_WAVES * a.vstride * 4;
     const dim3 grid((batch + EP_WAVES - 1) / EP_WAVES), block(64 * EP_WAVES);

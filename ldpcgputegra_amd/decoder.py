@@ -216,6 +216,22 @@ class Decoder:
                                                    sat_pos))
         return q
 
+    def decode_count_device(self, llr, hard, n_iter, k, counts, ref=None, params=None, soft=None, iters_used=None,
+                            stream=None):
+        """decode_*_device + count_errors_device in one call (float or int8 by
+        llr's dtype): counts[0] += bit errors over the first k bits vs ref
+        (None: the all-zero codeword), counts[1] += frame errors; fused into
+        the edge-parallel float kernel's epilogue."""
+        import torch
+        B = llr.shape[0]
+        assert llr.numel() == B * self.code.n and llr.is_contiguous()
+        f32 = llr.dtype == torch.float32
+        p = params or (_lib.default_params(algo=_lib.ALGO_MS) if f32 else _lib.default_params())
+        fn = _lib.lib().ldpc_decode_f32_count_async if f32 else _lib.lib().ldpc_decode_i8_count_async
+        self._on_stream(stream, lambda s: _lib.check(fn(
+            self._ctx, s, self._ptr(llr), self._ptr(hard), self._ptr(soft), self._ptr(iters_used), B, n_iter,
+            C.byref(p), int(k), self._ptr(ref), self._ptr(counts))), self.device)
+
     def count_errors_device(self, hard, k, counts, ref=None, stream=None):
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_count_errors_async(
             self._ctx, s, self._ptr(hard), hard.shape[0], k, self._ptr(ref), self._ptr(counts))), self.device)

@@ -785,3 +785,38 @@ def test_context_per_device_and_bad_device():
         d.close()
     with pytest.raises(LdpcError):
         Decoder(Code("576x288"), device=cnt.value, max_batch=64)
+
+
+@pytest.mark.parametrize("code,dtype,kernel", [("648x324", "f32", 9), ("648x324", "f32", 7), ("576x288", "f32", 9),
+                                               ("dvbs2_r1_2", "i8", 8), ("576x288", "i8", 7)])
+def test_decode_count_matches_separate_count(code, dtype, kernel):
+    """ldpc_decode_*_count_async (decode + CErrorAnalyzer-style count in one
+    call; fused into the ldsep epilogue) gives the hard decisions of the plain
+    decode and the counts ldpc_count_errors_async gives on them, for the
+    all-zero reference and for an explicit reference codeword array."""
+    import torch
+    t = load_table(code)
+    B = 96 if t.n < 10000 else 32
+    iters = 10
+    sigma = channel.sigma_from_ebn0(0.5, t.k_info / t.n)
+    dec = Decoder(Code(code), max_batch=B, kernel=kernel)
+    if dtype == "f32":
+        rng = np.random.default_rng(4)
+        llr = torch.from_numpy((-1.0 + sigma * rng.standard_normal((B, t.n))).astype(np.float32)).cuda()
+        p = default_params(algo=ALGO_MS, beta=0.0)
+    else:
+        llr = torch.from_numpy(channel.awgn_i8_host(t.n, B, seed=4, table=channel.i8_table(sigma))).cuda()
+        p = default_params()
+    ref = torch.from_numpy(np.random.default_rng(9).integers(0, 2, (B, t.n), dtype=np.uint8)).cuda()
+    for r in (None, ref):
+        hard = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+        hard2 = torch.empty_like(hard)
+        c1 = torch.zeros(2, dtype=torch.int64, device="cuda")
+        c2 = torch.zeros(2, dtype=torch.int64, device="cuda")
+        dec.decode_count_device(llr, hard, iters, t.k_info, c1, ref=r, params=p)
+        (dec.decode_f32_device if dtype == "f32" else dec.decode_i8_device)(llr, hard2, iters, params=p)
+        dec.count_errors_device(hard2, t.k_info, c2, ref=r)
+        torch.cuda.synchronize()
+        assert dec.last_kernel == Decoder.KERNEL_NAMES[kernel]
+        assert torch.equal(hard, hard2)
+        assert c1.tolist() == c2.tolist() and c1[1] > 0, (c1.tolist(), c2.tolist())
