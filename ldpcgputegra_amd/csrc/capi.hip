@@ -435,7 +435,8 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
         L.early = p->early_term;
         L.beta = (p->algo == LDPC_ALGO_MS) ? 0.0f : p->beta;
         L.iters_used = d_iters;
-        if (ec && kern == 9) {   // ldsep counts in its epilogue (one wave = one codeword)
+        const bool fuse = ec && kern == 9 && getenv_int("LDPC_FUSED_COUNT", 1) != 0;
+        if (fuse) {   // ldsep counts in its epilogue (one wave = one codeword)
             L.cnt = ec->counts;
             L.cnt_ref = ec->ref;
             L.cnt_k = ec->k;
@@ -454,7 +455,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
             c->events.emplace_back(ev0, ev1);
         }
         if (lr) return ldpc_set_error(LDPC_EDEVICE, "lds decode launch: %s", hipGetErrorString(hipGetLastError()));
-        if (ec && kern != 9 && launch_count_errors(d_hard, h->n, batch, ec->k, ec->ref, ec->counts, s))
+        if (ec && !fuse && launch_count_errors(d_hard, h->n, batch, ec->k, ec->ref, ec->counts, s))
             return ldpc_set_error(LDPC_EDEVICE, "count_errors: %s", hipGetErrorString(hipGetLastError()));
         return LDPC_OK;
     }

@@ -144,9 +144,13 @@ struct alignas(16) Smem3 {
     uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
-    uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post)
-    struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
-        uint4 d[5][8];                //   e < 4: message bytes 16e .. 16e+15, e = 4: the o-edge parity row
+    uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword c at [c ^ (c >> 3)] (chain ->
+                                      // post; the swizzle puts codewords 2q and 2q + 8, which lanes q and q + 4
+                                      // of a slot read, in different banks)
+    struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane L = 16-B
+        uint4 d[40];                  //   piece L): L < 32 message bytes 16 (L & 3) .. +15 of slot L >> 2 (slot-
+                                      //   major: the 8-B pair reads of a half-wave fill 256 B, no bank conflict),
+                                      //   L = 32 + slot the slot's o-edge parity row
     } in[WS][NI];
     uint4 mst[2][WS][8][6];           // window g's outputs per slab wave in mst[g & 1], per slot: its new
                                       // messages (pieces 0..3, 8 pairs x 8 B), the x edge's new V (piece 4)
@@ -234,6 +238,7 @@ struct Slab3 {
     // dword (4 (q >> 1)) and the post's u16 (2 q)
     uint32_t lrd, lwr;
     uint32_t mrd, prd;                // byte offsets in an In record: this lane's message pair / o-edge V dword
+    uint32_t xo0, xo1;                // u16 offsets of codewords 2q, 2q + 1 in an xo block (c ^ (c >> 3))
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
@@ -256,11 +261,21 @@ struct Slab3 {
         in.ad[2] = rc.pc.z + lwr;
         in.ad[3] = rc.pc.w + lwr;
         in.ad[4] = rc.pm.x + lwr;
+#ifdef C3X_BANK_LC   // attribution: the line-cache reads / writes at lane-contiguous addresses
+        const uint32_t lz = (rc.pc.x & 0x30000u) + 4u * (uint32_t)lane;   // keep a data dependence on the record
+        in.v[0] = *(const uint32_t *)(lcb() + lz);
+        in.v[1] = *(const uint32_t *)(lcb() + lz + 256);
+        in.v[2] = *(const uint32_t *)(lcb() + lz + 512);
+        in.v[3] = *(const uint32_t *)(lcb() + lz + 768);
+        in.v[4] = *(const uint32_t *)(lcb() + lz + 1024);
+        in.ad[0] = in.ad[1] = in.ad[2] = in.ad[3] = in.ad[4] = lz;
+#else
         in.v[0] = *(const uint32_t *)(lcb() + rc.pc.x + lrd);   // the dword holding this lane's pair
         in.v[1] = *(const uint32_t *)(lcb() + rc.pc.y + lrd);
         in.v[2] = *(const uint32_t *)(lcb() + rc.pc.z + lrd);
         in.v[3] = *(const uint32_t *)(lcb() + rc.pc.w + lrd);
         in.v[4] = *(const uint32_t *)(lcb() + rc.pm.x + lrd);
+#endif
         in.v[X] = *(const uint32_t *)(inb + prd);
 #ifdef C3X_BANK_MM   // bank-conflict attribution (timing-only builds, results wrong): conflict-free address
         const uint2 mm = *(const uint2 *)(inb + 8 * lane);
@@ -275,12 +290,12 @@ struct Slab3 {
     }
     LDPC_DEV uint32_t read_x(int g, const St3 &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
-        const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 16 * q;
+        const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs;
 #ifdef C3X_BANK_X
         const unsigned short *xz = (const unsigned short *)&sm.xo[g & 1][0][0] + 2 * lane;
         const uint32_t x0 = xz[0], x1 = xz[1];
 #else
-        const uint32_t x0 = xs[0], x1 = xs[8];
+        const uint32_t x0 = xs[xo0], x1 = xs[xo1];   // codewords 2q, 2q + 1 (xo swizzle)
 #endif
         return perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127]
     }
@@ -434,7 +449,11 @@ struct Slab3 {
         constexpr bool FZ = FZ_;
         unsigned short *sx = (unsigned short *)&sm.mst[g & 1][w][kl][4] + q, *so = (unsigned short *)&sm.mst[g & 1][w][kl][5] + q;
         auto put = [&](int j, uint32_t v) __attribute__((always_inline)) {
+#ifdef C3X_BANK_LC
+            *(unsigned short *)(lcw() + s.ad[j] + 256 * j) = (unsigned short)v;
+#else
             *(unsigned short *)(lcw() + s.ad[j]) = (unsigned short)v;
+#endif
         };
         uint32_t MA, MB;
         if constexpr (!TL) {
@@ -537,7 +556,7 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
             C3_STEP_SAME_NMS(w[2], kq[b & 1][4]);
             C3_STEP_CROSS_NMS(w[2], w[3], kq[b & 1][5]);
             C3_STEP_SAME_NMS(w[3], kq[b & 1][6]);
-            sm.xo[buf][b][c] = make_uint4(w[0], w[1], w[2], w[3]);
+            sm.xo[buf][b][c ^ (c >> 3)] = make_uint4(w[0], w[1], w[2], w[3]);
             C3_STEP_CROSS_NMS(w[3], w[0], kq[b & 1][7]);
         } else {
             C3_STEP_SAME(w[0], kq[b & 1][0]);          // pos 0 -> 1
@@ -547,7 +566,7 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
             C3_STEP_SAME(w[2], kq[b & 1][4]);          // 4 -> 5
             C3_STEP_CROSS(w[2], w[3], kq[b & 1][5]);   // 5 -> 6
             C3_STEP_SAME(w[3], kq[b & 1][6]);          // 6 -> 7
-            sm.xo[buf][b][c] = make_uint4(w[0], w[1], w[2], w[3]);
+            sm.xo[buf][b][c ^ (c >> 3)] = make_uint4(w[0], w[1], w[2], w[3]);
             C3_STEP_CROSS(w[3], w[0], kq[b & 1][7]);   // 7 -> 0 (the next block's first input)
         }
     }
@@ -868,10 +887,12 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         // per address (shift-and-add with a per-lane shift and base)
         const i32x4 vr = buffer_rsrc(Vg, 0u, 0xFFFFFFFFu);
         const uint32_t moff = (uint32_t)(Mb - (const char *)Vg), poff = (uint32_t)a.k * 16u;
-        // gathers: lane (e, slot) = (kl, q): e < 4 message piece e, e = 4 the o-edge parity row
-        const uint32_t gshl = kl < 4 ? 6u : 4u, goff = kl < 4 ? moff + 16u * (uint32_t)kl : poff;
-        const uint32_t gmask = kl < 4 ? COOP_CHK_MASK : 0xFFFFu;
-        const uint32_t gsel = (uint32_t)(kl < 4 ? W_META : W_O);
+        // gathers: lane L < 32 = message piece L & 3 of slot L >> 2, L = 32 + slot
+        // the slot's o-edge parity row (Smem3::In)
+        const int ge = lane < 32 ? (lane & 3) : 4, gslot = lane < 32 ? (lane >> 2) : (lane & 7);
+        const uint32_t gshl = ge < 4 ? 6u : 4u, goff = ge < 4 ? moff + 16u * (uint32_t)ge : poff;
+        const uint32_t gmask = ge < 4 ? COOP_CHK_MASK : 0xFFFFu;
+        const uint32_t gsel = (uint32_t)(ge < 4 ? W_META : W_O);
         // stores: lane (kl, q) of slot 8w + kl: q < 4 message piece q, q = 4 the
         // x-edge parity row, q = 5 the tail's last edge, the rest the sink row
         const uint32_t sshl = q < 4 ? 6u : 4u, soff = q < 4 ? moff + 16u * (uint32_t)q : poff;
@@ -880,7 +901,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         const uint32_t snk = q >= 5 ? 0xFFFFFFFFu : 0u, snk_tl = q >= 6 ? 0xFFFFFFFFu : 0u;
         static_assert(MREC == 64, "message block of a check: 1 << 6 bytes");
         auto gather = [&](int w, int g, int ib) __attribute__((always_inline)) {
-            const uint32_t idx = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
+            const uint32_t idx = sm.tab[g & (TQ - 1)][8 * w + gslot][gsel] & gmask;
             if (lane < 40) dma16_buf(vr, (idx << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][ib]);
         };
         // the store of window g's slots 8w .. 8w+7: its row / check index, read
@@ -946,7 +967,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 auto read_gix = [&]() __attribute__((always_inline)) {   // gather indices of window p+1+R
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
-                        gix[w] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
+                        gix[w] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + gslot][gsel] & gmask;
                     });
                 };
                 auto read_out = [&]() __attribute__((always_inline)) {   // writeback and store data
@@ -1049,8 +1070,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     Vg,
                     (uint32_t)(4 * (q >> 1)),
                     (uint32_t)(2 * q),
-                    (uint32_t)(((q >> 1) * 8 + kl) * 16 + (q & 1) * 8),
-                    (uint32_t)((32 + kl) * 16 + 4 * (q >> 1))};
+                    (uint32_t)(kl * 64 + q * 8),
+                    (uint32_t)((32 + kl) * 16 + 4 * (q >> 1)),
+                    (uint32_t)(8 * ((2 * q) ^ (q >> 2))),
+                    (uint32_t)(8 * ((2 * q + 1) ^ (q >> 2)))};
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
         if (STAMP) tseg = stamp3();
