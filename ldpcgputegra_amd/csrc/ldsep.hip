@@ -69,7 +69,11 @@ __global__ void __launch_bounds__(64 * EP_WAVES) ldsep_decode(EpArgs a)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * EP_WAVES + wave;
-    if (b >= a.batch) return;   // whole wave: no workgroup barrier below
+    // a wave past the batch skips the decode but stays for the workgroup's
+    // error-count reduction (the only workgroup barrier, at the end)
+    const bool live_cw = b < a.batch;
+    if (!live_cw && !a.cnt) return;
+    __shared__ unsigned long long ep_cnt[EP_WAVES][2];
     const uint32_t vbase = (uint32_t)wave * (uint32_t)a.vstride * 4u;
     float *V = ep_smem + (size_t)wave * a.vstride;
     char *L = (char *)ep_smem;
@@ -85,10 +89,11 @@ __global__ void __launch_bounds__(64 * EP_WAVES) ldsep_decode(EpArgs a)
     // so the sign bit of c is exactly the reference's c < 0.  Only the sign of
     // a zero soft value can differ from the reference's, never a comparison.
     const float *src = a.llr + (size_t)b * a.n;
-    for (int i = lane; i < a.n; i += 64) V[i] = src[i] + 0.0f;
+    if (live_cw)
+        for (int i = lane; i < a.n; i += 64) V[i] = src[i] + 0.0f;
     if (lane < 2) V[a.n + lane] = -__builtin_huge_valf();
     int it = 0;
-    while (it < a.iters) {
+    while (live_cw && it < a.iters) {
 #pragma unroll
         for (int l = 0; l < NL; l++) {
             float c[NP];
@@ -139,23 +144,29 @@ __global__ void __launch_bounds__(64 * EP_WAVES) ldsep_decode(EpArgs a)
             if (__builtin_amdgcn_ballot_w64(bad != 0) == 0) break;
         }
     }
-    if (a.iters_used && lane == 0) a.iters_used[b] = it;
+    if (a.iters_used && lane == 0 && live_cw) a.iters_used[b] = it;
     uint8_t *hd = a.hard ? a.hard + (size_t)b * a.n : nullptr;
     float *sd = a.soft ? a.soft + (size_t)b * a.n : nullptr;
     const uint8_t *rf = a.cnt_ref ? a.cnt_ref + (size_t)b * a.n : nullptr;
     int errs = 0;
-    for (int i = lane; i < a.n; i += 64) {
+    for (int i = lane; live_cw && i < a.n; i += 64) {
         const float v = V[i];
         const uint8_t hb = v > 0.0f;   // code/x86/CTools/CTools.cpp:370
         if (hd) hd[i] = hb;
         if (sd) sd[i] = v;
         if (a.cnt && i < a.cnt_k) errs += hb != (rf ? rf[i] : 0);   // CErrorAnalyzer.cpp:123-154
     }
-    if (a.cnt) {   // the whole wave is this codeword: reduce, one atomic pair per failing codeword
+    if (a.cnt) {   // wave = codeword; then the workgroup's 4 codewords: one atomic pair per workgroup
         for (int o = 32; o > 0; o >>= 1) errs += __shfl_xor(errs, o);
-        if (lane == 0 && errs) {
-            atomicAdd(&a.cnt[0], (unsigned long long)errs);
-            atomicAdd(&a.cnt[1], 1ull);
+        if (lane == 0) {
+            ep_cnt[wave][0] = (unsigned long long)errs;
+            ep_cnt[wave][1] = errs ? 1ull : 0ull;
+        }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+            unsigned long long s = 0;
+            for (int w = 0; w < EP_WAVES; w++) s += ep_cnt[w][threadIdx.x];
+            if (s) atomicAdd(&a.cnt[threadIdx.x], s);
         }
     }
 }
