@@ -461,7 +461,7 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     }
     const bool win = kern >= 2 && kern != 11;
     // + a sink row / sink words for the masked stores of the coop kernel
-    const size_t msg_zero = (kern == 8    ? coop3_msg_bytes(h, stride)
+    const size_t msg_zero = (kern == 8    ? 0
                              : kern == 11 ? stairf_msg_bytes(c->stairf, stride)
                              : win        ? windowed_msg_bytes(h, stride)
                                       : (size_t)h->e * stride * esz) +
@@ -494,7 +494,8 @@ static int decode_device(ldpc_ctx *c, Scratch &sc, hipStream_t s, const void *d_
     // messages start at 0 (CDecoder_OMS_fixed_SSE.cpp:129-131); the all-zero
     // compressed word is the all-zero message set as well.
     if (kern == 8) {
-        if (launch_zero_rows((char *)sc.d_V + vpart, vgroup, ((size_t)(h->m + 1) * 64 + 15) / 16 * 16, stride / 16, s))
+        if (launch_zero_rows((char *)sc.d_V + vpart, vgroup, ((size_t)(h->m + 1) * coop3_mrec(h->group_deg[0]) + 15) / 16 * 16,
+                             stride / 16, s))
             return ldpc_set_error(LDPC_EDEVICE, "message zeroing: %s", hipGetErrorString(hipGetLastError()));
     } else
         HIP_TRY(hipMemsetAsync(sc.d_msg, 0, msg_zero, s));

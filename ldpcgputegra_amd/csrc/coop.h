@@ -57,7 +57,7 @@ struct CoopPlan {
 // forwarded through the LDS ring; -1: no cooperative schedule
 int coop_build_plan(const ldpc_code *h, int S, int R, int dist, int recw, CoopPlan &o, bool want_tab);
 
-// ---- coop3.hip: slab waves doing pre + post, i16 chain (D0 = 7) ----
+// ---- coop3.hip: slab waves doing pre + post, i16 chain (first-group degree 7 or 10) ----
 bool coop3_params_ok(const ldpc_params *p, const CoopCode &cc);
 bool coop3_stride_ok(int stride);
 // coop3's per-group block (V rows, then messages): bytes of the V part and of
@@ -65,7 +65,7 @@ bool coop3_stride_ok(int stride);
 void coop3_group_layout(const ldpc_code *h, size_t *vpart, size_t *block);
 size_t coop3_group_bytes(const ldpc_code *h);
 // compressed messages: [stride / 16][m + 1][8 pairs][2] u32 (4 B per codeword and check; row m is the sink)
-size_t coop3_msg_bytes(const ldpc_code *h, int stride);
+int coop3_mrec(int d0);   // message bytes per check and 16-codeword group (64: first-group degree <= 8, 96: <= 16)
 int coop3_upload(const ldpc_code *h, CoopCode *cc);
 // host side of the coop3 schedule (coop3.hip): permuted slot records
 struct Coop3Host {
@@ -85,7 +85,6 @@ constexpr int LC_GAP = 10;    // accesses of a line >= LC_GAP periods apart: sep
 constexpr int LC_LEAD = 3;   // a line is loaded (into VGPRs) >= 3 periods before its first access
 constexpr int LC_PUT = 2;    // ... and written to its slot 2 periods after its load (coop3: loads first in a
                              // period, vmcnt(36) at its end completes those of the period before)
-constexpr int LC_OPS = 48;   // line loads / writebacks per period: 6 slab waves x 8 lane groups
 // A line's 8 rows sit in its slot XOR-swizzled: row i at piece position i ^ z
 // (z = 0..7 per residency, chosen by the planner so that the 4 pieces one
 // 32-lane half of a pre read / post write touches fall in distinct bank
@@ -97,7 +96,8 @@ constexpr uint32_t LC_SLOT_MASK = (1u << LC_SLOT_BITS) - 1;
 struct LcPlan {
     int slots = 0;                 // LDS line slots used, the sink (slot 0) included
     int residencies = 0;           // line residencies per iteration
-    std::vector<uint32_t> ops;     // [nw][LC_OPS][2]: load line | writeback line << 16,
+    std::vector<uint32_t> ops;     // [nw][S][2] (S line loads / writebacks per period, one per slab-wave lane
+                                   //   group): load line | writeback line << 16,
                                    //   slot written (the load of 2 periods earlier) | writeback slot << 16
                                    //   (each 16-bit slot field: slot | z << LC_SLOT_BITS)
     std::vector<uint32_t> piece;   // [nw][S][D0 - 2]: LDS byte offset (from the cache) of each info entry's piece

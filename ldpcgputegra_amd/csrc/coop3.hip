@@ -90,22 +90,44 @@ LDPC_DEV void dma16_buf(i32x4 rsrc, uint32_t voff, uint32_t lds_dst)
                  : "memory");
 }
 
-constexpr int D0 = 7, X = D0 - 2;   // first-group check degree, information edges per check
-constexpr int RECW = 12;            // slot record words (coop3_upload)
 constexpr int DPER = 2;             // a window table's LDS-DMA is waited for DPER periods after its issue
 constexpr int TQ = 8;               // window-table slots in LDS
-constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is the sink)
 
-// slot record (coop3_upload): words 0..4 the LDS byte offsets (from the line
-// cache) of the info entries' 16-B pieces, 5 / 6 the x / o edge parity rows
-// (row - k) in their low halves -- word 5's high half the u16 index of the
-// slot's chain input in xo[buf] and word 6's the byte offset of its chain
-// constants in cst[buf] (from its chain step: the pre needs no arithmetic on
-// it) -- 7 meta = check | COOP_M_ACT | chain step << STEP_SHIFT, 8 .. 11
-// the period's line ops of lane group (slot & 7) of the slot's slab wave
-// (LcPlan::ops) as byte offsets: 8 the line loaded, 9 the line written back
-// (from the group's V block), 10 the slot written with the load of LC_PUT
-// periods earlier, 11 the slot written back (from the line cache)
+// Per first-group check degree D0 (G3): DVB-S2 r1/2 (D0 = 7, 5 information
+// edges per check) and r2/3 (D0 = 10, 8), code/gpu_fixed/matrix/64800x21600.
+//
+// slot record (coop3_upload), X = D0 - 2: words 0 .. X-1 the LDS byte offsets
+// (from the line cache) of the info entries' 16-B pieces, W_X / W_O the x / o
+// edge parity rows (row - k) in their low halves -- W_X's high half the u16
+// index of the slot's chain input in xo[buf] and W_O's the byte offset of its
+// chain constants in cst[buf] (from its chain step: the pre needs no
+// arithmetic on it) -- W_META = check | COOP_M_ACT | chain step << STEP_SHIFT,
+// W_LOP .. W_LOP+3 the period's line ops of lane group (slot & 7) of the
+// slot's slab wave (LcPlan::ops) as byte offsets: the line loaded, the line
+// written back (from the group's V block), the slot written with the load of
+// LC_PUT periods earlier, the slot written back (from the line cache)
+//
+// Messages of a check, per 16-codeword group (MREC bytes): [8 pairs][MA0,
+// MB] u32 (MB: eps cst1 / eps cst2 bytes per codeword; MA0: 2-bit codes of
+// edges 0..7, 16 bits per codeword), then for D0 > 8 [8 pairs][MA1] (edges
+// 8 .. 15): 4 B (D0 <= 8) or 6 B per codeword and check.
+template <int D0_>
+struct G3 {
+    static constexpr int D0 = D0_, X = D0 - 2;                 // check degree, information edges per check
+    static constexpr int NMA = (D0 + 7) / 8;                   // edge-code words per codeword pair
+    static constexpr int MREC = 32 * (NMA + 1);                // message bytes per check and group
+    static constexpr int MP = MREC / 16;                       // message pieces (16 B) per check
+    static constexpr int NG = MP + 1;                          // pieces gathered per slot (+ the o-edge parity row)
+    static constexpr int W_X = X, W_O = X + 1, W_META = X + 2;
+    static constexpr int W_LOP = (W_META + 1 + 3) / 4 * 4;     // line-op words (one uint4)
+    static constexpr int RECW = W_LOP + 4;                     // slot record words
+    static constexpr int NR = (W_META + 1 + 3) / 4;            // uint4 a pre reads of its record
+    static constexpr int WS = D0 == 7 ? 6 : 4;                 // slab waves: S = 8 WS checks per window (r1/2's
+                                                               // windows fill 45 of 48, r2/3's 30 of 32)
+    static constexpr int LCS = D0 == 7 ? 752 : 848;            // line-cache slots (128 B each; slot 0 the sink):
+                                                               // what the 160 KB of LDS leave beside the rest
+    static_assert(NMA <= 2 && 8 * NG <= 64 && MP + 2 <= 8, "message pieces: one gather and one store per slot set");
+};
 #ifndef LDPC_C3_MSLEEP
 #define LDPC_C3_MSLEEP 4      // memory wave: s_sleep (x 64 cycles) after its line loads, before its LDS burst
 #endif
@@ -119,9 +141,6 @@ constexpr int LC_SLOTS = 752;       // line-cache slots (128 B each; slot 0 is t
 #define LDPC_C3_SWROT 0       // experiment: slab index = (the wave's slab position + SWROT) % WS (same-box
                               // A/B of 3 vs 0: -0.8 % on one box, +0.5 % on another)
 #endif
-constexpr int W_X = 5, W_O = 6, W_META = 7, W_LOP = 8;
-static_assert(W_LOP + 4 <= RECW, "line-op words");
-
 template <int WS, int R>
 struct Cfg {
     static constexpr int S = 8 * WS;                   // checks per window
@@ -129,30 +148,34 @@ struct Cfg {
     static constexpr int NI = R + 1;                   // LDS-DMA input windows in flight per slab wave
     static constexpr int NS = R + 1 < 3 ? 3 : R + 1;   // window states in VGPRs (pre at p-1, post at p+1)
     static constexpr int U = NS;                       // periods unrolled (multiple of NI and NS)
-    static constexpr int CHW = WS >= 3 ? 3 : WS;       // the chain wave (waves go to SIMDs 0,2,1,3,0,2,1: wave 3
-                                                       // has a SIMD of its own for WS = 3 and WS = 6)
+    // the chain wave (waves go to SIMDs 0,2,1,3,0,2,1,3): WS = 6: wave 3, a
+    // SIMD of its own beside the memory wave (two slab waves on each other
+    // SIMD); WS = 4: wave 4, so that the 4 slab waves have a SIMD each (the
+    // chain shares SIMD 0, the memory wave SIMD 2)
+    static constexpr int CHW = WS == 4 ? 4 : (WS >= 3 ? 3 : WS);
     static constexpr int NB = S / 8;                   // chain blocks of 8 steps
     static_assert(TQ >= KAHEAD + 2, "table ring: a window's records are read until its stores");
     static_assert(U % NI == 0 && U % NS == 0 && U % 3 == 0, "unroll");
 };
 
-template <int WS, int R>
+template <int D0, int WS, int R>
 struct alignas(16) Smem3 {
     using CF = Cfg<WS, R>;
+    using G = G3<D0>;
     static constexpr int S = CF::S, NI = CF::NI;
-    uint4 lc[LC_SLOTS][8];            // line cache: slot = 8 V rows x 16 codewords (LcPlan; slot 0: the sink)
-    uint32_t tab[TQ][S][RECW];        // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
+    uint4 lc[G::LCS][8];              // line cache: slot = 8 V rows x 16 codewords (LcPlan; slot 0: the sink)
+    uint32_t tab[TQ][S][G::RECW];     // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
     uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post; a
                                       // codeword swizzle c ^ (c >> 3) that removes the 2-way bank conflict of
                                       // read_x measured 0.3 % slower, r05g)
     struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
-        uint4 d[5][8];                //   e < 4: message bytes 16e .. 16e+15, e = 4: the o-edge parity row
+        uint4 d[G::NG][8];            //   e < MP: message bytes 16e .. 16e+15, e = MP: the o-edge parity row
     } in[WS][NI];
-    uint4 mst[2][WS][8][6];           // window g's outputs per slab wave in mst[g & 1], per slot: its new
-                                      // messages (pieces 0..3, 8 pairs x 8 B), the x edge's new V (piece 4)
-                                      // and the tail's last edge's (5), 16 codewords each (posted in period
+    uint4 mst[2][WS][8][G::MP + 2];   // window g's outputs per slab wave in mst[g & 1], per slot: its new
+                                      // messages (pieces 0..MP-1), the x edge's new V (piece MP) and the
+                                      // tail's last edge's (MP + 1), 16 codewords each (posted in period
                                       // g+1, stored by the memory wave in period g+2: lane q its piece q)
 };
 
@@ -160,7 +183,7 @@ struct Coop3Args {
     int8_t *V;                        // grouped V: Vg[group][row][16], groups gstride bytes apart; row n (and the
                                       // sink line n / 8) is the sink of inactive slots and unused line ops
     uint8_t *Mc;                      // [pitch / 16][mrows][8 pairs][2] u32; row m is the sink
-    const uint32_t *tab;              // [nw][S][RECW] slot records
+    const uint32_t *tab;              // [nw][S][G3::RECW] slot records
     const uint32_t *lc_pro, *lc_epi;  // line cache: resident lines at a segment start / written back at its end
     unsigned long long *stamps;       // diagnostic build: [grid][waves][4]
     // in-kernel early termination (ET kernels): layered edge list (group 0:
@@ -180,22 +203,26 @@ struct Coop3Args {
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset) + 255 (R - coff: C form), offset per half (value form)
 };
 
+template <int D0>
 struct St3 {                          // one window's state from pre to post (R / C pairs)
+    static constexpr int X = D0 - 2;
     uint32_t c[D0 - 1];               // contributions (info, o); tail: new V
     uint32_t a[D0 - 1];               // |c| (not clipped: min1 / min2 are, where the constants are made)
     uint32_t mn1, mn2, sacc, mx;      // min1 / min2 / sign parity over info + o; x-edge old message
-                                      // tail: mn1 = MA, mn2 = MB
+                                      // tail: mn1 = MA0, mn2 = MB, ma1 = MA1
+    uint32_t ma1;
     uint32_t xs;                      // the slot's chain step: u16 index of its x input in xo[buf]
     uint32_t ad[X];                   // the info edges' pair addresses in the line cache (pre reads, post writes)
     uint32_t v[X];                    // FZ (early termination): the info edges' V as read (R pairs)
 };
 
-// record meta (word D0): check | COOP_M_ACT | chain step << STEP_SHIFT.  The
-// host permutes a window's checks over its slots (coop3_upload: every
-// distance-2 writer and reader in slab wave 0); the chain runs the steps in
-// check order, so a slot's constants / x input sit at its step
+// record meta (word W_META = D0): check | COOP_M_ACT | chain step <<
+// STEP_SHIFT.  The host permutes a window's checks over its slots
+// (coop3_upload: every distance-2 writer and reader in slab wave 0); the
+// chain runs the steps in check order, so a slot's constants / x input sit at
+// its step
 constexpr int STEP_SHIFT = 22;
-static_assert(W_META == D0, "meta word");
+static_assert(G3<7>::W_META == 7 && G3<10>::W_META == 10, "meta word = plan record word D0");
 
 LDPC_DEV uint32_t pk_ashr8(uint32_t a) { return us(sv(a) >> (short)8); }
 LDPC_DEV uint32_t pk_add(uint32_t a, uint32_t b) { return us(sv(a) + sv(b)); }
@@ -208,23 +235,44 @@ LDPC_DEV uint32_t nms_v(uint32_t r, uint32_t f) { return us(__builtin_bit_cast(s
 LDPC_DEV uint32_t nms_c(uint32_t r, uint32_t f) { return (pk_mul_lo(pk_ashr8(r), f) << 3) & HIBYTES; }   // (<= 4032 << 3: no carry between halves)
 LDPC_DEV uint32_t pk_shl5(uint32_t a) { return us(sv(a) << (short)5); }
 
-// a window's records of one slot as a pre reads them: info pieces 0..3, and
-// (piece 4, x row, o row, meta)
+// a window's records of one slot as a pre reads them: words 0 .. W_META
+template <int D0>
 struct Rec {
-    uint4 pc, pm;
+    uint4 r[G3<D0>::NR];
+    LDPC_DEV uint32_t w(int i) const
+    {
+        const uint4 &q = r[i >> 2];
+        return (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
+    }
 };
 // what a pre reads from LDS
+template <int D0>
 struct PreIn {
+    static constexpr int X = D0 - 2;
     uint32_t v[D0 - 1];               // raw V dwords (info edges from the line cache, the o edge from In)
     uint32_t ad[X];                   // the info pairs' byte offsets in the line cache
-    uint32_t ma, mb;                  // old message record of this pair
-    uint32_t meta, wx, wo;            // record words 7, 5, 6
+    uint32_t ma, mb, ma1;             // old message record of this pair (MA1: D0 > 8)
+    uint32_t meta, wx, wo;            // record words W_META, W_X, W_O
 };
 
-template <int WS, int R, bool NMS = false>
+// old message / new code of edge J: edges 0..7 in MA0, 8..15 in MA1
+template <int J>
+LDPC_DEV uint32_t old_msg2(uint32_t MA0, uint32_t MA1, const MsgTab &t, const PkK &K)
+{
+    if constexpr (J < 8)
+        return old_msg<J>(MA0, t, K.m3, K.c4);
+    else
+        return old_msg<J - 8>(MA1, t, K.m3, K.c4);
+}
+
+template <int D0, int WS, int R, bool NMS = false>
 struct Slab3 {
-    using SM = Smem3<WS, R>;
-    static constexpr int S = SM::S;
+    using SM = Smem3<D0, WS, R>;
+    using G = G3<D0>;
+    using St = St3<D0>;
+    using RecT = Rec<D0>;
+    using In = PreIn<D0>;
+    static constexpr int S = SM::S, X = G::X;
     SM &sm;
     const Coop3Args &a;
     int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
@@ -236,6 +284,7 @@ struct Slab3 {
     // dword (4 (q >> 1)) and the post's u16 (2 q)
     uint32_t lrd, lwr;
     uint32_t mrd, prd;                // byte offsets in an In record: this lane's message pair / o-edge V dword
+    uint32_t m1rd;                    // D0 > 8: byte offset of this lane's MA1 word in an In record
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
@@ -244,35 +293,22 @@ struct Slab3 {
     LDPC_DEV char *lcw() const { return (char *)&sm.lc[0][0]; }
 
     // ---- reads
-    LDPC_DEV Rec read_rec(int g) const
+    LDPC_DEV RecT read_rec(int g) const
     {
         const uint4 *r = (const uint4 *)&sm.tab[g & (TQ - 1)][k][0];
-        return {r[0], r[1]};
+        RecT o;
+#pragma unroll
+        for (int i = 0; i < G::NR; i++) o.r[i] = r[i];
+        return o;
     }
     // pre inputs of the window whose records are rc (its gathers landed in in[w][ib])
-    LDPC_DEV void read_pre(int ib, const Rec &rc, PreIn &in) const
+    LDPC_DEV void read_pre(int ib, const RecT &rc, In &in) const
     {
         const char *inb = (const char *)&sm.in[w][ib];
-        in.ad[0] = rc.pc.x + lwr;
-        in.ad[1] = rc.pc.y + lwr;
-        in.ad[2] = rc.pc.z + lwr;
-        in.ad[3] = rc.pc.w + lwr;
-        in.ad[4] = rc.pm.x + lwr;
-#ifdef C3X_BANK_LC   // attribution: the line-cache reads / writes at lane-contiguous addresses
-        const uint32_t lz = (rc.pc.x & 0x30000u) + 4u * (uint32_t)lane;   // keep a data dependence on the record
-        in.v[0] = *(const uint32_t *)(lcb() + lz);
-        in.v[1] = *(const uint32_t *)(lcb() + lz + 256);
-        in.v[2] = *(const uint32_t *)(lcb() + lz + 512);
-        in.v[3] = *(const uint32_t *)(lcb() + lz + 768);
-        in.v[4] = *(const uint32_t *)(lcb() + lz + 1024);
-        in.ad[0] = in.ad[1] = in.ad[2] = in.ad[3] = in.ad[4] = lz;
-#else
-        in.v[0] = *(const uint32_t *)(lcb() + rc.pc.x + lrd);   // the dword holding this lane's pair
-        in.v[1] = *(const uint32_t *)(lcb() + rc.pc.y + lrd);
-        in.v[2] = *(const uint32_t *)(lcb() + rc.pc.z + lrd);
-        in.v[3] = *(const uint32_t *)(lcb() + rc.pc.w + lrd);
-        in.v[4] = *(const uint32_t *)(lcb() + rc.pm.x + lrd);
-#endif
+#pragma unroll
+        for (int j = 0; j < X; j++) in.ad[j] = rc.w(j) + lwr;
+#pragma unroll
+        for (int j = 0; j < X; j++) in.v[j] = *(const uint32_t *)(lcb() + rc.w(j) + lrd);   // the dword holding this lane's pair
         in.v[X] = *(const uint32_t *)(inb + prd);
 #ifdef C3X_BANK_MM   // bank-conflict attribution (timing-only builds, results wrong): conflict-free address
         const uint2 mm = *(const uint2 *)(inb + 8 * lane);
@@ -281,11 +317,12 @@ struct Slab3 {
 #endif
         in.ma = mm.x;
         in.mb = mm.y;
-        in.meta = rc.pm.w;
-        in.wx = rc.pm.y;
-        in.wo = rc.pm.z;
+        in.ma1 = G::NMA > 1 ? *(const uint32_t *)(inb + m1rd) : 0u;
+        in.meta = rc.w(G::W_META);
+        in.wx = rc.w(G::W_X);
+        in.wo = rc.w(G::W_O);
     }
-    LDPC_DEV uint32_t read_x(int g, const St3 &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
+    LDPC_DEV uint32_t read_x(int g, const St &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
         const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 16 * q;
 #ifdef C3X_BANK_X
@@ -299,7 +336,7 @@ struct Slab3 {
 
     // pre of window g: chain constants -> cst[g & 1], state -> s
     template <bool TL, bool FZ_ = false, int MP = -1>
-    LDPC_DEV void pre(int g, const PreIn &in, St3 &s) const
+    LDPC_DEV void pre(int g, const In &in, St &s) const
     {
         constexpr bool FZ = FZ_;
         const uint32_t meta = in.meta;
@@ -309,7 +346,7 @@ struct Slab3 {
 #pragma unroll
         for (int j = 0; j < X; j++) s.ad[j] = in.ad[j];
         const MsgTab t = msg_tab(in.mb);
-        const uint32_t MA = in.ma, neg127 = K.neg127, c510 = K.c510;
+        const uint32_t MA = in.ma, MA1 = in.ma1, neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
         uint32_t A, B, EPS, COV, L, H;
         if constexpr (!TL) {
@@ -321,7 +358,7 @@ struct Slab3 {
             // and |c| (abs_sat caps it at R(127) as the reference's clamp does)
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_sub_sat(v[J], old_msg<J>(MA, t, K.m3, K.c4));
+                const uint32_t c = pk_sub_sat(v[J], old_msg2<J>(MA, MA1, t, K));
                 const uint32_t aj = abs_sat(c, c510);
                 s.c[J] = c;
                 s.a[J] = aj;
@@ -338,14 +375,14 @@ struct Slab3 {
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
-            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg<D0 - 1>(MA, t, K.m3, K.c4)), neg127);
+            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg2<D0 - 1>(MA, MA1, t, K)), neg127);
             const uint32_t ao = abs_r(cor, c510);
             s.c[X] = cor;
             s.a[X] = ao;
             s.sacc = sacc ^ cor;
             s.mn2 = pk_max(min1, pk_min(ao, min2));
             s.mn1 = pk_min(min1, ao);
-            const uint32_t mx = old_msg<X>(MA, t, K.m3, K.c4);
+            const uint32_t mx = old_msg2<X>(MA, MA1, t, K);
             s.mx = mx;
             // chain constants in value form (R >> 8, C >> 8), both codewords at once
             COV = pk_ashr8(cor);
@@ -378,7 +415,7 @@ struct Slab3 {
             // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg<J>(MA, t, K.m3, K.c4)), neg127);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg2<J>(MA, MA1, t, K)), neg127);
                 // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2
                 const uint32_t aj = NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510);
                 s.c[J] = c;
@@ -391,16 +428,20 @@ struct Slab3 {
                                     : pk_min(pk_max(pk_sub(min2, K.coff), 0u), K.rmm) & HIBYTES;
             const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
                                     : pk_min(pk_max(pk_sub(min1, K.coff), 0u), K.rmm) & HIBYTES;
-            uint32_t e1, e2, MAn = 0;
+            uint32_t e1, e2, MAn = 0, MAn1 = 0;
             signed_csts(k1, k2, sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u), e1, e2);
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                s.c[J] = new_v_later<J>(s.c[J], s.a[J], min1, e1, e2, MAn, neg127);
+                if constexpr (J < 8)
+                    s.c[J] = new_v_later<J>(s.c[J], s.a[J], min1, e1, e2, MAn, neg127);
+                else
+                    s.c[J] = new_v_later<J - 8>(s.c[J], s.a[J], min1, e1, e2, MAn1, neg127);
                 if constexpr (FZ) s.c[J] = bfi(fm, v[J], s.c[J]);   // converged codewords keep their V
             });
             s.mx = 0;
             s.sacc = 0;
             s.mn1 = MAn;
+            s.ma1 = MAn1;
             s.mn2 = perm(e2, e1, 0x07030501u);
             // the chain passes V[p_0] (the tail's last edge) on: A = B = c_o = L = H = y
             // (NMS: A = 32 y, B = 32 y + 31)
@@ -441,18 +482,24 @@ struct Slab3 {
     // the addresses its pre read), messages and parity V -> mst[g & 1][w][kl];
     // those leave in the memory wave's store of period g + 2
     template <bool TL, bool FZ_ = false, int MP = -1>
-    LDPC_DEV void post(int g, uint32_t xr, const St3 &s) const
+    LDPC_DEV void post(int g, uint32_t xr, const St &s) const
     {
         constexpr bool FZ = FZ_;
-        unsigned short *sx = (unsigned short *)&sm.mst[g & 1][w][kl][4] + q, *so = (unsigned short *)&sm.mst[g & 1][w][kl][5] + q;
+        unsigned short *sx = (unsigned short *)&sm.mst[g & 1][w][kl][G::MP] + q,
+                       *so = (unsigned short *)&sm.mst[g & 1][w][kl][G::MP + 1] + q;
         auto put = [&](int j, uint32_t v) __attribute__((always_inline)) {
-#ifdef C3X_BANK_LC
-            *(unsigned short *)(lcw() + s.ad[j] + 256 * j) = (unsigned short)v;
-#else
             *(unsigned short *)(lcw() + s.ad[j]) = (unsigned short)v;
-#endif
         };
-        uint32_t MA, MB;
+        // edge J's code into MA (J < 8) or MA1
+        auto nv = [&](auto jc, uint32_t c, uint32_t av, uint32_t min1, uint32_t e1, uint32_t e2, uint32_t &MA0,
+                      uint32_t &MA1_) __attribute__((always_inline)) -> uint32_t {
+            constexpr int J = decltype(jc)::value;
+            if constexpr (J < 8)
+                return new_v<J>(c, av, min1, e1, e2, MA0, K.c510);
+            else
+                return new_v<J - 8>(c, av, min1, e1, e2, MA1_, K.c510);
+        };
+        uint32_t MA, MB, MA1 = 0;
         if constexpr (!TL) {
             const uint32_t cx = pk_sub_sat(xr, s.mx);   // unclamped, as the info edges' (new_v)
             const uint32_t ax = abs_sat(cx, K.c510);
@@ -467,15 +514,18 @@ struct Slab3 {
             MA = 0;
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t n = new_v<J>(s.c[J], s.a[J], min1, e1, e2, MA, K.c510);
+                const uint32_t n = nv(jc, s.c[J], s.a[J], min1, e1, e2, MA, MA1);
                 put(J, FZ ? perm(n, s.v[J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
-            const uint32_t nx = new_v<X>(cx, ax, min1, e1, e2, MA, K.c510);
+            const uint32_t nx = nv(std::integral_constant<int, X>{}, cx, ax, min1, e1, e2, MA, MA1);
             *sx = (unsigned short)(FZ ? perm(nx, xr, psel) : pack_v(nx));
             // the o edge: its code only (the next check rewrites V[o] as its x edge)
-            msg_code<D0 - 1>(s.c[X], s.a[X], min1, MA);
+            if constexpr (D0 - 1 < 8)
+                msg_code<D0 - 1>(s.c[X], s.a[X], min1, MA);
+            else
+                msg_code<D0 - 9>(s.c[X], s.a[X], min1, MA1);
             MB = perm(e2, e1, 0x07030501u);
         } else {
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
@@ -486,12 +536,14 @@ struct Slab3 {
             *so = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
             MA = s.mn1;
             MB = s.mn2;
+            MA1 = s.ma1;
         }
 #ifdef C3X_BANK_MST
         *(uint2 *)((char *)&sm.mst[g & 1][w][0][0] + 8 * lane) = make_uint2(MA, MB);
 #else
         *(uint2 *)((char *)&sm.mst[g & 1][w][kl][0] + 8 * q) = make_uint2(MA, MB);
 #endif
+        if constexpr (G::NMA > 1) *(uint32_t *)((char *)&sm.mst[g & 1][w][kl][4] + 4 * q) = MA1;   // [8 pairs][MA1]
     }
 };
 
@@ -621,11 +673,12 @@ LDPC_DEV uint32_t row_hbits(uint4 y)
 // converging now and freezes them, and leaves when none is live.  Same result
 // as the reference's per-codeword stop (oracle: syndrome after every
 // iteration), in one launch.
-template <int WS, int R, bool STAMP, bool ET = false, bool NMS = false>
+template <int D0, int WS, int R, bool STAMP, bool ET = false, bool NMS = false>
 __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 {
-    using SM = Smem3<WS, R>;
+    using SM = Smem3<D0, WS, R>;
     using CF = Cfg<WS, R>;
+    using GG = G3<D0>;
     constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U, CHW = CF::CHW, NB = CF::NB;
     __shared__ SM sm;
 
@@ -817,7 +870,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     if (wave == CHW) {
         // ------------------------------------------------------------ chain wave
         if (a.prio) __builtin_amdgcn_s_setprio(3);
-        constexpr int TABW = S * RECW;   // words per window table
+        constexpr int TABW = S * GG::RECW;   // words per window table
         constexpr int NCH = TABW / 4;   // 16-B chunks per window table
         constexpr int CPL = (NCH + 63) / 64;
         static_assert(CPL * DPER <= 63, "table staging");
@@ -884,22 +937,34 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         // per address (shift-and-add with a per-lane shift and base)
         const i32x4 vr = buffer_rsrc(Vg, 0u, 0xFFFFFFFFu);
         const uint32_t moff = (uint32_t)(Mb - (const char *)Vg), poff = (uint32_t)a.k * 16u;
-        // gathers: lane (e, slot) = (kl, q): e < 4 message piece e, e = 4 the
+        // gathers: lane (e, slot) = (kl, q): e < MP message piece e, e = MP the
         // o-edge parity row (Smem3::In; a slot-major order without the pair
         // reads' 2-way bank conflict measured 0.3 % slower, r05g)
-        const uint32_t gshl = kl < 4 ? 6u : 4u, goff = kl < 4 ? moff + 16u * (uint32_t)kl : poff;
-        const uint32_t gmask = kl < 4 ? COOP_CHK_MASK : 0xFFFFu;
-        const uint32_t gsel = (uint32_t)(kl < 4 ? W_META : W_O);
-        // stores: lane (kl, q) of slot 8w + kl: q < 4 message piece q, q = 4 the
-        // x-edge parity row, q = 5 the tail's last edge, the rest the sink row
-        const uint32_t sshl = q < 4 ? 6u : 4u, soff = q < 4 ? moff + 16u * (uint32_t)q : poff;
-        const uint32_t stw = 4u * (uint32_t)(q < 4 ? W_META : q == 4 ? W_X : W_O);
-        const uint32_t stm = q < 4 ? COOP_CHK_MASK : 0xFFFFu;
-        const uint32_t snk = q >= 5 ? 0xFFFFFFFFu : 0u, snk_tl = q >= 6 ? 0xFFFFFFFFu : 0u;
-        static_assert(MREC == 64, "message block of a check: 1 << 6 bytes");
+        constexpr int MP = GG::MP;
+        constexpr uint32_t MREC = GG::MREC;
+        const uint32_t gshl = kl < MP ? 6u : 4u, goff = kl < MP ? moff + 16u * (uint32_t)kl : poff;
+        const uint32_t gmul = kl < MP ? MREC : 16u;
+        const uint32_t gmask = kl < MP ? COOP_CHK_MASK : 0xFFFFu;
+        const uint32_t gsel = (uint32_t)(kl < MP ? GG::W_META : GG::W_O);
+        // stores: lane (kl, q) of slot 8w + kl: q < MP message piece q, q = MP the
+        // x-edge parity row, q = MP + 1 the tail's last edge, the rest the sink row
+        const uint32_t sshl = q < MP ? 6u : 4u, soff = q < MP ? moff + 16u * (uint32_t)q : poff;
+        const uint32_t smul = q < MP ? MREC : 16u;
+        const uint32_t stw = 4u * (uint32_t)(q < MP ? GG::W_META : q == MP ? GG::W_X : GG::W_O);
+        const uint32_t stm = q < MP ? COOP_CHK_MASK : 0xFFFFu;
+        const uint32_t snk = q >= MP + 1 ? 0xFFFFFFFFu : 0u, snk_tl = q >= MP + 2 ? 0xFFFFFFFFu : 0u;
+        // byte offset of record idx: a shift when the message block is 64 B (r1/2), else one mad
+        auto goffs = [&](uint32_t idx) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (MREC == 64) return (idx << gshl) + goff;
+            else return idx * gmul + goff;
+        };
+        auto soffs = [&](uint32_t idx) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (MREC == 64) return (idx << sshl) + soff;
+            else return idx * smul + soff;
+        };
         auto gather = [&](int w, int g, int ib) __attribute__((always_inline)) {
             const uint32_t idx = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
-            if (lane < 40) dma16_buf(vr, (idx << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][ib]);
+            if (lane < 8 * GG::NG) dma16_buf(vr, goffs(idx), (uint32_t)(uintptr_t)&sm.in[w][ib]);
         };
         // the store of window g's slots 8w .. 8w+7: its row / check index, read
         // from window g's records one period before the store (the chain wave
@@ -909,9 +974,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             const uint32_t rw = *(const uint32_t *)((const char *)&sm.tab[g & (TQ - 1)][8 * w + kl][0] + stw) & stm;
             return live ? bfi(tl ? snk_tl : snk, (uint32_t)a.m, rw) : (uint32_t)a.m;
         };
-        const int qp = q < 5 ? q : 5;   // lane q's piece of a slot's outputs (q > 5: any, stored to the sink)
+        const int qp = q < MP + 1 ? q : MP + 1;   // lane q's piece of a slot's outputs (q > MP + 1: any, to the sink)
         auto store_win = [&](int w, int g, uint32_t idx) __attribute__((always_inline)) {
-            rbuf_store_v4(__builtin_bit_cast(i32x4, sm.mst[g & 1][w][kl][qp]), vr, (int)((idx << sshl) + soff), 0, 0);
+            rbuf_store_v4(__builtin_bit_cast(i32x4, sm.mst[g & 1][w][kl][qp]), vr, (int)soffs(idx), 0, 0);
         };
         for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
             __syncthreads();   // prologue 1: tables and resident lines in LDS
@@ -935,18 +1000,18 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 #pragma unroll
             for (int w = 0; w < WS; w++) {
                 sidx[w] = (uint32_t)a.m;
-                lop[w] = *(const uint4 *)&sm.tab[0][8 * w + kl][W_LOP];
+                lop[w] = *(const uint4 *)&sm.tab[0][8 * w + kl][GG::W_LOP];
             }
             // period p, vector memory in this order: the line loads of period
             // p, the gathers of window p+1+R, the line writebacks of period p,
-            // the stores of window p-2 (4 WS = 24 ops); vmcnt(36) = 24 + 2 WS
-            // at its end completes everything up to the gathers of period p-1
+            // the stores of window p-2 (4 WS ops: 24 at WS = 6); vmcnt(6 WS) =
+            // 4 WS + 2 WS at its end completes everything up to the gathers of period p-1
             // (the pre of window p+2 reads them next period) and so the line
             // loads of period p-1 (the slot writes of period p+1 take those of
             // period p+1-LC_PUT = p-1), and a writeback two periods after its
             // issue (its line is loaded again >= 3 periods later,
             // linecache.cpp).  The count holds only while the compiler emits
-            // exactly these 24 vector-memory instructions per period:
+            // exactly these 4 WS vector-memory instructions per period:
             // tools/check_vmcnt.py (run by __graft_entry__.build) checks the
             // ISA.  The compiler's own waits for the line loads it tracks (it
             // does not see the LDS-DMA gathers) are stricter than needed.
@@ -989,7 +1054,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
 #ifndef C3X_BANK_NODMA
-                        if (lane < 40) dma16_buf(vr, (gix[w] << gshl) + goff, (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
+                        if (lane < 8 * GG::NG) dma16_buf(vr, goffs(gix[w]), (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
 #endif
                     });
                 };
@@ -1009,16 +1074,16 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 });
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // stores of window p-2 (sink before period 2)
                     constexpr int w = decltype(wc)::value;
-                    rbuf_store_v4(__builtin_bit_cast(i32x4, std_[w]), vr, (int)((sidx[w] << sshl) + soff), 0, 0);
+                    rbuf_store_v4(__builtin_bit_cast(i32x4, std_[w]), vr, (int)soffs(sidx[w]), 0, 0);
                 });
                 // the indices of window p-1's stores and of the next period's line ops
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
                     sidx[w] = store_idx(w, p - 1, uS == a.tail, p >= 1);
-                    lop[w] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][W_LOP];
+                    lop[w] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][GG::W_LOP];
                 });
                 if (STAMP) sP[1] += stampL() - tx;
-                asm volatile("s_waitcnt vmcnt(36)" ::: "memory");   // the gathers of p-1: 12 + 24 ops after them
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * WS) : "memory");   // the gathers of p-1: 2 WS + 4 WS ops after them
                 if (STAMP) sA += stampL() - tx;
                 __syncthreads();
                 uS = (uS + 1 == a.nw) ? 0 : uS + 1;
@@ -1052,7 +1117,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
-    Slab3<WS, R, NMS> sl{sm,
+    Slab3<D0, WS, R, NMS> sl{sm,
                     a,
                     8 * sw + kl,
                     kl,
@@ -1068,7 +1133,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     (uint32_t)(4 * (q >> 1)),
                     (uint32_t)(2 * q),
                     (uint32_t)(((q >> 1) * 8 + kl) * 16 + (q & 1) * 8),
-                    (uint32_t)((32 + kl) * 16 + 4 * (q >> 1))};
+                    (uint32_t)((8 * GG::MP + kl) * 16 + 4 * (q >> 1)),
+                    (uint32_t)(((4 + (q >> 2)) * 8 + kl) * 16 + (q & 3) * 4)};
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
         if (STAMP) tseg = stamp3();
@@ -1098,10 +1164,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             sl.fm = ((conv & 1u) ? 0x0000FFFFu : 0u) | ((conv & 2u) ? 0xFFFF0000u : 0u);
             sl.psel = 0x0c0c0000u | ((conv & 2u) ? 0x0300u : 0x0700u) | ((conv & 1u) ? 0x01u : 0x05u);
         }
-        St3 st[NS];
+        St3<D0> st[NS];
         __syncthreads();   // prologue 1b: the memory wave's first gathers landed
-        PreIn in;
-        Rec rcn = sl.read_rec(1 % a.nw);   // records of the next pre's window
+        PreIn<D0> in;
+        Rec<D0> rcn = sl.read_rec(1 % a.nw);   // records of the next pre's window
         sl.read_pre(0, sl.read_rec(0), in);
         if (a.tail == 0)
             sl.template pre<true, ET>(0, in, st[0]);
@@ -1135,8 +1201,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             if (STAMP) tx = stampL();
             const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
             const bool fast = !GU && uA != a.tail && uB != a.tail;
-            PreIn in;
-            St3 &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
+            PreIn<D0> in;
+            St3<D0> &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
             if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
@@ -1254,7 +1320,7 @@ int env_int3(const char *name, int def)
 template <int WS>
 void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
 {
-    constexpr int nwaves = WS + 2, CHW = WS >= 3 ? 3 : WS;
+    constexpr int nwaves = WS + 2, CHW = Cfg<WS, 2>::CHW;
     std::vector<unsigned long long> h((size_t)grid * nwaves * 8);
     if (hipStreamSynchronize(s) != hipSuccess ||
         hipMemcpy(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
@@ -1283,25 +1349,52 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
     }
 }
 
-template <int WS, int R>
-int launch_wsr(const Coop3Args &a, int grid, bool stamped, hipStream_t s)
+// one decode launch of the D0 kernel (its slab-wave count G3<D0>::WS, R = 2):
+// fixed iterations or early termination, OMS / MS or NMS, stamped or not
+template <int D0>
+int launch_d0(const Coop3Args &a, int grid, bool et, bool nms, bool stamped, hipStream_t s)
 {
-    constexpr int threads = 64 * (WS + 2);
-    if (stamped)
-        hipLaunchKernelGGL((coop3_decode<WS, R, true>), dim3(grid), dim3(threads), 0, s, a);
+    constexpr int WS = G3<D0>::WS, R = 2, threads = 64 * (WS + 2);
+    if (et && nms)
+        hipLaunchKernelGGL((coop3_decode<D0, WS, R, false, true, true>), dim3(grid), dim3(threads), 0, s, a);
+    else if (et && stamped)
+        hipLaunchKernelGGL((coop3_decode<D0, WS, R, true, true>), dim3(grid), dim3(threads), 0, s, a);
+    else if (et)
+        hipLaunchKernelGGL((coop3_decode<D0, WS, R, false, true>), dim3(grid), dim3(threads), 0, s, a);
+    else if (nms)
+        hipLaunchKernelGGL((coop3_decode<D0, WS, R, false, false, true>), dim3(grid), dim3(threads), 0, s, a);
+    else if (stamped)
+        hipLaunchKernelGGL((coop3_decode<D0, WS, R, true>), dim3(grid), dim3(threads), 0, s, a);
     else
-        hipLaunchKernelGGL((coop3_decode<WS, R, false>), dim3(grid), dim3(threads), 0, s, a);
+        hipLaunchKernelGGL((coop3_decode<D0, WS, R, false>), dim3(grid), dim3(threads), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int launch_any(int d0, const Coop3Args &a, int grid, bool et, bool nms, bool stamped, hipStream_t s)
+{
+    return d0 == 7 ? launch_d0<7>(a, grid, et, nms, stamped, s) : d0 == 10 ? launch_d0<10>(a, grid, et, nms, stamped, s) : -1;
+}
+
+// per-degree constants at run time
+int g3_recw(int d0) { return d0 == 7 ? G3<7>::RECW : G3<10>::RECW; }
+int g3_ws(int d0) { return d0 == 7 ? G3<7>::WS : G3<10>::WS; }
+size_t g3_smem(int d0) { return d0 == 7 ? sizeof(Smem3<7, G3<7>::WS, 2>) : sizeof(Smem3<10, G3<10>::WS, 2>); }
+static_assert(sizeof(Smem3<7, G3<7>::WS, 2>) + 512 <= 160 * 1024 && sizeof(Smem3<10, G3<10>::WS, 2>) + 512 <= 160 * 1024,
+              "LDS: the workgroup's Smem3 plus the ET kernel's static words fit 160 KB");
+int g3_lcs(int d0) { return d0 == 7 ? G3<7>::LCS : G3<10>::LCS; }
+
 }  // namespace
 
+// message bytes per check and 16-codeword group (G3::MREC): 64 for first-group
+// degree <= 8, 96 up to 16
+int coop3_mrec(int d0) { return 32 * ((d0 + 7) / 8 + 1); }
+
 // OMS / MS as coop (coop_params_ok); NMS with factor <= 64 (msg_max <= 63: the
-// products fit the i16 halves) at the default WS = 6
+// products fit the i16 halves)
 bool coop3_params_ok(const ldpc_params *p, const CoopCode &cc)
 {
     if (p->algo == LDPC_ALGO_NMS)
-        return cc.S == 48 && p->var_min == -127 && p->var_max == 127 && p->msg_max >= 0 && p->msg_max <= 63 &&
+        return cc.valid && p->var_min == -127 && p->var_max == 127 && p->msg_max >= 0 && p->msg_max <= 63 &&
                p->factor >= 0 && p->factor <= 64;
     return coop_params_ok(p);
 }
@@ -1309,7 +1402,6 @@ bool coop3_params_ok(const ldpc_params *p, const CoopCode &cc)
 // V and P are addressed with 64-bit flat addresses: no batch cap
 bool coop3_stride_ok(int stride) { return stride > 0 && stride % 64 == 0; }
 
-size_t coop3_msg_bytes(const ldpc_code *h, int stride) { return (size_t)(h->m + 1) * (size_t)stride * 4; }
 
 // host side of coop3's schedule: the window plan with every window's slots
 // permuted (distance-2 forwarding sources and readers in slab wave 0) and the
@@ -1318,8 +1410,11 @@ size_t coop3_msg_bytes(const ldpc_code *h, int stride) { return (size_t)(h->m + 
 int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
 {
     o = Coop3Host{};
-    if (!h->staircase || h->n_groups != 2 || h->group_deg[0] != D0) return 1;
-    if (ws != 6 || r != 2) return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be 6 and LDPC_COOP3_R 2");
+    if (!h->staircase || h->n_groups != 2 || (h->group_deg[0] != 7 && h->group_deg[0] != 10)) return 1;
+    const int D0 = h->group_deg[0], X = D0 - 2, RECW = g3_recw(D0);
+    if (ws != g3_ws(D0) || r != 2)
+        return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be %d for first-group degree %d, LDPC_COOP3_R 2",
+                              g3_ws(D0), D0);
     const int S = 8 * ws;
     CoopPlan &pl = o.pl;
     // dist 1: neighbouring windows share no information variable; the plan's
@@ -1384,7 +1479,8 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
 // the line ops of its lane group (LcPlan::ops)
 static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vector<uint32_t> &out)
 {
-    const int S = ho.S, nw = ho.nw;
+    const int S = ho.S, nw = ho.nw, D0 = ho.d0, X = D0 - 2, RECW = ho.recw;
+    const int W_X = X, W_O = X + 1, W_META = X + 2, W_LOP = RECW - 4;   // G3
     out.assign((size_t)nw * S * RECW, 0);
     for (int u = 0; u < nw; u++)
         for (int kk = 0; kk < S; kk++) {
@@ -1395,7 +1491,7 @@ static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vec
             rec[W_X] = (src[X] - (uint32_t)k) | ((step >> 3) * (CW * 8) + (step & 7)) << 16;   // + xo index
             rec[W_O] = (src[D0 - 1] - (uint32_t)k) | (step * 2 * NP * 16) << 16;              // + cst offset
             rec[W_META] = src[D0];
-            const uint32_t lines = lp.ops[((size_t)u * LC_OPS + kk) * 2], slots = lp.ops[((size_t)u * LC_OPS + kk) * 2 + 1];
+            const uint32_t lines = lp.ops[((size_t)u * S + kk) * 2], slots = lp.ops[((size_t)u * S + kk) * 2 + 1];
             rec[W_LOP] = (lines & 0xFFFFu) * 128u;        // line loaded (byte offset in the group's V block)
             rec[W_LOP + 1] = (lines >> 16) * 128u;        // line written back
             // slot byte offsets with the line's swizzle z in bits 4..6: lane q's
@@ -1408,12 +1504,13 @@ static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vec
 
 int coop3_plan_lc(const ldpc_code *h, Coop3Host &ho, LcPlan &lp)
 {
-    const int ws = env_int3("LDPC_COOP3_WS", 6), r = env_int3("LDPC_COOP3_R", 2);
+    const int d0 = h->n_groups == 2 ? h->group_deg[0] : 0;
+    const int ws = env_int3("LDPC_COOP3_WS", d0 == 10 ? g3_ws(10) : g3_ws(7)), r = env_int3("LDPC_COOP3_R", 2);
     const int rc = coop3_plan_host(h, ws, r, ho);
     if (rc != 0) return rc;
     const int k = h->n - h->m;
     if (h->m > 0xFFFF) return 1;   // parity rows - k (and the sink row n - k = m) share a record word with 16-bit fields
-    if (lc_build_plan(ho.pl.tab, RECW, ho.nw, ho.S, D0, h->n, k, LC_SLOTS, lp) != 0) return 1;
+    if (lc_build_plan(ho.pl.tab, ho.recw, ho.nw, ho.S, ho.d0, h->n, k, g3_lcs(ho.d0), lp) != 0) return 1;
     return 0;
 }
 
@@ -1440,13 +1537,13 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
         return e;
     }
     cc->valid = 1;
-    cc->d0 = D0;
+    cc->d0 = ho.d0;
     cc->S = ho.S;
     cc->R = 2;
     cc->nw = ho.nw;
     cc->tail = ho.pl.tail;
     cc->n_fwd = ho.pl.n_fwd;
-    cc->x0 = (int)h->edge_var[h->check_start[0] + X];
+    cc->x0 = (int)h->edge_var[h->check_start[0] + ho.d0 - 2];   // check 0's x edge
     cc->m0 = h->group_cnt[0];
     cc->d1 = h->group_deg[1];
     cc->lc_slots = lp.slots;
@@ -1456,13 +1553,13 @@ int coop3_upload(const ldpc_code *h, CoopCode *cc)
 }
 
 // coop3's per-group block: the group's V rows 0 .. n+7 (row n and the line
-// n / 8: the sinks) of 16 B, then its messages ((m + 1) checks x 64 B), an odd
-// number of 128-B lines in all (groups spread over the L2 channels).  One
+// n / 8: the sinks) of 16 B, then its messages ((m + 1) checks x MREC B), an
+// odd number of 128-B lines in all (groups spread over the L2 channels).  One
 // block per group lets the memory wave address all of it with 32-bit buffer
 // offsets from one resource
-void coop3_group_layout_nm(int n, int m, size_t *vpart, size_t *block)
+void coop3_group_layout_nm(int n, int m, int mrec, size_t *vpart, size_t *block)
 {
-    const size_t vlines = ((size_t)n + 8 + 7) / 8, mlines = ((size_t)(m + 1) * MREC + 127) / 128;
+    const size_t vlines = ((size_t)n + 8 + 7) / 8, mlines = ((size_t)(m + 1) * mrec + 127) / 128;
     size_t lines = vlines + mlines;
     if (lines % 2 == 0) lines++;
     *vpart = vlines * 128;
@@ -1470,11 +1567,7 @@ void coop3_group_layout_nm(int n, int m, size_t *vpart, size_t *block)
 }
 void coop3_group_layout(const ldpc_code *h, size_t *vpart, size_t *block)
 {
-    const size_t vlines = ((size_t)h->n + 8 + 7) / 8, mlines = ((size_t)(h->m + 1) * MREC + 127) / 128;
-    size_t lines = vlines + mlines;
-    if (lines % 2 == 0) lines++;
-    *vpart = vlines * 128;
-    *block = lines * 128;
+    coop3_group_layout_nm(h->n, h->m, coop3_mrec(h->n_groups >= 1 ? h->group_deg[0] : 7), vpart, block);
 }
 size_t coop3_group_bytes(const ldpc_code *h)
 {
@@ -1485,7 +1578,7 @@ size_t coop3_group_bytes(const ldpc_code *h)
 
 // the workgroup's LDS (the ET kernel stages the hard bits of all n variables,
 // u16 each, in it between segments)
-bool coop3_et_in_kernel(const CoopCode &cc, int n) { return cc.S == 48 && (size_t)n * 2 <= sizeof(Smem3<6, 2>); }
+bool coop3_et_in_kernel(const CoopCode &cc, int n) { return cc.valid && (size_t)n * 2 <= g3_smem(cc.d0); }
 
 // ---- staged early termination (batches of more than one workgroup per CU):
 // after a first launch of K iterations the codewords still decoding are
@@ -1521,7 +1614,7 @@ __global__ void et_select_k(const int32_t *its, int n, const int *n_dev, const i
 // message halves of the codewords map[16 g2 + i] (i < 16; the padding past
 // count gets zeros)
 __global__ void et_gather_k(const char *Vs, char *Vd, const int32_t *map, const int *count, int vrows, int mrows,
-                            size_t gstride, size_t vpart)
+                            size_t gstride, size_t vpart, int mrec)
 {
     const int g2 = blockIdx.y, nlive = *count;
     if (16 * g2 >= nlive) return;
@@ -1539,23 +1632,29 @@ __global__ void et_gather_k(const char *Vs, char *Vd, const int32_t *map, const 
                     w[i >> 2] |= (uint32_t)v << (8 * (i & 3));
                 }
             *(uint4 *)(d + (size_t)r * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-        } else {   // message record of check c: pair q's (MA, MB) words, codeword 2q + h in half h of each
+        } else {   // message record of check c: pair q's (MA0, MB) words, codeword 2q + h in half h of each,
+                   // then (mrec 96) the pairs' MA1 words
             const int c = r - vrows;
-            uint32_t w[16];
+            uint32_t w[24];
 #pragma unroll
-            for (int i = 0; i < 16; i++) w[i] = 0;
+            for (int i = 0; i < 24; i++) w[i] = 0;
 #pragma unroll
             for (int i = 0; i < 16; i++)
                 if (src[i] >= 0) {
-                    const char *rec = Vs + (size_t)(src[i] >> 4) * gstride + vpart + (size_t)c * MREC;
+                    const char *rec = Vs + (size_t)(src[i] >> 4) * gstride + vpart + (size_t)c * mrec;
                     const int qs = (src[i] & 15) >> 1, hs = src[i] & 1, qd = i >> 1, hd = i & 1;
                     const uint32_t ma = ((const uint16_t *)(rec + 8 * qs))[hs], mb = ((const uint16_t *)(rec + 8 * qs + 4))[hs];
                     w[2 * qd] |= ma << (16 * hd);
                     w[2 * qd + 1] |= mb << (16 * hd);
+                    if (mrec > 64) w[16 + qd] |= (uint32_t)((const uint16_t *)(rec + 64 + 4 * qs))[hs] << (16 * hd);
                 }
-            uint4 *o = (uint4 *)(d + vpart + (size_t)c * MREC);
+            uint4 *o = (uint4 *)(d + vpart + (size_t)c * mrec);
 #pragma unroll
             for (int k = 0; k < 4; k++) o[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+            if (mrec > 64) {
+                o[4] = make_uint4(w[16], w[17], w[18], w[19]);
+                o[5] = make_uint4(w[20], w[21], w[22], w[23]);
+            }
         }
     }
 }
@@ -1636,20 +1735,12 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups
     const bool stamped = env_int3("LDPC_COOP3_STAMP", 0) != 0 && !nms;
     if (stamped) {
-        const size_t bytes = (size_t)grid * 8 * 8 * sizeof(unsigned long long);
+        const size_t bytes = (size_t)grid * (g3_ws(cc.d0) + 2) * 8 * sizeof(unsigned long long);
         if (hipMalloc(&a.stamps, bytes) != hipSuccess) return -1;
         (void)hipMemsetAsync(a.stamps, 0, bytes, s);
     }
     int rc;
-    auto launch_et = [&](const Coop3Args &x) -> int {
-        if (nms)
-            hipLaunchKernelGGL((coop3_decode<6, 2, false, true, true>), dim3(grid), dim3(64 * 8), 0, s, x);
-        else if (stamped)
-            hipLaunchKernelGGL((coop3_decode<6, 2, true, true>), dim3(grid), dim3(64 * 8), 0, s, x);
-        else
-            hipLaunchKernelGGL((coop3_decode<6, 2, false, true>), dim3(grid), dim3(64 * 8), 0, s, x);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    };
+    auto launch_et = [&](const Coop3Args &x) -> int { return launch_any(cc.d0, x, grid, true, nms, stamped, s); };
     const int k1 = et && L.V2 && L.et2 ? coop3_et_stage_iters(L.batch, L.iters) : 0;
     if (et && k1 > 0 && !stamped) {
         // stage 0: K iterations on the whole batch (codewords still decoding
@@ -1659,7 +1750,8 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
         // (V rows and iterations) after it
         const int step = std::max(1, env_int3("LDPC_COOP3_ET_STEP", 5));
         size_t vpart = 0, block = 0;
-        coop3_group_layout_nm(L.n, L.m, &vpart, &block);
+        const int mrec = coop3_mrec(cc.d0);
+        coop3_group_layout_nm(L.n, L.m, mrec, &vpart, &block);
         const size_t vbytes = (size_t)grid * L.vgroup;
         char *buf[2] = {(char *)L.V2, (char *)L.V2 + vbytes};
         const int S = L.stride;
@@ -1683,7 +1775,7 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
             hipLaunchKernelGGL(et_select_k, dim3((S + 255) / 256), dim3(256), 0, s, src_its, L.batch, src_n, src_map,
                                sel, map[b], count + st);
             hipLaunchKernelGGL(et_gather_k, dim3(64, grid), dim3(256), 0, s, src, buf[b], sel, count + st, L.n + 8,
-                               L.m + 1, L.vgroup, vpart);
+                               L.m + 1, L.vgroup, vpart, mrec);
             if (hipGetLastError() != hipSuccess) return -1;
             // the compacted codewords from iteration `done` on: no XCD remap
             // (the live groups are the first ones), the batch read on the device
@@ -1708,16 +1800,9 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
         }
         return 0;
     }
-    if (et) {
-        rc = launch_et(a);
-    } else if (nms) {
-        hipLaunchKernelGGL((coop3_decode<6, 2, false, false, true>), dim3(grid), dim3(64 * 8), 0, s, a);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    } else {
-        rc = launch_wsr<6, 2>(a, grid, stamped, s);
-    }
+    rc = launch_any(cc.d0, a, grid, et, nms, stamped, s);
     if (stamped) {
-        if (rc == 0) report_stamps3<6>(a.stamps, grid, s);
+        if (rc == 0) (cc.d0 == 7 ? report_stamps3<G3<7>::WS> : report_stamps3<G3<10>::WS>)(a.stamps, grid, s);
         (void)hipFree(a.stamps);
     }
     return rc;
@@ -1745,7 +1830,7 @@ extern "C" int ldpc_code_coop3_lc_info(const ldpc_code *h, int *slots, int *max_
     const int rc = coop3_plan_lc(h, ho, lp);
     if (rc < 0) return rc;
     *slots = rc == 0 ? lp.slots : 0;
-    if (max_slots) *max_slots = LC_SLOTS;
+    if (max_slots) *max_slots = rc == 0 ? g3_lcs(ho.d0) : 0;
     if (residencies) *residencies = rc == 0 ? lp.residencies : 0;
     if (prologue) *prologue = rc == 0 ? (int)lp.pro.size() : 0;
     if (epilogue) *epilogue = rc == 0 ? (int)lp.epi.size() : 0;

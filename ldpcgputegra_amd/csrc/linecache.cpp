@@ -23,9 +23,9 @@
 //     slot is held over [tl + LC_PUT, tw];
 //   * a line written back is loaded again >= 3 periods after its store (the
 //     kernel's per-period vmcnt waits complete a store by then);
-//   * at most LC_OPS loads and LC_OPS writebacks per period (6 slab waves x 8
-//     lane groups: one 64-lane global load and one 64-lane global store per
-//     wave and period, unused lane groups on the sink line / sink slot);
+//   * at most S loads and S writebacks per period (S / 8 slab waves x 8 lane
+//     groups: one 64-lane global load and one 64-lane global store per wave and
+//     period, unused lane groups on the sink line / sink slot);
 //   * no load in the last LC_PUT periods of an iteration, so that a segment start
 //     has no load in flight: the lines resident at a segment start are filled
 //     by its prologue (LcPlan::pro) and the dirty ones left at its end are
@@ -70,7 +70,8 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
 {
     o = LcPlan{};
     const int X = D0 - 2;
-    if (S != LC_OPS || nw < 4 * LC_GAP || n % 8 != 0 || k % 8 != 0 || k <= 0 || max_slots < 2 || n / 8 + 1 >= 65536)
+    const int LC_OPS = S;   // line loads / writebacks per period: one per lane group (slot) of the slab waves
+    if (S % 8 != 0 || S > 64 || nw < 4 * LC_GAP || n % 8 != 0 || k % 8 != 0 || k <= 0 || max_slots < 2 || n / 8 + 1 >= 65536)
         return lc_fail(__LINE__);
     const uint32_t nlines = (uint32_t)(k / 8), sink_line = (uint32_t)(n / 8);
     auto rec_at = [&](int u, int kk) { return &tab[((size_t)u * S + kk) * recw]; };
@@ -285,7 +286,11 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     const int used = assign(best_p0);
     o.slots = used + 1;
     o.residencies = (int)rs.size();
-    if (o.slots > max_slots || o.slots > (int)LC_SLOT_MASK + 1) return lc_fail(__LINE__);
+    if (o.slots > max_slots || o.slots > (int)LC_SLOT_MASK + 1) {
+        const char *dbg = getenv("LDPC_LC_DEBUG");
+        if (dbg && *dbg) fprintf(stderr, "coop3 line cache: %d slots needed, %d available\n", o.slots, max_slots);
+        return lc_fail(__LINE__);
+    }
     // residency holding line L at access period p (cyclic)
     auto res_id_at = [&](uint32_t L, int p) -> int {
         for (int id : res_of[L]) {
@@ -460,6 +465,7 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
 int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int n, int k,
                   int iters)
 {
+    const int LC_OPS = S;
     const int X = D0 - 2;
     const uint32_t sink_line = (uint32_t)(n / 8);
     const int NSL = o.slots;

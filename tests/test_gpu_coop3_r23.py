@@ -1,0 +1,113 @@
+"""coop3 at first-group degree 10 (DVB-S2 r2/3, the reference's
+code/gpu_fixed/matrix/64800x21600 table): coop3_decode<10, 4, 2> -- 4 slab
+waves (one per SIMD) over windows of <= 32 checks, 8 information edges per
+check, two 16-bit edge-code words per codeword (96-B message records) --
+against the oracle (the reference's recurrence, CDecoder_OMS_fixed_SSE.cpp:
+172-546; NMS CDecoder_NMS_fixed_SSE.cpp:188-240; early termination as the
+commented `arret` test, :551-553).  The reference ships no r2/3 decoder build
+(its x86 tree has no constantes_sse.h for 64800x21600), so the oracle --
+pinned on the 88 reference golden cases -- is the checker: soft output, hard
+decisions and iterations used, bit for bit."""
+import numpy as np
+import pytest
+
+import oracle as O
+from ldpcgputegra_amd import ALGO_NMS, Code, Decoder, channel, default_params, load_table
+
+pytestmark = pytest.mark.gpu
+CODE = "dvbs2_r2_3"
+
+
+def _run(llr, iters, params, batch=None, max_batch=None):
+    import torch
+    t = load_table(CODE)
+    B = llr.shape[0]
+    dec = Decoder(Code(CODE), max_batch=max_batch or max(B, 64), kernel=8)
+    d_hard = torch.empty((B, t.n), dtype=torch.uint8, device="cuda")
+    d_soft = torch.empty((B, t.n), dtype=torch.int8, device="cuda")
+    d_its = torch.empty(B, dtype=torch.int32, device="cuda")
+    dec.decode_i8_device(torch.from_numpy(llr).cuda(), d_hard, iters, params=params, soft=d_soft, iters_used=d_its)
+    torch.cuda.synchronize()
+    assert dec.last_kernel == "coop3"
+    out = d_hard.cpu().numpy(), d_soft.cpu().numpy(), d_its.cpu().numpy(), dec.last_et_stage
+    dec.close()
+    return out
+
+
+def _llr(B, ebn0, seed):
+    t = load_table(CODE)
+    return channel.awgn_i8_host(t.n, B, seed=seed, table=channel.i8_table(channel.sigma_from_ebn0(ebn0, t.k_info / t.n)))
+
+
+@pytest.mark.parametrize("batch,iters", [(1, 3), (37, 10), (200, 25)])
+def test_r23_fixed_iterations_vs_oracle(batch, iters):
+    """Fixed iterations, OMS offset 1: ragged batch (37), one codeword, and a
+    batch that turns the XCD workgroup remap on (200: grid 16)."""
+    t = load_table(CODE)
+    llr = _llr(batch, 1.9, 11 + batch)
+    eh, es, _ = O.decode_i8(t, llr, iters, return_soft=True, threads=O.host_threads())
+    h, s, its, _ = _run(llr, iters, default_params())
+    assert np.array_equal(s, es)
+    assert np.array_equal(h, eh)
+    assert (its == iters).all()
+
+
+@pytest.mark.parametrize("nms", [False, True])
+def test_r23_early_termination_vs_oracle(nms):
+    """In-kernel early termination (one launch): soft, hard and iterations
+    used equal the oracle's per-codeword stop; OMS and NMS factor 24."""
+    t = load_table(CODE)
+    B, iters = 200, 30
+    llr = _llr(B, 1.9, 5)
+    algo, param = (O.NMS, 24) if nms else (O.OMS, 1)
+    eh, es, eit = O.decode_i8(t, llr, iters, algo, param, early_term=True, return_soft=True, threads=O.host_threads())
+    assert eit.min() < iters and eit.max() > eit.min()
+    p = default_params(early_term=1, algo=ALGO_NMS, factor=24) if nms else default_params(early_term=1)
+    h, s, its, st = _run(llr, iters, p)
+    assert st == 0
+    assert np.array_equal(its, eit)
+    assert np.array_equal(s, es)
+    assert np.array_equal(h, eh)
+
+
+def test_r23_nms_fixed_vs_oracle():
+    t = load_table(CODE)
+    llr = _llr(64, 2.0, 8)
+    eh, es, _ = O.decode_i8(t, llr, 12, O.NMS, 29, return_soft=True, threads=O.host_threads())
+    h, s, _, _ = _run(llr, 12, default_params(algo=ALGO_NMS, factor=29))
+    assert np.array_equal(s, es) and np.array_equal(h, eh)
+
+
+def test_r23_staged_early_termination_vs_oracle(monkeypatch):
+    """Staged early termination (compaction of the codewords still decoding
+    into 16-codeword groups, messages in the 96-B record layout), forced at a
+    small batch: equal to the oracle."""
+    t = load_table(CODE)
+    B, iters = 200, 30
+    llr = _llr(B, 1.8, 17)
+    eh, es, eit = O.decode_i8(t, llr, iters, early_term=True, return_soft=True, threads=O.host_threads())
+    k1 = int(np.percentile(eit, 30))
+    assert 0 < k1 < iters and (eit > k1).any()
+    monkeypatch.setenv("LDPC_COOP3_ET_STAGE_MIN", "0")
+    monkeypatch.setenv("LDPC_COOP3_ET_K", str(k1))
+    monkeypatch.setenv("LDPC_COOP3_ET_STEP", "3")
+    h, s, its, st = _run(llr, iters, default_params(early_term=1), max_batch=256)
+    assert st == k1
+    assert np.array_equal(its, eit)
+    assert np.array_equal(s, es)
+    assert np.array_equal(h, eh)
+
+
+def test_r23_full_batch_fixed_50_sampled_vs_oracle():
+    """configs[2]'s shape on r2/3: batch 4096, 50 iterations, 2.2 dB (bench.py
+    --mixed-codes reference's Eb/N0 for r2/3): a seeded sample of 256
+    codewords (spread over every XCD's workgroups) equals the oracle's
+    decode, hard decisions and soft output."""
+    t = load_table(CODE)
+    B, iters = 4096, 50
+    llr = _llr(B, 2.2, 2024)
+    h, s, _, _ = _run(llr, iters, default_params(), max_batch=B)
+    sel = np.sort(np.random.default_rng(1).choice(B, 256, replace=False))
+    eh, es, _ = O.decode_i8(t, llr[sel], iters, return_soft=True, threads=O.host_threads())
+    assert np.array_equal(s[sel], es)
+    assert np.array_equal(h[sel], eh)

@@ -33,7 +33,7 @@ def kernels_for(code):
     """Kernel families that can run this code: 1 generic, 2 windowed,
     3 windowed2 (S=16), 5 coop (workgroup-cooperative), 7 lds (LDS-resident
     short codes), 8 coop3 (slab waves doing pre + post, i16 chain; first-group
-    degree 7).  (4 = windowed2 S=32 and 6 = coop2 were superseded and removed.)"""
+    degree 7 or 10).  (4 = windowed2 S=32 and 6 = coop2 were superseded and removed.)"""
     ks = [1]
     c = Code(code)
     if c.plan_info()["windowed"]:
@@ -42,7 +42,7 @@ def kernels_for(code):
         ks.append(3)
     if c.coop_plan() is not None and c.max_deg in (7, 10, 14, 22):
         ks.append(5)
-    if c.coop_plan(32, 2, 2) is not None and c.max_deg == 7:
+    if c.coop3_line_cache() is not None:
         ks.append(8)
     if c.layer_info()["lds_i8"]:
         ks.append(7)

@@ -19,7 +19,18 @@ def test_dvbs2_r1_2_plan_fits_and_replays():
     assert 0 < lc["epilogue"] <= lc["prologue"] < lc["slots"]
 
 
-@pytest.mark.parametrize("name", ["576x288", "dvbs2_r2_3"])
+def test_dvbs2_r2_3_plan_fits_and_replays():
+    """First-group degree 10 (r2/3: 8 information edges per check, windows of
+    30 checks at S = 32): the plan fits the degree-10 kernel's larger line
+    cache and replays; the swizzle spreads its bank groups too."""
+    lc = Code("dvbs2_r2_3").coop3_line_cache()
+    assert lc is not None and 2 <= lc["slots"] <= lc["max_slots"] == 848
+    assert 0 < lc["epilogue"] <= lc["prologue"] < lc["slots"]
+    b = Code("dvbs2_r2_3").coop3_lc_banks()
+    assert b["swizzled"] < 0.02 * b["plain"]
+
+
+@pytest.mark.parametrize("name", ["576x288", "dvbs2shape_r3_4", "dvbs2_r8_9"])
 def test_codes_without_coop3_have_no_plan(name):
     if name not in available():
         pytest.skip("code table absent")

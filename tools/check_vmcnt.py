@@ -2,10 +2,11 @@
 """Build-time guard for coop3's hand-counted `s_waitcnt vmcnt(36)`.
 
 coop3's memory wave (csrc/coop3.hip, `mperiod`) issues, per period, for each of
-the WS = 6 slab-wave sets, in this order: one line load, one LDS-DMA gather
-(`buffer_load_dwordx4 ... lds`, inline asm the compiler does not count), one
-line writeback and one store -- 4 * WS = 24 vector-memory instructions -- and
-closes the period with vmcnt(24 + 2 * WS = 36) right before its barrier:
+the WS slab-wave sets (6 for DVB-S2 r1/2's kernel, 4 for r2/3's), in this
+order: one line load, one LDS-DMA gather (`buffer_load_dwordx4 ... lds`,
+inline asm the compiler does not count), one line writeback and one store --
+4 * WS vector-memory instructions -- and closes the period with vmcnt(4 * WS +
+2 * WS) right before its barrier:
 everything up to the previous period's gathers (and so its line loads) has
 landed.  That count is only right while the compiler emits exactly those 24
 instructions per period (no split, no extra load, no scratch spill).  This
@@ -18,7 +19,7 @@ periods) must hold exactly --ops vector-memory instructions, at least
 scratch.  (The compiler's own waits for the line loads it tracks are stricter
 than needed and not period boundaries.)
 
-usage: check_vmcnt.py [--ops 24] [--vmcnt 36] <coop3.o | libldpc_mi355x.so | file.s>
+usage: check_vmcnt.py [--ops N] [--vmcnt N] <coop3.o | libldpc_mi355x.so | file.s>
 exit 0 = ok, 1 = mismatch (the message names the kernel and region).
 """
 import argparse
@@ -90,20 +91,25 @@ def closes_period(lines, i, reach=8):
     return False
 
 
-ET_NAME = re.compile(r"coop3_decodeILi\d+ELi\d+ELb[01]ELb1E")
+# coop3_decode<D0, WS, R, STAMP, ET, NMS>: the slab-wave count WS sets the
+# period's op count (4 WS) and closing wait (6 WS)
+WS_NAME = re.compile(r"coop3_decodeILi(\d+)ELi(\d+)ELi\d+E")
 
 
-def check(isa, ops, vmcnt, min_regions=1, pattern="coop3_decode", et_ops=24, et_vmcnt=36):
+def check(isa, ops=None, vmcnt=None, min_regions=1, pattern="coop3_decode"):
     """List of error strings (empty = ok) and the number of regions checked.
-    Early-termination kernels (template flag ET) are checked against
-    et_ops / et_vmcnt (the same counts today)."""
+    ops / vmcnt: force the counts (default: 4 WS / 6 WS from each kernel's
+    template arguments)."""
     errs, checked = [], 0
     kernels = {k: v for k, v in functions(isa).items() if pattern in k}
     if not kernels:
         return ["no %s kernel in the disassembly" % pattern], 0
     base_ops, base_vmcnt = ops, vmcnt
     for name, lines in kernels.items():
-        ops, vmcnt = (et_ops, et_vmcnt) if ET_NAME.search(name) else (base_ops, base_vmcnt)
+        m = WS_NAME.search(name)
+        ws = int(m.group(2)) if m else 6
+        ops = base_ops if base_ops is not None else 4 * ws
+        vmcnt = base_vmcnt if base_vmcnt is not None else 6 * ws
         wait = re.compile(r"^\s*s_waitcnt\s+.*vmcnt\(%d\)" % vmcnt)
         if any(re.match(r"^\s*scratch_", l) for l in lines):
             errs.append("%s: scratch access (a spill adds vector-memory ops the vmcnt does not count)" % name)
@@ -140,19 +146,17 @@ def check(isa, ops, vmcnt, min_regions=1, pattern="coop3_decode", et_ops=24, et_
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
-    ap.add_argument("--ops", type=int, default=24, help="vector-memory ops per memory-wave period (4 * WS)")
-    ap.add_argument("--vmcnt", type=int, default=36, help="the period's closing wait (4 * WS + 2 * WS)")
-    ap.add_argument("--et-ops", type=int, default=24, help="ET kernels' vector-memory ops per period")
-    ap.add_argument("--et-vmcnt", type=int, default=36, help="ET kernels' period-closing wait")
+    ap.add_argument("--ops", type=int, default=None, help="force the vector-memory ops per period (default 4 WS)")
+    ap.add_argument("--vmcnt", type=int, default=None, help="force the period's closing wait (default 6 WS)")
     ap.add_argument("--min-regions", type=int, default=1)
     a = ap.parse_args()
-    errs, n = check(disassemble(a.path), a.ops, a.vmcnt, a.min_regions, et_ops=a.et_ops, et_vmcnt=a.et_vmcnt)
+    errs, n = check(disassemble(a.path), a.ops, a.vmcnt, a.min_regions)
     if errs:
         for e in errs:
             print("check_vmcnt: " + e, file=sys.stderr)
         return 1
-    print("check_vmcnt: ok (%d memory-wave periods of %d / %d vector-memory ops, vmcnt(%d) / vmcnt(%d) with ET)"
-          % (n, a.ops, a.et_ops, a.vmcnt, a.et_vmcnt))
+    print("check_vmcnt: ok (%d memory-wave periods checked: 4 WS vector-memory ops in order, vmcnt(6 WS); "
+          "WS = 6 for degree 7, 4 for degree 10)" % n)
     return 0
 
 
