@@ -119,13 +119,15 @@ struct G3 {
     static constexpr int MP = MREC / 16;                       // message pieces (16 B) per check
     static constexpr int NG = MP + 1;                          // pieces gathered per slot (+ the o-edge parity row)
     static constexpr int W_X = X, W_O = X + 1, W_META = X + 2;
-    static constexpr int W_LOP = (W_META + 1 + 3) / 4 * 4;     // line-op words (one uint4)
-    static constexpr int RECW = W_LOP + 4;                     // slot record words
+    static constexpr int NLD = (X + 7) / 8;                    // line loads / writebacks per lane group and
+                                                               // period (a window touches ~S X / 8 new lines)
+    static constexpr int W_LOP = (W_META + 1 + 3) / 4 * 4;     // line-op words (NLD uint4)
+    static constexpr int RECW = W_LOP + 4 * NLD;               // slot record words
     static constexpr int NR = (W_META + 1 + 3) / 4;            // uint4 a pre reads of its record
     static constexpr int WS = D0 == 7 ? 6 : 4;                 // slab waves: S = 8 WS checks per window (r1/2's
                                                                // windows fill 45 of 48, r2/3's 30 of 32)
-    static constexpr int LCS = D0 == 7 ? 752 : 848;            // line-cache slots (128 B each; slot 0 the sink):
-                                                               // what the 160 KB of LDS leave beside the rest
+    static constexpr int LCS = D0 == 7 ? 752 : D0 == 10 ? 848 : 784;   // line-cache slots (128 B each; slot 0
+                                                               // the sink): what the 160 KB of LDS leave beside the rest
     static_assert(NMA <= 2 && 8 * NG <= 64 && MP + 2 <= 8, "message pieces: one gather and one store per slot set");
 };
 #ifndef LDPC_C3_MSLEEP
@@ -203,17 +205,20 @@ struct Coop3Args {
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset) + 255 (R - coff: C form), offset per half (value form)
 };
 
-template <int D0>
+// LEAN (early termination at degree 14: VGPRs): |c| is not kept from pre to
+// post but recomputed there (abs_sat / abs_r of c, 2 VALU per edge)
+template <int D0, bool LEAN = false>
 struct St3 {                          // one window's state from pre to post (R / C pairs)
     static constexpr int X = D0 - 2;
     uint32_t c[D0 - 1];               // contributions (info, o); tail: new V
-    uint32_t a[D0 - 1];               // |c| (not clipped: min1 / min2 are, where the constants are made)
+    uint32_t a[LEAN ? 1 : D0 - 1];    // |c| (not clipped: min1 / min2 are, where the constants are made)
     uint32_t mn1, mn2, sacc, mx;      // min1 / min2 / sign parity over info + o; x-edge old message
                                       // tail: mn1 = MA0, mn2 = MB, ma1 = MA1
     uint32_t ma1;
     uint32_t xs;                      // the slot's chain step: u16 index of its x input in xo[buf]
     uint32_t ad[X];                   // the info edges' pair addresses in the line cache (pre reads, post writes)
-    uint32_t v[X];                    // FZ (early termination): the info edges' V as read (R pairs)
+    uint32_t v[X > 8 ? 1 : X];        // FZ (early termination): the info edges' V as read (R pairs; X > 8:
+                                      // re-read from LDS by the post, Slab3::FZ_REREAD)
 };
 
 // record meta (word W_META = D0): check | COOP_M_ACT | chain step <<
@@ -265,11 +270,11 @@ LDPC_DEV uint32_t old_msg2(uint32_t MA0, uint32_t MA1, const MsgTab &t, const Pk
         return old_msg<J - 8>(MA1, t, K.m3, K.c4);
 }
 
-template <int D0, int WS, int R, bool NMS = false>
+template <int D0, int WS, int R, bool NMS = false, bool LEAN = false>
 struct Slab3 {
     using SM = Smem3<D0, WS, R>;
     using G = G3<D0>;
-    using St = St3<D0>;
+    using St = St3<D0, LEAN>;
     using RecT = Rec<D0>;
     using In = PreIn<D0>;
     static constexpr int S = SM::S, X = G::X;
@@ -288,6 +293,11 @@ struct Slab3 {
     uint32_t fm = 0;                  // FZ: halves of this pair's converged codewords (early termination):
                                       // their V is rewritten unchanged and the chain passes V[p_i] unchanged
     uint32_t psel = 0x0c0c0705u;      // FZ: perm(new, old, psel) = pack_v of new, or of old where converged
+    uint32_t psel_raw = 0x0c0c0705u;  // FZ with X > 8: the same from the old pair's raw u16 (re-read from LDS)
+    // FZ: X > 8 keeps no copy of the info edges' old V from pre to post (VGPRs);
+    // the post re-reads it from the line cache, where it is unchanged until
+    // this post writes it (no other window between this pre and post touches it)
+    static constexpr bool FZ_REREAD = X > 8;
 
     LDPC_DEV const char *lcb() const { return (const char *)&sm.lc[0][0]; }
     LDPC_DEV char *lcw() const { return (char *)&sm.lc[0][0]; }
@@ -361,7 +371,7 @@ struct Slab3 {
                 const uint32_t c = pk_sub_sat(v[J], old_msg2<J>(MA, MA1, t, K));
                 const uint32_t aj = abs_sat(c, c510);
                 s.c[J] = c;
-                s.a[J] = aj;
+                if constexpr (!LEAN) s.a[J] = aj;
                 sacc ^= c;
                 if constexpr (J == 0) {   // a <= R(127): the first edge is min1
                     min1 = aj;
@@ -378,7 +388,7 @@ struct Slab3 {
             const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg2<D0 - 1>(MA, MA1, t, K)), neg127);
             const uint32_t ao = abs_r(cor, c510);
             s.c[X] = cor;
-            s.a[X] = ao;
+            if constexpr (!LEAN) s.a[X] = ao;
             s.sacc = sacc ^ cor;
             s.mn2 = pk_max(min1, pk_min(ao, min2));
             s.mn1 = pk_min(min1, ao);
@@ -404,8 +414,10 @@ struct Slab3 {
             L = pk_max(pk_sub(COV, TV), VNEG127);
             H = pk_min(pk_add(COV, TV), V127);
             if constexpr (FZ) {   // converged codewords: L = H = V[p_i] as read, the step returns it
+                if constexpr (!FZ_REREAD) {
 #pragma unroll
-                for (int j = 0; j < X; j++) s.v[j] = v[j];
+                    for (int j = 0; j < X; j++) s.v[j] = v[j];
+                }
                 const uint32_t VO = pk_ashr8(v[X]);
                 L = bfi(fm, VO, L);
                 H = bfi(fm, VO, H);
@@ -413,13 +425,15 @@ struct Slab3 {
         } else {
             // the tail check (later degree group: a = |min(c, msg_max)|,
             // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
+            uint32_t avl[LEAN ? X + 1 : 1];   // LEAN: the tail's |c| (used in this pre only), else in s.a
+            auto av = [&](int j) __attribute__((always_inline)) -> uint32_t & { return LEAN ? avl[LEAN ? j : 0] : s.a[LEAN ? 0 : j]; };
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
                 const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg2<J>(MA, MA1, t, K)), neg127);
                 // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2
                 const uint32_t aj = NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510);
                 s.c[J] = c;
-                s.a[J] = aj;
+                av(J) = aj;
                 sacc ^= c;
                 min2 = pk_max(min1, pk_min(aj, min2));
                 min1 = pk_min(min1, aj);
@@ -433,9 +447,9 @@ struct Slab3 {
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
                 if constexpr (J < 8)
-                    s.c[J] = new_v_later<J>(s.c[J], s.a[J], min1, e1, e2, MAn, neg127);
+                    s.c[J] = new_v_later<J>(s.c[J], av(J), min1, e1, e2, MAn, neg127);
                 else
-                    s.c[J] = new_v_later<J - 8>(s.c[J], s.a[J], min1, e1, e2, MAn1, neg127);
+                    s.c[J] = new_v_later<J - 8>(s.c[J], av(J), min1, e1, e2, MAn1, neg127);
                 if constexpr (FZ) s.c[J] = bfi(fm, v[J], s.c[J]);   // converged codewords keep their V
             });
             s.mx = 0;
@@ -514,18 +528,23 @@ struct Slab3 {
             MA = 0;
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t n = nv(jc, s.c[J], s.a[J], min1, e1, e2, MA, MA1);
-                put(J, FZ ? perm(n, s.v[J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
+                const uint32_t aJ = LEAN ? abs_sat(s.c[J], K.c510) : s.a[LEAN ? 0 : J];
+                const uint32_t n = nv(jc, s.c[J], aJ, min1, e1, e2, MA, MA1);
+                if constexpr (FZ && FZ_REREAD)
+                    put(J, perm(n, *(const unsigned short *)(lcb() + s.ad[J]), psel_raw));
+                else
+                    put(J, FZ ? perm(n, s.v[FZ_REREAD ? 0 : J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
             const uint32_t nx = nv(std::integral_constant<int, X>{}, cx, ax, min1, e1, e2, MA, MA1);
             *sx = (unsigned short)(FZ ? perm(nx, xr, psel) : pack_v(nx));
             // the o edge: its code only (the next check rewrites V[o] as its x edge)
+            const uint32_t aO = LEAN ? abs_r(s.c[X], K.c510) : s.a[LEAN ? 0 : X];
             if constexpr (D0 - 1 < 8)
-                msg_code<D0 - 1>(s.c[X], s.a[X], min1, MA);
+                msg_code<D0 - 1>(s.c[X], aO, min1, MA);
             else
-                msg_code<D0 - 9>(s.c[X], s.a[X], min1, MA1);
+                msg_code<D0 - 9>(s.c[X], aO, min1, MA1);
             MB = perm(e2, e1, 0x07030501u);
         } else {
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
@@ -807,17 +826,18 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             }
             __syncthreads();
             bool done = false;
-            for (int c0 = 0; c0 < a.m0 && !done; c0 += NT * 8) {
-                uint32_t ev[8][D0];
+            constexpr int CR = D0 * 8 <= 80 ? 8 : 4;   // checks per thread and round (their edge ids in VGPRs)
+            for (int c0 = 0; c0 < a.m0 && !done; c0 += NT * CR) {
+                uint32_t ev[CR][D0];
 #pragma unroll
-                for (int r = 0; r < 8; r++) {
+                for (int r = 0; r < CR; r++) {
                     const int cc = min(c0 + r * NT + (int)threadIdx.x, a.m0 - 1);
 #pragma unroll
                     for (int j = 0; j < D0; j++) ev[r][j] = a.ev[(size_t)cc * D0 + j];
                 }
                 uint32_t f = 0;
 #pragma unroll
-                for (int r = 0; r < 8; r++) {
+                for (int r = 0; r < CR; r++) {
                     const int c = c0 + r * NT + (int)threadIdx.x;
                     uint32_t x = 0;
 #pragma unroll
@@ -989,18 +1009,22 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             __syncthreads();   // prologue 2
             if (STAMP && it == 0) t0 = stamp3();
             constexpr int NPD = LC_PUT + 1;
-            uint4 pend[NPD][WS];   // line loads of periods p-LC_PUT .. p (written to their slots LC_PUT periods on)
+            constexpr int NLD = GG::NLD;
+            uint4 pend[NPD][WS][NLD];   // line loads of periods p-LC_PUT .. p (written to their slots LC_PUT periods on)
 #pragma unroll
             for (int i = 0; i < NPD; i++)
 #pragma unroll
-                for (int w = 0; w < WS; w++) pend[i][w] = make_uint4(0, 0, 0, 0);
+                for (int w = 0; w < WS; w++)
+#pragma unroll
+                    for (int l = 0; l < NLD; l++) pend[i][w][l] = make_uint4(0, 0, 0, 0);
             int uS = a.nw - 1;   // local index of window p-1 (the next period's stores)
             uint32_t sidx[WS];   // the stores' indices (window p-2), read in period p-1
-            uint4 lop[WS];       // the line ops of period p (byte offsets, record words 8 .. 11), read in period p-1
+            uint4 lop[WS][NLD];  // the line ops of period p (byte offsets, record words W_LOP ..), read in period p-1
 #pragma unroll
             for (int w = 0; w < WS; w++) {
                 sidx[w] = (uint32_t)a.m;
-                lop[w] = *(const uint4 *)&sm.tab[0][8 * w + kl][GG::W_LOP];
+#pragma unroll
+                for (int l = 0; l < NLD; l++) lop[w][l] = *(const uint4 *)&sm.tab[0][8 * w + kl][GG::W_LOP + 4 * l];
             }
             // period p, vector memory in this order: the line loads of period
             // p, the gathers of window p+1+R, the line writebacks of period p,
@@ -1019,11 +1043,14 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 constexpr int s = decltype(sc_)::value;   // p % NPD
                 if (STAMP) tx = stampL();
                 uint32_t gix[WS];
-                uint4 wbd[WS], std_[WS];
+                uint4 wbd[WS][NLD], std_[WS];
                 auto loads = [&]() __attribute__((always_inline)) {   // line loads of period p
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
-                        pend[s][w] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w].x + lq), 0, 0));
+                        static_for<0, NLD>([&](auto lc) __attribute__((always_inline)) {
+                            constexpr int l = decltype(lc)::value;
+                            pend[s][w][l] = __builtin_bit_cast(uint4, rbuf_load_v4(vr, (int)(lop[w][l].x + lq), 0, 0));
+                        });
                     });
                 };
                 auto read_gix = [&]() __attribute__((always_inline)) {   // gather indices of window p+1+R
@@ -1036,10 +1063,12 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
 #ifdef C3X_BANK_MEM
-                        wbd[w] = *(const uint4 *)(lcb + 16 * lane);
+                        wbd[w][0] = *(const uint4 *)(lcb + 16 * lane);
                         std_[w] = *(const uint4 *)((const char *)&sm.mst[(p - 2) & 1][w][0][0] + 16 * (lane & 31));
 #else
-                        wbd[w] = *(const uint4 *)(lcb + (lop[w].w ^ lq));   // row q of the swizzled slot
+#pragma unroll
+                        for (int l = 0; l < NLD; l++)
+                            wbd[w][l] = *(const uint4 *)(lcb + (lop[w][l].w ^ lq));   // row q of the swizzled slot
                         std_[w] = sm.mst[(p - 2) & 1][w][kl][qp];
 #endif
                     });
@@ -1047,7 +1076,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 auto slot_writes = [&]() __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
-                        *(uint4 *)(lcb + (lop[w].z ^ lq)) = pend[(s + 1) % NPD][w];
+#pragma unroll
+                        for (int l = 0; l < NLD; l++) *(uint4 *)(lcb + (lop[w][l].z ^ lq)) = pend[(s + 1) % NPD][w][l];
                     });
                 };
                 auto gathers = [&]() __attribute__((always_inline)) {
@@ -1070,7 +1100,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 slot_writes();
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // writebacks of period p
                     constexpr int w = decltype(wc)::value;
-                    rbuf_store_v4(__builtin_bit_cast(i32x4, wbd[w]), vr, (int)(lop[w].y + lq), 0, 0);
+                    static_for<0, NLD>([&](auto lc) __attribute__((always_inline)) {
+                        constexpr int l = decltype(lc)::value;
+                        rbuf_store_v4(__builtin_bit_cast(i32x4, wbd[w][l]), vr, (int)(lop[w][l].y + lq), 0, 0);
+                    });
                 });
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // stores of window p-2 (sink before period 2)
                     constexpr int w = decltype(wc)::value;
@@ -1080,10 +1113,13 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
                     sidx[w] = store_idx(w, p - 1, uS == a.tail, p >= 1);
-                    lop[w] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][GG::W_LOP];
+#pragma unroll
+                    for (int l = 0; l < NLD; l++)
+                        lop[w][l] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][GG::W_LOP + 4 * l];
                 });
                 if (STAMP) sP[1] += stampL() - tx;
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * WS) : "memory");   // the gathers of p-1: 2 WS + 4 WS ops after them
+                // the gathers of p-1: (NLD + 1) WS ops of p-1 and (2 NLD + 2) WS of p after them
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((3 * NLD + 3) * WS) : "memory");
                 if (STAMP) sA += stampL() - tx;
                 __syncthreads();
                 uS = (uS + 1 == a.nw) ? 0 : uS + 1;
@@ -1117,7 +1153,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
-    Slab3<D0, WS, R, NMS> sl{sm,
+    constexpr bool LEAN = ET && GG::X > 8;
+    Slab3<D0, WS, R, NMS, LEAN> sl{sm,
                     a,
                     8 * sw + kl,
                     kl,
@@ -1163,8 +1200,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             const uint32_t conv = (((1u << valid) - 1u) & ~et_sh[0]) >> (2 * q);
             sl.fm = ((conv & 1u) ? 0x0000FFFFu : 0u) | ((conv & 2u) ? 0xFFFF0000u : 0u);
             sl.psel = 0x0c0c0000u | ((conv & 2u) ? 0x0300u : 0x0700u) | ((conv & 1u) ? 0x01u : 0x05u);
+            sl.psel_raw = 0x0c0c0000u | ((conv & 2u) ? 0x0100u : 0x0700u) | ((conv & 1u) ? 0x00u : 0x05u);
         }
-        St3<D0> st[NS];
+        St3<D0, LEAN> st[NS];
         __syncthreads();   // prologue 1b: the memory wave's first gathers landed
         PreIn<D0> in;
         Rec<D0> rcn = sl.read_rec(1 % a.nw);   // records of the next pre's window
@@ -1202,7 +1240,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
             const bool fast = !GU && uA != a.tail && uB != a.tail;
             PreIn<D0> in;
-            St3<D0> &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
+            St3<D0, LEAN> &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
             if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
@@ -1372,16 +1410,31 @@ int launch_d0(const Coop3Args &a, int grid, bool et, bool nms, bool stamped, hip
 
 int launch_any(int d0, const Coop3Args &a, int grid, bool et, bool nms, bool stamped, hipStream_t s)
 {
-    return d0 == 7 ? launch_d0<7>(a, grid, et, nms, stamped, s) : d0 == 10 ? launch_d0<10>(a, grid, et, nms, stamped, s) : -1;
+    switch (d0) {
+    case 7: return launch_d0<7>(a, grid, et, nms, stamped, s);
+    case 10: return launch_d0<10>(a, grid, et, nms, stamped, s);
+    case 14: return launch_d0<14>(a, grid, et, nms, stamped, s);
+    default: return -1;
+    }
 }
 
-// per-degree constants at run time
-int g3_recw(int d0) { return d0 == 7 ? G3<7>::RECW : G3<10>::RECW; }
-int g3_ws(int d0) { return d0 == 7 ? G3<7>::WS : G3<10>::WS; }
-size_t g3_smem(int d0) { return d0 == 7 ? sizeof(Smem3<7, G3<7>::WS, 2>) : sizeof(Smem3<10, G3<10>::WS, 2>); }
-static_assert(sizeof(Smem3<7, G3<7>::WS, 2>) + 512 <= 160 * 1024 && sizeof(Smem3<10, G3<10>::WS, 2>) + 512 <= 160 * 1024,
+// per-degree constants at run time (first-group degrees 7, 10, 14)
+template <template <int> class F>
+auto g3_at(int d0) -> decltype(F<7>::v)
+{
+    return d0 == 7 ? F<7>::v : d0 == 10 ? F<10>::v : F<14>::v;
+}
+template <int D> struct RecwOf { static constexpr int v = G3<D>::RECW; };
+template <int D> struct WsOf { static constexpr int v = G3<D>::WS; };
+template <int D> struct LcsOf { static constexpr int v = G3<D>::LCS; };
+template <int D> struct SmemOf { static constexpr size_t v = sizeof(Smem3<D, G3<D>::WS, 2>); };
+int g3_recw(int d0) { return g3_at<RecwOf>(d0); }
+int g3_ws(int d0) { return g3_at<WsOf>(d0); }
+size_t g3_smem(int d0) { return g3_at<SmemOf>(d0); }
+bool g3_degree_ok(int d0) { return d0 == 7 || d0 == 10 || d0 == 14; }
+static_assert(SmemOf<7>::v + 512 <= 160 * 1024 && SmemOf<10>::v + 512 <= 160 * 1024 && SmemOf<14>::v + 512 <= 160 * 1024,
               "LDS: the workgroup's Smem3 plus the ET kernel's static words fit 160 KB");
-int g3_lcs(int d0) { return d0 == 7 ? G3<7>::LCS : G3<10>::LCS; }
+int g3_lcs(int d0) { return g3_at<LcsOf>(d0); }
 
 }  // namespace
 
@@ -1410,7 +1463,7 @@ bool coop3_stride_ok(int stride) { return stride > 0 && stride % 64 == 0; }
 int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
 {
     o = Coop3Host{};
-    if (!h->staircase || h->n_groups != 2 || (h->group_deg[0] != 7 && h->group_deg[0] != 10)) return 1;
+    if (!h->staircase || h->n_groups != 2 || !g3_degree_ok(h->group_deg[0])) return 1;
     const int D0 = h->group_deg[0], X = D0 - 2, RECW = g3_recw(D0);
     if (ws != g3_ws(D0) || r != 2)
         return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be %d for first-group degree %d, LDPC_COOP3_R 2",
@@ -1480,7 +1533,7 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
 static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vector<uint32_t> &out)
 {
     const int S = ho.S, nw = ho.nw, D0 = ho.d0, X = D0 - 2, RECW = ho.recw;
-    const int W_X = X, W_O = X + 1, W_META = X + 2, W_LOP = RECW - 4;   // G3
+    const int W_X = X, W_O = X + 1, W_META = X + 2, NLD = (X + 7) / 8, W_LOP = RECW - 4 * NLD;   // G3
     out.assign((size_t)nw * S * RECW, 0);
     for (int u = 0; u < nw; u++)
         for (int kk = 0; kk < S; kk++) {
@@ -1491,21 +1544,26 @@ static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vec
             rec[W_X] = (src[X] - (uint32_t)k) | ((step >> 3) * (CW * 8) + (step & 7)) << 16;   // + xo index
             rec[W_O] = (src[D0 - 1] - (uint32_t)k) | (step * 2 * NP * 16) << 16;              // + cst offset
             rec[W_META] = src[D0];
-            const uint32_t lines = lp.ops[((size_t)u * S + kk) * 2], slots = lp.ops[((size_t)u * S + kk) * 2 + 1];
-            rec[W_LOP] = (lines & 0xFFFFu) * 128u;        // line loaded (byte offset in the group's V block)
-            rec[W_LOP + 1] = (lines >> 16) * 128u;        // line written back
-            // slot byte offsets with the line's swizzle z in bits 4..6: lane q's
-            // piece is at (offset ^ 16 q) (LcPlan, coop.h)
-            auto slot_off = [](uint32_t f) { return (f & LC_SLOT_MASK) * 128u + (f >> LC_SLOT_BITS) * 16u; };
-            rec[W_LOP + 2] = slot_off(slots & 0xFFFFu);   // slot written with the load of LC_PUT periods earlier
-            rec[W_LOP + 3] = slot_off(slots >> 16);       // slot written back
+            // lane group kk's line ops (LcPlan::ops, S NLD per period: op sub * S + kk)
+            for (int sub = 0; sub < NLD; sub++) {
+                const size_t o = (size_t)u * S * NLD + (size_t)sub * S + kk;
+                const uint32_t lines = lp.ops[o * 2], slots = lp.ops[o * 2 + 1];
+                uint32_t *lw = rec + W_LOP + 4 * sub;
+                lw[0] = (lines & 0xFFFFu) * 128u;        // line loaded (byte offset in the group's V block)
+                lw[1] = (lines >> 16) * 128u;            // line written back
+                // slot byte offsets with the line's swizzle z in bits 4..6: lane q's
+                // piece is at (offset ^ 16 q) (LcPlan, coop.h)
+                auto slot_off = [](uint32_t f) { return (f & LC_SLOT_MASK) * 128u + (f >> LC_SLOT_BITS) * 16u; };
+                lw[2] = slot_off(slots & 0xFFFFu);       // slot written with the load of LC_PUT periods earlier
+                lw[3] = slot_off(slots >> 16);           // slot written back
+            }
         }
 }
 
 int coop3_plan_lc(const ldpc_code *h, Coop3Host &ho, LcPlan &lp)
 {
     const int d0 = h->n_groups == 2 ? h->group_deg[0] : 0;
-    const int ws = env_int3("LDPC_COOP3_WS", d0 == 10 ? g3_ws(10) : g3_ws(7)), r = env_int3("LDPC_COOP3_R", 2);
+    const int ws = env_int3("LDPC_COOP3_WS", g3_ws(g3_degree_ok(d0) ? d0 : 7)), r = env_int3("LDPC_COOP3_R", 2);
     const int rc = coop3_plan_host(h, ws, r, ho);
     if (rc != 0) return rc;
     const int k = h->n - h->m;

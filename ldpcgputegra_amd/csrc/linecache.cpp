@@ -33,6 +33,7 @@
 //   * slot 0 is the sink (the inactive slots' info entries), HBM line n / 8
 //     the sink line (rows n .. n+7: row n is the parity sink as well).
 #include <algorithm>
+#include <map>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -70,7 +71,9 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
 {
     o = LcPlan{};
     const int X = D0 - 2;
-    const int LC_OPS = S;   // line loads / writebacks per period: one per lane group (slot) of the slab waves
+    // line loads / writebacks per period: NLD per lane group (slot) of the slab
+    // waves, NLD = ceil(X / 8) (a window's ~S X accesses touch ~S X / 8 new lines)
+    const int LC_OPS = S * ((D0 - 2 + 7) / 8);
     if (S % 8 != 0 || S > 64 || nw < 4 * LC_GAP || n % 8 != 0 || k % 8 != 0 || k <= 0 || max_slots < 2 || n / 8 + 1 >= 65536)
         return lc_fail(__LINE__);
     const uint32_t nlines = (uint32_t)(k / 8), sink_line = (uint32_t)(n / 8);
@@ -222,8 +225,10 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     for (const Res &R : rs)
         if (!R.whole)
             for (int p = R.tl + LC_PUT; p <= R.tw; p++) live[cmod(p, nw)]++;
-    // assignment from the cut at p0; returns the slots used (sink excluded)
-    auto assign = [&](int p0) -> int {
+    // assignment from the cut at p0 with fit rule `rule` (0: the fitting slot
+    // whose next hold starts soonest, 1: the one freed last); returns the slots
+    // used (sink excluded)
+    auto assign = [&](int p0, int rule) -> int {
         std::vector<int> free_from, next_busy;   // per slot 1.. (index + 1), relative to p0
         constexpr int INF = 1 << 30;
         std::vector<int> order;
@@ -254,8 +259,10 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
             int best = -1;
             for (int c = 0; c < (int)free_from.size(); c++) {
                 if (free_from[c] > ra || next_busy[c] <= rb) continue;
-                if (best < 0 || next_busy[c] < next_busy[best] ||
-                    (next_busy[c] == next_busy[best] && free_from[c] > free_from[best]))
+                if (rule == 0 ? (best < 0 || next_busy[c] < next_busy[best] ||
+                                 (next_busy[c] == next_busy[best] && free_from[c] > free_from[best]))
+                              : (best < 0 || free_from[c] > free_from[best] ||
+                                 (free_from[c] == free_from[best] && next_busy[c] < next_busy[best])))
                     best = c;
             }
             if (best < 0) {
@@ -274,21 +281,171 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     std::stable_sort(cand.begin(), cand.end(), [&](int x, int y) { return live[x] < live[y]; });
     const char *ev = getenv("LDPC_LC_CUTS");
     const int ncut = std::min(nw, ev && *ev ? atoi(ev) : 1);
-    int best_p0 = cand[0], best_n = 1 << 30;
-    for (int i = 0; i < ncut; i++) {
-        const int nsl = assign(cand[i]);
-        if (ev && *ev) fprintf(stderr, "cut %d live %d -> %d slots\n", cand[i], live[cand[i]], nsl);
-        if (nsl < best_n) {
-            best_n = nsl;
-            best_p0 = cand[i];
+    // slot-by-slot chains: each new slot starts at the unassigned hold that
+    // starts first (from p0) and takes, again and again, the unassigned hold
+    // that starts soonest after its last one ends and ends before its first
+    // one starts again an iteration later -- every slot packed around the
+    // circle once (near max-live slots for holds of similar length)
+    auto chains = [&](int p0) -> int {
+        std::multimap<int, int> free_at;   // start (relative to p0) -> residency
+        int nsl = 0;
+        for (int i = 0; i < (int)rs.size(); i++) {
+            Res &R = rs[i];
+            if (R.whole) {
+                R.slot = ++nsl;
+                continue;
+            }
+            free_at.emplace(cmod(R.tl + LC_PUT - p0, nw), i);
+        }
+        while (!free_at.empty()) {
+            auto it = free_at.begin();
+            const int first = it->first, slot = ++nsl;
+            int end = first + (rs[it->second].tw - (rs[it->second].tl + LC_PUT));   // relative to p0, may pass nw
+            rs[it->second].slot = slot;
+            free_at.erase(it);
+            for (;;) {
+                // the unassigned hold starting soonest after `end` (on the line
+                // unrolled from p0; past nw it wraps to the starts + nw), if it
+                // ends before this slot's first hold starts again
+                const int want = end + 1;
+                bool wrapped = want >= nw;
+                auto nx = free_at.lower_bound(wrapped ? want - nw : want);
+                if (nx == free_at.end() && !wrapped) {
+                    nx = free_at.begin();
+                    wrapped = true;
+                }
+                if (nx == free_at.end()) break;
+                const int s_abs = nx->first + (wrapped ? nw : 0);
+                const int len = rs[nx->second].tw - (rs[nx->second].tl + LC_PUT);
+                if (s_abs + len >= first + nw) break;   // would meet the slot's first hold: slot full
+                rs[nx->second].slot = slot;
+                end = s_abs + len;
+                free_at.erase(nx);
+            }
+        }
+        return nsl;
+    };
+    // rule 0 first (the r1/2 plan measured in r04/r05); rule 1 only if that
+    // does not fit the slots the kernel has
+    int best_p0 = cand[0], best_n = 1 << 30, best_rule = 0;
+    for (int rule = 0; rule < 2 && best_n + 1 > max_slots; rule++)
+        for (int i = 0; i < ncut; i++) {
+            const int nsl = assign(cand[i], rule);
+            if (ev && *ev) fprintf(stderr, "cut %d rule %d live %d -> %d slots\n", cand[i], rule, live[cand[i]], nsl);
+            if (nsl < best_n) {
+                best_n = nsl;
+                best_p0 = cand[i];
+                best_rule = rule;
+            }
+        }
+    int used = assign(best_p0, best_rule);
+    if (used + 1 > max_slots) {   // rule 2: packed chains from the same cut
+        const int nsl = chains(best_p0);
+        const char *dbg = getenv("LDPC_LC_DEBUG");
+        if (dbg && *dbg) fprintf(stderr, "coop3 line cache: chains from cut %d -> %d slots (greedy %d)\n", best_p0, nsl, used);
+        used = nsl;
+    }
+    // still too many: empty the least-used slots by moving each of their holds
+    // into a gap of another slot (holds are cyclic arcs [tl + LC_PUT, tw]; one
+    // slot's arcs must not overlap), most-used targets first, until no slot
+    // can be emptied (the greedy cut above wastes slots near the cut)
+    if (used + 1 > max_slots) {
+        // per slot: its residencies and a bitmap of the periods its holds occupy
+        const int NWD = (nw + 63) / 64;
+        std::vector<std::vector<int>> of(used + 1);
+        std::vector<std::vector<uint64_t>> occ(used + 1, std::vector<uint64_t>(NWD, 0));
+        auto span = [&](int i, auto &&f) {   // f(word, mask) over the periods of residency i's hold
+            const Res &R = rs[i];
+            if (R.whole) {
+                for (int w = 0; w < NWD; w++) f(w, ~0ull);
+                return;
+            }
+            const int a0 = cmod(R.tl + LC_PUT, nw), len = R.tw - (R.tl + LC_PUT);
+            for (int p = 0; p <= len; p++) {
+                const int q = (a0 + p) % nw;
+                f(q >> 6, 1ull << (q & 63));
+            }
+        };
+        auto fits = [&](int i, int t) {
+            bool ok = true;
+            span(i, [&](int w, uint64_t m) { ok = ok && !(occ[t][w] & m); });
+            return ok;
+        };
+        auto put = [&](int i, int t, bool set) {
+            span(i, [&](int w, uint64_t m) { occ[t][w] = set ? (occ[t][w] | m) : (occ[t][w] & ~m); });
+        };
+        for (int i = 0; i < (int)rs.size(); i++) {
+            of[rs[i].slot].push_back(i);
+            put(i, rs[i].slot, true);
+        }
+        for (bool progress = true; progress && used + 1 > max_slots;) {
+            progress = false;
+            std::vector<int> order;
+            for (int s2 = 1; s2 <= used; s2++)
+                if (!of[s2].empty()) order.push_back(s2);
+            std::sort(order.begin(), order.end(), [&](int x, int y) { return of[x].size() < of[y].size(); });
+            for (int s2 : order) {
+                if (of[s2].empty() || used + 1 <= max_slots) continue;
+                // a home for every hold of slot s2 (the fullest slot it fits), or none moves
+                std::vector<std::pair<int, int>> moves;
+                bool ok = true;
+                for (int i : of[s2]) {
+                    int home = -1;
+                    for (int k = (int)order.size() - 1; k >= 0; k--) {   // fullest first
+                        const int t = order[k];
+                        if (t != s2 && !of[t].empty() && fits(i, t)) {
+                            home = t;
+                            break;
+                        }
+                    }
+                    if (home < 0) {
+                        ok = false;
+                        break;
+                    }
+                    put(i, home, true);
+                    moves.push_back({i, home});
+                }
+                if (!ok) {
+                    for (auto &mv : moves) put(mv.first, mv.second, false);
+                    continue;
+                }
+                for (auto &mv : moves) {
+                    rs[mv.first].slot = mv.second;
+                    of[mv.second].push_back(mv.first);
+                }
+                of[s2].clear();
+                std::fill(occ[s2].begin(), occ[s2].end(), 0);
+                used--;   // (renumbered below)
+                progress = true;
+            }
+            // renumber the slots in use densely (1 ..)
+            std::vector<int> ren(of.size(), 0);
+            int n2 = 0;
+            for (int s2 = 1; s2 < (int)of.size(); s2++)
+                if (!of[s2].empty()) ren[s2] = ++n2;
+            std::vector<std::vector<int>> of2(n2 + 1);
+            std::vector<std::vector<uint64_t>> occ2(n2 + 1);
+            for (int s2 = 1; s2 < (int)of.size(); s2++)
+                if (ren[s2]) occ2[ren[s2]].swap(occ[s2]);
+            for (int i = 0; i < (int)rs.size(); i++) {
+                rs[i].slot = ren[rs[i].slot];
+                of2[rs[i].slot].push_back(i);
+            }
+            of.swap(of2);
+            occ.swap(occ2);
+            used = n2;
         }
     }
-    const int used = assign(best_p0);
     o.slots = used + 1;
     o.residencies = (int)rs.size();
     if (o.slots > max_slots || o.slots > (int)LC_SLOT_MASK + 1) {
         const char *dbg = getenv("LDPC_LC_DEBUG");
-        if (dbg && *dbg) fprintf(stderr, "coop3 line cache: %d slots needed, %d available\n", o.slots, max_slots);
+        if (dbg && *dbg) {
+            int whole = 0;
+            for (const Res &R : rs) whole += R.whole;
+            fprintf(stderr, "coop3 line cache: %d slots needed, %d available (max live %d + %d whole residencies)\n",
+                    o.slots, max_slots, *std::max_element(live.begin(), live.end()), whole);
+        }
         return lc_fail(__LINE__);
     }
     // residency holding line L at access period p (cyclic)
@@ -465,7 +622,7 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
 int lc_check_plan(const LcPlan &o, const std::vector<uint32_t> &tab, int recw, int nw, int S, int D0, int n, int k,
                   int iters)
 {
-    const int LC_OPS = S;
+    const int LC_OPS = S * ((D0 - 2 + 7) / 8);
     const int X = D0 - 2;
     const uint32_t sink_line = (uint32_t)(n / 8);
     const int NSL = o.slots;

@@ -1,8 +1,9 @@
 """coop3 at first-group degree 10 (DVB-S2 r2/3, the reference's
-code/gpu_fixed/matrix/64800x21600 table): coop3_decode<10, 4, 2> -- 4 slab
-waves (one per SIMD) over windows of <= 32 checks, 8 information edges per
-check, two 16-bit edge-code words per codeword (96-B message records) --
-against the oracle (the reference's recurrence, CDecoder_OMS_fixed_SSE.cpp:
+code/gpu_fixed/matrix/64800x21600 table) and 14 (the DVB-S2-shaped r3/4 of
+configs[4]): coop3_decode<10 | 14, 4, 2> -- 4 slab waves (one per SIMD) over
+windows of <= 32 checks, 8 / 12 information edges per check, two 16-bit
+edge-code words per codeword (96-B message records), 1 / 2 line loads per lane
+group and period -- against the oracle (the reference's recurrence, CDecoder_OMS_fixed_SSE.cpp:
 172-546; NMS CDecoder_NMS_fixed_SSE.cpp:188-240; early termination as the
 commented `arret` test, :551-553).  The reference ships no r2/3 decoder build
 (its x86 tree has no constantes_sse.h for 64800x21600), so the oracle --
@@ -15,10 +16,11 @@ import oracle as O
 from ldpcgputegra_amd import ALGO_NMS, Code, Decoder, channel, default_params, load_table
 
 pytestmark = pytest.mark.gpu
-CODE = "dvbs2_r2_3"
+CODES = ["dvbs2_r2_3", "dvbs2shape_r3_4"]
+EBN0 = {"dvbs2_r2_3": (1.9, 2.3, 1.8, 2.2), "dvbs2shape_r3_4": (2.35, 2.6, 2.3, 2.8)}   # OMS ET, NMS ET, staged, full
 
 
-def _run(llr, iters, params, batch=None, max_batch=None):
+def _run(CODE, llr, iters, params, batch=None, max_batch=None):
     import torch
     t = load_table(CODE)
     B = llr.shape[0]
@@ -34,79 +36,84 @@ def _run(llr, iters, params, batch=None, max_batch=None):
     return out
 
 
-def _llr(B, ebn0, seed):
+def _llr(CODE, B, ebn0, seed):
     t = load_table(CODE)
     return channel.awgn_i8_host(t.n, B, seed=seed, table=channel.i8_table(channel.sigma_from_ebn0(ebn0, t.k_info / t.n)))
 
 
+@pytest.mark.parametrize("CODE", CODES)
 @pytest.mark.parametrize("batch,iters", [(1, 3), (37, 10), (200, 25)])
-def test_r23_fixed_iterations_vs_oracle(batch, iters):
+def test_r23_fixed_iterations_vs_oracle(CODE, batch, iters):
     """Fixed iterations, OMS offset 1: ragged batch (37), one codeword, and a
     batch that turns the XCD workgroup remap on (200: grid 16)."""
     t = load_table(CODE)
-    llr = _llr(batch, 1.9, 11 + batch)
+    llr = _llr(CODE, batch, EBN0[CODE][0], 11 + batch)
     eh, es, _ = O.decode_i8(t, llr, iters, return_soft=True, threads=O.host_threads())
-    h, s, its, _ = _run(llr, iters, default_params())
+    h, s, its, _ = _run(CODE, llr, iters, default_params())
     assert np.array_equal(s, es)
     assert np.array_equal(h, eh)
     assert (its == iters).all()
 
 
+@pytest.mark.parametrize("CODE", CODES)
 @pytest.mark.parametrize("nms", [False, True])
-def test_r23_early_termination_vs_oracle(nms):
+def test_r23_early_termination_vs_oracle(CODE, nms):
     """In-kernel early termination (one launch): soft, hard and iterations
     used equal the oracle's per-codeword stop; OMS and NMS factor 24."""
     t = load_table(CODE)
     B, iters = 200, 30
-    llr = _llr(B, 1.9, 5)
+    llr = _llr(CODE, B, EBN0[CODE][1] if nms else EBN0[CODE][0], 5)   # NMS 24/32 converges later than OMS
     algo, param = (O.NMS, 24) if nms else (O.OMS, 1)
     eh, es, eit = O.decode_i8(t, llr, iters, algo, param, early_term=True, return_soft=True, threads=O.host_threads())
     assert eit.min() < iters and eit.max() > eit.min()
     p = default_params(early_term=1, algo=ALGO_NMS, factor=24) if nms else default_params(early_term=1)
-    h, s, its, st = _run(llr, iters, p)
+    h, s, its, st = _run(CODE, llr, iters, p)
     assert st == 0
     assert np.array_equal(its, eit)
     assert np.array_equal(s, es)
     assert np.array_equal(h, eh)
 
 
-def test_r23_nms_fixed_vs_oracle():
+@pytest.mark.parametrize("CODE", CODES)
+def test_r23_nms_fixed_vs_oracle(CODE):
     t = load_table(CODE)
-    llr = _llr(64, 2.0, 8)
+    llr = _llr(CODE, 64, EBN0[CODE][1], 8)
     eh, es, _ = O.decode_i8(t, llr, 12, O.NMS, 29, return_soft=True, threads=O.host_threads())
-    h, s, _, _ = _run(llr, 12, default_params(algo=ALGO_NMS, factor=29))
+    h, s, _, _ = _run(CODE, llr, 12, default_params(algo=ALGO_NMS, factor=29))
     assert np.array_equal(s, es) and np.array_equal(h, eh)
 
 
-def test_r23_staged_early_termination_vs_oracle(monkeypatch):
+@pytest.mark.parametrize("CODE", CODES)
+def test_r23_staged_early_termination_vs_oracle(CODE, monkeypatch):
     """Staged early termination (compaction of the codewords still decoding
     into 16-codeword groups, messages in the 96-B record layout), forced at a
     small batch: equal to the oracle."""
     t = load_table(CODE)
     B, iters = 200, 30
-    llr = _llr(B, 1.8, 17)
+    llr = _llr(CODE, B, EBN0[CODE][2], 17)
     eh, es, eit = O.decode_i8(t, llr, iters, early_term=True, return_soft=True, threads=O.host_threads())
     k1 = int(np.percentile(eit, 30))
     assert 0 < k1 < iters and (eit > k1).any()
     monkeypatch.setenv("LDPC_COOP3_ET_STAGE_MIN", "0")
     monkeypatch.setenv("LDPC_COOP3_ET_K", str(k1))
     monkeypatch.setenv("LDPC_COOP3_ET_STEP", "3")
-    h, s, its, st = _run(llr, iters, default_params(early_term=1), max_batch=256)
+    h, s, its, st = _run(CODE, llr, iters, default_params(early_term=1), max_batch=256)
     assert st == k1
     assert np.array_equal(its, eit)
     assert np.array_equal(s, es)
     assert np.array_equal(h, eh)
 
 
-def test_r23_full_batch_fixed_50_sampled_vs_oracle():
-    """configs[2]'s shape on r2/3: batch 4096, 50 iterations, 2.2 dB (bench.py
-    --mixed-codes reference's Eb/N0 for r2/3): a seeded sample of 256
-    codewords (spread over every XCD's workgroups) equals the oracle's
-    decode, hard decisions and soft output."""
+@pytest.mark.parametrize("CODE", CODES)
+def test_r23_full_batch_fixed_50_sampled_vs_oracle(CODE):
+    """configs[2]'s shape on the higher rates: batch 4096, 50 iterations, at
+    bench.py's --mixed Eb/N0 of the rate: a seeded sample of 256 codewords
+    (spread over every XCD's workgroups) equals the oracle's decode, hard
+    decisions and soft output."""
     t = load_table(CODE)
     B, iters = 4096, 50
-    llr = _llr(B, 2.2, 2024)
-    h, s, _, _ = _run(llr, iters, default_params(), max_batch=B)
+    llr = _llr(CODE, B, EBN0[CODE][3], 2024)
+    h, s, _, _ = _run(CODE, llr, iters, default_params(), max_batch=B)
     sel = np.sort(np.random.default_rng(1).choice(B, 256, replace=False))
     eh, es, _ = O.decode_i8(t, llr[sel], iters, return_soft=True, threads=O.host_threads())
     assert np.array_equal(s[sel], es)

@@ -30,7 +30,7 @@ def test_dvbs2_r2_3_plan_fits_and_replays():
     assert b["swizzled"] < 0.02 * b["plain"]
 
 
-@pytest.mark.parametrize("name", ["576x288", "dvbs2shape_r3_4", "dvbs2_r8_9"])
+@pytest.mark.parametrize("name", ["576x288", "dvbs2shape_r5_6", "dvbs2_r8_9"])
 def test_codes_without_coop3_have_no_plan(name):
     if name not in available():
         pytest.skip("code table absent")

@@ -2,11 +2,11 @@
 """Build-time guard for coop3's hand-counted `s_waitcnt vmcnt(36)`.
 
 coop3's memory wave (csrc/coop3.hip, `mperiod`) issues, per period, for each of
-the WS slab-wave sets (6 for DVB-S2 r1/2's kernel, 4 for r2/3's), in this
-order: one line load, one LDS-DMA gather (`buffer_load_dwordx4 ... lds`,
-inline asm the compiler does not count), one line writeback and one store --
-4 * WS vector-memory instructions -- and closes the period with vmcnt(4 * WS +
-2 * WS) right before its barrier:
+the WS slab-wave sets (6 for DVB-S2 r1/2's kernel, 4 for the higher rates'),
+in this order: NLD line loads (all sets), one LDS-DMA gather (`buffer_load_dwordx4
+... lds`, inline asm the compiler does not count), NLD line writebacks and one
+store -- (2 NLD + 2) WS vector-memory instructions, NLD = ceil((D0 - 2) / 8) --
+and closes the period with vmcnt((3 NLD + 3) WS) right before its barrier:
 everything up to the previous period's gathers (and so its line loads) has
 landed.  That count is only right while the compiler emits exactly those 24
 instructions per period (no split, no extra load, no scratch spill).  This
@@ -91,9 +91,18 @@ def closes_period(lines, i, reach=8):
     return False
 
 
-# coop3_decode<D0, WS, R, STAMP, ET, NMS>: the slab-wave count WS sets the
-# period's op count (4 WS) and closing wait (6 WS)
+# coop3_decode<D0, WS, R, STAMP, ET, NMS>: the slab-wave count WS and the line
+# ops per lane group NLD = ceil((D0 - 2) / 8) set the period's op count
+# ((2 NLD + 2) WS), their order and the closing wait ((3 NLD + 3) WS)
 WS_NAME = re.compile(r"coop3_decodeILi(\d+)ELi(\d+)ELi\d+E")
+
+
+def counts(name):
+    """(ops, vmcnt, expected order) of a coop3 kernel from its template arguments."""
+    m = WS_NAME.search(name)
+    d0, ws = (int(m.group(1)), int(m.group(2))) if m else (7, 6)
+    nld = (d0 - 2 + 7) // 8
+    return (2 * nld + 2) * ws, (3 * nld + 3) * ws, "L" * (nld * ws) + "G" * ws + "S" * ((nld + 1) * ws)
 
 
 def check(isa, ops=None, vmcnt=None, min_regions=1, pattern="coop3_decode"):
@@ -106,10 +115,9 @@ def check(isa, ops=None, vmcnt=None, min_regions=1, pattern="coop3_decode"):
         return ["no %s kernel in the disassembly" % pattern], 0
     base_ops, base_vmcnt = ops, vmcnt
     for name, lines in kernels.items():
-        m = WS_NAME.search(name)
-        ws = int(m.group(2)) if m else 6
-        ops = base_ops if base_ops is not None else 4 * ws
-        vmcnt = base_vmcnt if base_vmcnt is not None else 6 * ws
+        k_ops, k_vmcnt, want = counts(name)
+        ops = base_ops if base_ops is not None else k_ops
+        vmcnt = base_vmcnt if base_vmcnt is not None else k_vmcnt
         wait = re.compile(r"^\s*s_waitcnt\s+.*vmcnt\(%d\)" % vmcnt)
         if any(re.match(r"^\s*scratch_", l) for l in lines):
             errs.append("%s: scratch access (a spill adds vector-memory ops the vmcnt does not count)" % name)
@@ -127,11 +135,9 @@ def check(isa, ops=None, vmcnt=None, min_regions=1, pattern="coop3_decode"):
                 errs.append("%s: %d vector-memory instructions between the vmcnt(%d) waits at ISA lines %d and %d, "
                             "the wait assumes %d per period" % (name, n, vmcnt, a, b, ops))
             else:
-                # the count is right only in this order: WS line loads, WS
-                # LDS-DMA gathers, then the 2 WS writebacks / stores
+                # the count is right only in this order: NLD WS line loads,
+                # WS LDS-DMA gathers, then the (NLD + 1) WS writebacks / stores
                 seq = "".join(kind(l) for l in body if VMEM.match(l))
-                ws = ops // 4
-                want = "L" * ws + "G" * ws + "S" * (2 * ws)
                 if seq != want:
                     errs.append("%s: vector-memory order %s between the waits at ISA lines %d and %d, the vmcnt(%d) "
                                 "argument assumes %s (line loads, gathers, stores)" % (name, seq, a, b, vmcnt, want))
@@ -155,8 +161,8 @@ def main():
         for e in errs:
             print("check_vmcnt: " + e, file=sys.stderr)
         return 1
-    print("check_vmcnt: ok (%d memory-wave periods checked: 4 WS vector-memory ops in order, vmcnt(6 WS); "
-          "WS = 6 for degree 7, 4 for degree 10)" % n)
+    print("check_vmcnt: ok (%d memory-wave periods checked: (2 NLD + 2) WS vector-memory ops in order, "
+          "vmcnt((3 NLD + 3) WS); degree 7: WS 6, NLD 1; 10: WS 4, NLD 1; 14: WS 4, NLD 2)" % n)
     return 0
 
 
