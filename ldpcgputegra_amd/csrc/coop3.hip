@@ -1485,9 +1485,11 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
         for (int k = 0; k < pl.count[u]; k++)
             for (int j = 0; j < X; j++) {
                 const uint32_t f = code_at(rec_at(u, k), j);
-                if (f == COOP_FWD_NONE || (f >> 9) != 2) continue;
+                // forwarding code: dW << (6 + EB) | slot << EB | edge (coop.h; EB = 5 above 8 info edges)
+                const int EB = coop_fwd_eb(X);
+                if (f == COOP_FWD_NONE || (int)(f >> (6 + EB)) != 2) continue;
                 special[(size_t)u * S + k] = 1;
-                special[(size_t)((u + nw - 2) % nw) * S + ((f >> 3) & 63)] = 1;
+                special[(size_t)((u + nw - 2) % nw) * S + ((f >> EB) & 63)] = 1;
             }
     std::vector<int> check_at((size_t)nw * S);   // slot -> plan slot (= chain step)
     for (int u = 0; u < nw; u++) {
@@ -1519,6 +1521,34 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
             rec[D0] |= (uint32_t)k << STEP_SHIFT;
         }
     pl.tab.swap(tab);
+    // self-check of what the kernel relies on, from the records themselves:
+    // no information variable is shared by a window and its neighbour, and a
+    // variable window u reads that window u-2 wrote (the writer's post and the
+    // reader's pre run in the same period) has writer and reader in slab wave 0
+    // (slots 0..7), which posts before its pre
+    {
+        std::vector<int> wu(h->n, -1), wk(h->n, -1);   // last writer window / slot per variable (two sweeps)
+        for (int pass = 0; pass < 2; pass++)
+            for (int u = 0; u < nw; u++)
+                for (int k = 0; k < S; k++) {
+                    const uint32_t *rec = &pl.tab[((size_t)u * S + k) * RECW];
+                    if (!(rec[D0] & COOP_M_ACT)) continue;
+                    for (int j = 0; j < X; j++) {
+                        const uint32_t v = rec[j];
+                        if (pass == 1 && wu[v] >= 0) {
+                            const int d = (u - wu[v] + nw) % nw;
+                            if (d == 1 || (d == 0 && nw > 1 && wk[v] != k))
+                                return ldpc_set_error(LDPC_EINVAL, "coop3 plan: variable %u in windows %d and %d", v,
+                                                      wu[v], u);
+                            if (d == 2 && (k >= 8 || wk[v] >= 8))
+                                return ldpc_set_error(LDPC_EINVAL, "coop3 plan: distance-2 variable %u outside slab "
+                                                      "wave 0 (slots %d, %d)", v, wk[v], k);
+                        }
+                        wu[v] = u;
+                        wk[v] = k;
+                    }
+                }
+    }
     o.S = S;
     o.nw = nw;
     o.recw = RECW;

@@ -16,11 +16,14 @@
 //   floats for 648), and the LDS byte offset of its edge's variable per slot
 //   (host-built table, loaded once): per layer and pass the only LDS traffic is
 //   one V read and one V write per lane;
-// * min1 / min2 and the sign parity of the 8 lanes by a 3-step DPP
-//   butterfly (quad_perm xor 1, xor 2, row_half_mirror) on the magnitudes as
-//   integers (|c| bit patterns order like the floats) and on the sign bits;
-//   each lane's message is its constant with the sign bit of the others'
-//   parity xored in (-0.0 exactly as the reference's -r);
+// * each lane's minimum over the check's OTHER edges and the sign parity of
+//   the 8 lanes by a 3-step DPP butterfly (quad_perm xor 1, xor 2,
+//   row_half_mirror) on the magnitudes as integers (|c| bit patterns order
+//   like the floats) and on the sign bits -- an exclusive-min butterfly (5
+//   VALU, r05; min1 / min2 and a select took ~14) whose result equals the
+//   reference's (a == min1 ? min2 : min1); each lane's message is its
+//   constant with the sign bit of the others' parity xored in (-0.0 exactly
+//   as the reference's -r);
 // * unused lanes of a check (degree 7 in an 8-lane group) read a sink
 //   variable V[N] = -inf: |c| = +inf never wins a minimum, and c < 0 adds one
 //   to the sign parity -- exactly the reference's odd-degree flip
@@ -105,23 +108,24 @@ __global__ void __launch_bounds__(64 * EP_WAVES) ldsep_decode(EpArgs a)
                 const float cj = c[p] - msg[s];
                 const uint32_t aj = __float_as_uint(cj) & ~SIGN;   // |c| (as an ordered integer)
                 const uint32_t sj = __float_as_uint(cj) & SIGN;    // c < 0
-                // min1 / min2 and the sign parity of the 8 lanes
-                uint32_t t = dpp_xor1(aj);
-                uint32_t m1 = min(aj, t), m2 = max(aj, t);
+                // the minimum over the OTHER 7 lanes of the check (E) by an
+                // exclusive-min butterfly: M = the min of this lane's group,
+                // E = the min of its group without itself; each stage E =
+                // min(E, partner's M), M = min(M, partner's M) (5 VALU, each
+                // with its DPP fused).  E is exactly the reference's selection
+                // (a_j == min1 ? min2 : min1): min2 is the min without one
+                // occurrence of min1
+                uint32_t e = dpp_xor1(aj);
+                uint32_t mm = min(aj, e);
+                e = min(e, dpp_xor2(mm));
+                mm = min(mm, dpp_xor2(mm));
+                e = min(e, dpp_hmirror(mm));
                 uint32_t sg = sj ^ dpp_xor1(sj);
-                t = dpp_xor2(m1);
-                uint32_t u = dpp_xor2(m2);
-                m2 = min(max(m1, t), min(m2, u));
-                m1 = min(m1, t);
                 sg ^= dpp_xor2(sg);
-                t = dpp_hmirror(m1);
-                u = dpp_hmirror(m2);
-                m2 = min(max(m1, t), min(m2, u));
-                m1 = min(m1, t);
                 sg ^= dpp_hmirror(sg);
-                // cst1 (from min2) on the min1 edge, else cst2; negative when
-                // the parity of the other edges' signs (and the degree flip) is odd
-                const float sel = __uint_as_float(aj == m1 ? m2 : m1);
+                // cst of the others' minimum; negative when the parity of the
+                // other edges' signs (and the degree flip) is odd
+                const float sel = __uint_as_float(e);
                 const float r = NMS ? sel * a.beta : fmaxf(sel - a.beta, 0.0f);
                 const float m = __uint_as_float(__float_as_uint(r) ^ (sg ^ sj));
                 msg[s] = m;

@@ -30,6 +30,17 @@ def test_dvbs2_r2_3_plan_fits_and_replays():
     assert b["swizzled"] < 0.02 * b["plain"]
 
 
+def test_dvbs2shape_r3_4_plan_fits_and_replays():
+    """First-group degree 14 (the shaped r3/4: 12 information edges per
+    check, two line loads per lane group and period): the greedy slot
+    assignment does not fit the 784 slots, the packed chains + slot
+    elimination do; the plan replays, and the schedule's self-check (no
+    variable in neighbouring windows, every distance-2 writer / reader pair in
+    slab wave 0 -- the pair the forwarding codes with 5 edge bits mark) holds."""
+    lc = Code("dvbs2shape_r3_4").coop3_line_cache()
+    assert lc is not None and 2 <= lc["slots"] <= lc["max_slots"] == 784
+
+
 @pytest.mark.parametrize("name", ["576x288", "dvbs2shape_r5_6", "dvbs2_r8_9"])
 def test_codes_without_coop3_have_no_plan(name):
     if name not in available():
