@@ -109,8 +109,20 @@ constexpr int TQ = 8;               // window-table slots in LDS
 //
 // Messages of a check, per 16-codeword group (MREC bytes): [8 pairs][MA0,
 // MB] u32 (MB: eps cst1 / eps cst2 bytes per codeword; MA0: 2-bit codes of
-// edges 0..7, 16 bits per codeword), then for D0 > 8 [8 pairs][MA1] (edges
-// 8 .. 15): 4 B (D0 <= 8) or 6 B per codeword and check.
+// edges 0..7, 16 bits per codeword), then for each further 8 edges
+// [8 pairs][MAk] (edges 8k .. 8k+7): 4 B (D0 <= 8) up to 10 B (D0 <= 32) per
+// codeword and check.
+//
+// First-group degrees 22, 27, 30 (the shaped r5/6, r8/9, r9/10: 20 to 28
+// information edges) run WS = 2 slab waves (S = 16: the records, messages and
+// line-op words of larger windows would not leave the line cache the ~700
+// live lines these codes need), each alone on its SIMD, with the window plan
+// at distance 2 (windows u and u+2 share no information variable either --
+// at S = 16 this costs these codes no window -- so no slot permutation is
+// needed), |c| recomputed in the post and the info edges' line-cache offsets
+// re-read there from the window's records (VGPRs: 3 window states of ~30
+// contributions each).  Their gathers (9 / 11 pieces per slot) and stores
+// (10 / 12) take two 64-lane instructions per 8-slot set.
 template <int D0_>
 struct G3 {
     static constexpr int D0 = D0_, X = D0 - 2;                 // check degree, information edges per check
@@ -118,17 +130,22 @@ struct G3 {
     static constexpr int MREC = 32 * (NMA + 1);                // message bytes per check and group
     static constexpr int MP = MREC / 16;                       // message pieces (16 B) per check
     static constexpr int NG = MP + 1;                          // pieces gathered per slot (+ the o-edge parity row)
+    static constexpr int NGI = (8 * NG + 63) / 64;             // gather instructions per 8-slot set
+    static constexpr int NSI = (MP + 2 + 7) / 8;               // store instructions per 8-slot set (MP + 2 pieces)
     static constexpr int W_X = X, W_O = X + 1, W_META = X + 2;
     static constexpr int NLD = (X + 7) / 8;                    // line loads / writebacks per lane group and
                                                                // period (a window touches ~S X / 8 new lines)
     static constexpr int W_LOP = (W_META + 1 + 3) / 4 * 4;     // line-op words (NLD uint4)
     static constexpr int RECW = W_LOP + 4 * NLD;               // slot record words
     static constexpr int NR = (W_META + 1 + 3) / 4;            // uint4 a pre reads of its record
-    static constexpr int WS = D0 == 7 ? 6 : 4;                 // slab waves: S = 8 WS checks per window (r1/2's
+    static constexpr int WS = D0 == 7 ? 6 : D0 <= 14 ? 4 : 2;  // slab waves: S = 8 WS checks per window (r1/2's
                                                                // windows fill 45 of 48, r2/3's 30 of 32)
-    static constexpr int LCS = D0 == 7 ? 752 : D0 == 10 ? 848 : 784;   // line-cache slots (128 B each; slot 0
-                                                               // the sink): what the 160 KB of LDS leave beside the rest
-    static_assert(NMA <= 2 && 8 * NG <= 64 && MP + 2 <= 8, "message pieces: one gather and one store per slot set");
+    static constexpr int DIST = WS == 2 ? 2 : 1;               // windows closer than DIST + 1 share no info variable
+    static constexpr bool KEEP_AD = X <= 16;                   // info edges' LDS offsets kept from pre to post
+    static constexpr int LCS = D0 == 7 ? 752 : D0 == 10 ? 848 : D0 == 14 ? 784 : D0 == 22 ? 960 : D0 == 27 ? 912 : 896;
+                                                               // line-cache slots (128 B each; slot 0 the sink): what
+                                                               // the 160 KB of LDS leave beside the rest
+    static_assert(NMA <= 4 && NGI <= 2 && NSI <= 2 && LCS <= 1023, "message pieces / slot field");
 };
 #ifndef LDPC_C3_MSLEEP
 #define LDPC_C3_MSLEEP 4      // memory wave: s_sleep (x 64 cycles) after its line loads, before its LDS burst
@@ -174,7 +191,7 @@ struct alignas(16) Smem3 {
                                       // read_x measured 0.3 % slower, r05g)
     struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
         uint4 d[G::NG][8];            //   e < MP: message bytes 16e .. 16e+15, e = MP: the o-edge parity row
-    } in[WS][NI];
+    } in[WS][NI];                     //   (NGI = 2: the second gather lands pieces 8 .. MP, 1 KB further)
     uint4 mst[2][WS][8][G::MP + 2];   // window g's outputs per slab wave in mst[g & 1], per slot: its new
                                       // messages (pieces 0..MP-1), the x edge's new V (piece MP) and the
                                       // tail's last edge's (MP + 1), 16 codewords each (posted in period
@@ -209,14 +226,15 @@ struct Coop3Args {
 // post but recomputed there (abs_sat / abs_r of c, 2 VALU per edge)
 template <int D0, bool LEAN = false>
 struct St3 {                          // one window's state from pre to post (R / C pairs)
-    static constexpr int X = D0 - 2;
+    static constexpr int X = D0 - 2, NMA = G3<D0>::NMA;
     uint32_t c[D0 - 1];               // contributions (info, o); tail: new V
     uint32_t a[LEAN ? 1 : D0 - 1];    // |c| (not clipped: min1 / min2 are, where the constants are made)
     uint32_t mn1, mn2, sacc, mx;      // min1 / min2 / sign parity over info + o; x-edge old message
-                                      // tail: mn1 = MA0, mn2 = MB, ma1 = MA1
-    uint32_t ma1;
+                                      // tail: mn1 = MA0, mn2 = MB, mat = MA1 ..
+    uint32_t mat[NMA > 1 ? NMA - 1 : 1];
     uint32_t xs;                      // the slot's chain step: u16 index of its x input in xo[buf]
-    uint32_t ad[X];                   // the info edges' pair addresses in the line cache (pre reads, post writes)
+    uint32_t ad[G3<D0>::KEEP_AD ? X : 1];   // the info edges' pair addresses in the line cache (pre reads, post
+                                      // writes; !KEEP_AD: the post re-reads them from the window's records)
     uint32_t v[X > 8 ? 1 : X];        // FZ (early termination): the info edges' V as read (R pairs; X > 8:
                                       // re-read from LDS by the post, Slab3::FZ_REREAD)
 };
@@ -253,21 +271,18 @@ struct Rec {
 // what a pre reads from LDS
 template <int D0>
 struct PreIn {
-    static constexpr int X = D0 - 2;
+    static constexpr int X = D0 - 2, NMA = G3<D0>::NMA;
     uint32_t v[D0 - 1];               // raw V dwords (info edges from the line cache, the o edge from In)
-    uint32_t ad[X];                   // the info pairs' byte offsets in the line cache
-    uint32_t ma, mb, ma1;             // old message record of this pair (MA1: D0 > 8)
+    uint32_t ad[G3<D0>::KEEP_AD ? X : 1];   // the info pairs' byte offsets in the line cache
+    uint32_t ma[NMA], mb;             // old message record of this pair (MA0 .. MA(NMA-1), MB)
     uint32_t meta, wx, wo;            // record words W_META, W_X, W_O
 };
 
-// old message / new code of edge J: edges 0..7 in MA0, 8..15 in MA1
-template <int J>
-LDPC_DEV uint32_t old_msg2(uint32_t MA0, uint32_t MA1, const MsgTab &t, const PkK &K)
+// old message of edge J: edges 8k .. 8k+7 in MA[k]
+template <int J, int NMA>
+LDPC_DEV uint32_t old_msg2(const uint32_t (&MA)[NMA], const MsgTab &t, const PkK &K)
 {
-    if constexpr (J < 8)
-        return old_msg<J>(MA0, t, K.m3, K.c4);
-    else
-        return old_msg<J - 8>(MA1, t, K.m3, K.c4);
+    return old_msg<J & 7>(MA[J >> 3], t, K.m3, K.c4);
 }
 
 template <int D0, int WS, int R, bool NMS = false, bool LEAN = false>
@@ -315,8 +330,10 @@ struct Slab3 {
     LDPC_DEV void read_pre(int ib, const RecT &rc, In &in) const
     {
         const char *inb = (const char *)&sm.in[w][ib];
+        if constexpr (G::KEEP_AD) {
 #pragma unroll
-        for (int j = 0; j < X; j++) in.ad[j] = rc.w(j) + lwr;
+            for (int j = 0; j < X; j++) in.ad[j] = rc.w(j) + lwr;
+        }
 #pragma unroll
         for (int j = 0; j < X; j++) in.v[j] = *(const uint32_t *)(lcb() + rc.w(j) + lrd);   // the dword holding this lane's pair
         in.v[X] = *(const uint32_t *)(inb + prd);
@@ -325,12 +342,21 @@ struct Slab3 {
 #else
         const uint2 mm = *(const uint2 *)(inb + mrd);
 #endif
-        in.ma = mm.x;
+        in.ma[0] = mm.x;
         in.mb = mm.y;
-        in.ma1 = G::NMA > 1 ? *(const uint32_t *)(inb + m1rd) : 0u;
+#pragma unroll
+        for (int i = 1; i < G::NMA; i++) in.ma[i] = *(const uint32_t *)(inb + m1rd + 256 * (i - 1));   // [8 pairs][MAi]
         in.meta = rc.w(G::W_META);
         in.wx = rc.w(G::W_X);
         in.wo = rc.w(G::W_O);
+    }
+    // LDS byte offset of this lane's pair of info edge j of window g (pre reads, post writes)
+    LDPC_DEV uint32_t ad_of(int g, const St &s, int j) const
+    {
+        if constexpr (G::KEEP_AD)
+            return s.ad[j];
+        else
+            return sm.tab[g & (TQ - 1)][k][j] + lwr;   // window g's records stay in the ring until its stores
     }
     LDPC_DEV uint32_t read_x(int g, const St &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
@@ -353,10 +379,12 @@ struct Slab3 {
         uint32_t v[D0 - 1];
 #pragma unroll
         for (int j = 0; j <= X; j++) v[j] = unpack_v(in.v[j], usel);
+        if constexpr (G::KEEP_AD) {
 #pragma unroll
-        for (int j = 0; j < X; j++) s.ad[j] = in.ad[j];
+            for (int j = 0; j < X; j++) s.ad[j] = in.ad[j];
+        }
         const MsgTab t = msg_tab(in.mb);
-        const uint32_t MA = in.ma, MA1 = in.ma1, neg127 = K.neg127, c510 = K.c510;
+        const uint32_t neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
         uint32_t A, B, EPS, COV, L, H;
         if constexpr (!TL) {
@@ -368,7 +396,7 @@ struct Slab3 {
             // and |c| (abs_sat caps it at R(127) as the reference's clamp does)
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_sub_sat(v[J], old_msg2<J>(MA, MA1, t, K));
+                const uint32_t c = pk_sub_sat(v[J], old_msg2<J>(in.ma, t, K));
                 const uint32_t aj = abs_sat(c, c510);
                 s.c[J] = c;
                 if constexpr (!LEAN) s.a[J] = aj;
@@ -385,14 +413,14 @@ struct Slab3 {
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
-            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg2<D0 - 1>(MA, MA1, t, K)), neg127);
+            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg2<D0 - 1>(in.ma, t, K)), neg127);
             const uint32_t ao = abs_r(cor, c510);
             s.c[X] = cor;
             if constexpr (!LEAN) s.a[X] = ao;
             s.sacc = sacc ^ cor;
             s.mn2 = pk_max(min1, pk_min(ao, min2));
             s.mn1 = pk_min(min1, ao);
-            const uint32_t mx = old_msg2<X>(MA, MA1, t, K);
+            const uint32_t mx = old_msg2<X>(in.ma, t, K);
             s.mx = mx;
             // chain constants in value form (R >> 8, C >> 8), both codewords at once
             COV = pk_ashr8(cor);
@@ -429,7 +457,7 @@ struct Slab3 {
             auto av = [&](int j) __attribute__((always_inline)) -> uint32_t & { return LEAN ? avl[LEAN ? j : 0] : s.a[LEAN ? 0 : j]; };
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg2<J>(MA, MA1, t, K)), neg127);
+                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg2<J>(in.ma, t, K)), neg127);
                 // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2
                 const uint32_t aj = NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510);
                 s.c[J] = c;
@@ -442,20 +470,20 @@ struct Slab3 {
                                     : pk_min(pk_max(pk_sub(min2, K.coff), 0u), K.rmm) & HIBYTES;
             const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
                                     : pk_min(pk_max(pk_sub(min1, K.coff), 0u), K.rmm) & HIBYTES;
-            uint32_t e1, e2, MAn = 0, MAn1 = 0;
+            uint32_t e1, e2, MAn[G::NMA];
+#pragma unroll
+            for (int i = 0; i < G::NMA; i++) MAn[i] = 0;
             signed_csts(k1, k2, sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u), e1, e2);
             static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                if constexpr (J < 8)
-                    s.c[J] = new_v_later<J>(s.c[J], av(J), min1, e1, e2, MAn, neg127);
-                else
-                    s.c[J] = new_v_later<J - 8>(s.c[J], av(J), min1, e1, e2, MAn1, neg127);
+                s.c[J] = new_v_later<J & 7>(s.c[J], av(J), min1, e1, e2, MAn[J >> 3], neg127);
                 if constexpr (FZ) s.c[J] = bfi(fm, v[J], s.c[J]);   // converged codewords keep their V
             });
             s.mx = 0;
             s.sacc = 0;
-            s.mn1 = MAn;
-            s.ma1 = MAn1;
+            s.mn1 = MAn[0];
+#pragma unroll
+            for (int i = 1; i < G::NMA; i++) s.mat[i - 1] = MAn[i];
             s.mn2 = perm(e2, e1, 0x07030501u);
             // the chain passes V[p_0] (the tail's last edge) on: A = B = c_o = L = H = y
             // (NMS: A = 32 y, B = 32 y + 31)
@@ -501,19 +529,18 @@ struct Slab3 {
         constexpr bool FZ = FZ_;
         unsigned short *sx = (unsigned short *)&sm.mst[g & 1][w][kl][G::MP] + q,
                        *so = (unsigned short *)&sm.mst[g & 1][w][kl][G::MP + 1] + q;
-        auto put = [&](int j, uint32_t v) __attribute__((always_inline)) {
-            *(unsigned short *)(lcw() + s.ad[j]) = (unsigned short)v;
+        auto put = [&](uint32_t ad, uint32_t v) __attribute__((always_inline)) {
+            *(unsigned short *)(lcw() + ad) = (unsigned short)v;
         };
-        // edge J's code into MA (J < 8) or MA1
-        auto nv = [&](auto jc, uint32_t c, uint32_t av, uint32_t min1, uint32_t e1, uint32_t e2, uint32_t &MA0,
-                      uint32_t &MA1_) __attribute__((always_inline)) -> uint32_t {
+        // edge J's code into MA[J / 8]
+        uint32_t MA[G::NMA], MB;
+#pragma unroll
+        for (int i = 0; i < G::NMA; i++) MA[i] = 0;
+        auto nv = [&](auto jc, uint32_t c, uint32_t av, uint32_t min1, uint32_t e1, uint32_t e2)
+                      __attribute__((always_inline)) -> uint32_t {
             constexpr int J = decltype(jc)::value;
-            if constexpr (J < 8)
-                return new_v<J>(c, av, min1, e1, e2, MA0, K.c510);
-            else
-                return new_v<J - 8>(c, av, min1, e1, e2, MA1_, K.c510);
+            return new_v<J & 7>(c, av, min1, e1, e2, MA[J >> 3], K.c510);
         };
-        uint32_t MA, MB, MA1 = 0;
         if constexpr (!TL) {
             const uint32_t cx = pk_sub_sat(xr, s.mx);   // unclamped, as the info edges' (new_v)
             const uint32_t ax = abs_sat(cx, K.c510);
@@ -525,44 +552,44 @@ struct Slab3 {
                                     : pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), 0u);
             uint32_t e1, e2;
             signed_csts(k1, k2, sacc ^ ((D0 & 1) ? SIGNS : 0u), e1, e2);
-            MA = 0;
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
                 const uint32_t aJ = LEAN ? abs_sat(s.c[J], K.c510) : s.a[LEAN ? 0 : J];
-                const uint32_t n = nv(jc, s.c[J], aJ, min1, e1, e2, MA, MA1);
+                const uint32_t n = nv(jc, s.c[J], aJ, min1, e1, e2);
+                const uint32_t ad = ad_of(g, s, J);
                 if constexpr (FZ && FZ_REREAD)
-                    put(J, perm(n, *(const unsigned short *)(lcb() + s.ad[J]), psel_raw));
+                    put(ad, perm(n, *(const unsigned short *)(lcb() + ad), psel_raw));
                 else
-                    put(J, FZ ? perm(n, s.v[FZ_REREAD ? 0 : J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
+                    put(ad, FZ ? perm(n, s.v[FZ_REREAD ? 0 : J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
             });
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
-            const uint32_t nx = nv(std::integral_constant<int, X>{}, cx, ax, min1, e1, e2, MA, MA1);
+            const uint32_t nx = nv(std::integral_constant<int, X>{}, cx, ax, min1, e1, e2);
             *sx = (unsigned short)(FZ ? perm(nx, xr, psel) : pack_v(nx));
             // the o edge: its code only (the next check rewrites V[o] as its x edge)
             const uint32_t aO = LEAN ? abs_r(s.c[X], K.c510) : s.a[LEAN ? 0 : X];
-            if constexpr (D0 - 1 < 8)
-                msg_code<D0 - 1>(s.c[X], aO, min1, MA);
-            else
-                msg_code<D0 - 9>(s.c[X], aO, min1, MA1);
+            msg_code<(D0 - 1) & 7>(s.c[X], aO, min1, MA[(D0 - 1) >> 3]);
             MB = perm(e2, e1, 0x07030501u);
         } else {
             static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                put(J, pack_v(s.c[J]));
+                put(ad_of(g, s, J), pack_v(s.c[J]));
             });
             *sx = (unsigned short)pack_v(xr);       // V of the last group-0 check's o edge
             *so = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
-            MA = s.mn1;
+            MA[0] = s.mn1;
             MB = s.mn2;
-            MA1 = s.ma1;
+#pragma unroll
+            for (int i = 1; i < G::NMA; i++) MA[i] = s.mat[i - 1];
         }
 #ifdef C3X_BANK_MST
-        *(uint2 *)((char *)&sm.mst[g & 1][w][0][0] + 8 * lane) = make_uint2(MA, MB);
+        *(uint2 *)((char *)&sm.mst[g & 1][w][0][0] + 8 * lane) = make_uint2(MA[0], MB);
 #else
-        *(uint2 *)((char *)&sm.mst[g & 1][w][kl][0] + 8 * q) = make_uint2(MA, MB);
+        *(uint2 *)((char *)&sm.mst[g & 1][w][kl][0] + 8 * q) = make_uint2(MA[0], MB);
 #endif
-        if constexpr (G::NMA > 1) *(uint32_t *)((char *)&sm.mst[g & 1][w][kl][4] + 4 * q) = MA1;   // [8 pairs][MA1]
+#pragma unroll
+        for (int i = 1; i < G::NMA; i++)   // [8 pairs][MAi]: pieces 4 + 2 (i - 1) ..
+            *(uint32_t *)((char *)&sm.mst[g & 1][w][kl][4 + 2 * (i - 1)] + 4 * q) = MA[i];
     }
 };
 
@@ -826,7 +853,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             }
             __syncthreads();
             bool done = false;
-            constexpr int CR = D0 * 8 <= 80 ? 8 : 4;   // checks per thread and round (their edge ids in VGPRs)
+            constexpr int CR = D0 <= 10 ? 8 : D0 <= 16 ? 4 : 2;   // checks per thread and round (edge ids in VGPRs)
             for (int c0 = 0; c0 < a.m0 && !done; c0 += NT * CR) {
                 uint32_t ev[CR][D0];
 #pragma unroll
@@ -957,46 +984,67 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         // per address (shift-and-add with a per-lane shift and base)
         const i32x4 vr = buffer_rsrc(Vg, 0u, 0xFFFFFFFFu);
         const uint32_t moff = (uint32_t)(Mb - (const char *)Vg), poff = (uint32_t)a.k * 16u;
-        // gathers: lane (e, slot) = (kl, q): e < MP message piece e, e = MP the
-        // o-edge parity row (Smem3::In; a slot-major order without the pair
-        // reads' 2-way bank conflict measured 0.3 % slower, r05g)
-        constexpr int MP = GG::MP;
+        // gathers, instruction i: lane (kl, q) = (piece e - 8 i, slot): e < MP message
+        // piece e, e = MP the o-edge parity row (Smem3::In; a slot-major order
+        // without the pair reads' 2-way bank conflict measured 0.3 % slower, r05g)
+        constexpr int MP = GG::MP, NGI = GG::NGI, NSI = GG::NSI;
         constexpr uint32_t MREC = GG::MREC;
-        const uint32_t gshl = kl < MP ? 6u : 4u, goff = kl < MP ? moff + 16u * (uint32_t)kl : poff;
-        const uint32_t gmul = kl < MP ? MREC : 16u;
-        const uint32_t gmask = kl < MP ? COOP_CHK_MASK : 0xFFFFu;
-        const uint32_t gsel = (uint32_t)(kl < MP ? GG::W_META : GG::W_O);
-        // stores: lane (kl, q) of slot 8w + kl: q < MP message piece q, q = MP the
-        // x-edge parity row, q = MP + 1 the tail's last edge, the rest the sink row
-        const uint32_t sshl = q < MP ? 6u : 4u, soff = q < MP ? moff + 16u * (uint32_t)q : poff;
-        const uint32_t smul = q < MP ? MREC : 16u;
-        const uint32_t stw = 4u * (uint32_t)(q < MP ? GG::W_META : q == MP ? GG::W_X : GG::W_O);
-        const uint32_t stm = q < MP ? COOP_CHK_MASK : 0xFFFFu;
-        const uint32_t snk = q >= MP + 1 ? 0xFFFFFFFFu : 0u, snk_tl = q >= MP + 2 ? 0xFFFFFFFFu : 0u;
-        // byte offset of record idx: a shift when the message block is 64 B (r1/2), else one mad
-        auto goffs = [&](uint32_t idx) __attribute__((always_inline)) -> uint32_t {
-            if constexpr (MREC == 64) return (idx << gshl) + goff;
-            else return idx * gmul + goff;
+        constexpr bool MSHIFT = MREC == 64 || MREC == 128;   // record offsets by a shift, else one mad
+        constexpr uint32_t MSH = MREC == 64 ? 6u : 7u;
+        uint32_t gshl[NGI], goff[NGI], gmul[NGI], gmask[NGI], gsel[NGI];
+#pragma unroll
+        for (int i = 0; i < NGI; i++) {
+            const int e = kl + 8 * i;
+            gshl[i] = e < MP ? MSH : 4u;
+            goff[i] = e < MP ? moff + 16u * (uint32_t)e : poff;
+            gmul[i] = e < MP ? MREC : 16u;
+            gmask[i] = e < MP ? COOP_CHK_MASK : 0xFFFFu;
+            gsel[i] = (uint32_t)(e < MP ? GG::W_META : GG::W_O);
+        }
+        // stores, instruction i: lane (kl, q) of slot 8w + kl, piece c = q + 8 i:
+        // c < MP message piece c, c = MP the x-edge parity row, c = MP + 1 the
+        // tail's last edge, the rest the sink row
+        uint32_t sshl[NSI], soff[NSI], smul[NSI], stw[NSI], stm[NSI], snk[NSI], snk_tl[NSI];
+        int qp[NSI];   // lane q's piece of a slot's outputs (c > MP + 1: any, to the sink)
+#pragma unroll
+        for (int i = 0; i < NSI; i++) {
+            const int c = q + 8 * i;
+            sshl[i] = c < MP ? MSH : 4u;
+            soff[i] = c < MP ? moff + 16u * (uint32_t)c : poff;
+            smul[i] = c < MP ? MREC : 16u;
+            stw[i] = 4u * (uint32_t)(c < MP ? GG::W_META : c == MP ? GG::W_X : GG::W_O);
+            stm[i] = c < MP ? COOP_CHK_MASK : 0xFFFFu;
+            snk[i] = c >= MP + 1 ? 0xFFFFFFFFu : 0u;
+            snk_tl[i] = c >= MP + 2 ? 0xFFFFFFFFu : 0u;
+            qp[i] = c < MP + 1 ? c : MP + 1;
+        }
+        auto goffs = [&](int i, uint32_t idx) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (MSHIFT) return (idx << gshl[i]) + goff[i];
+            else return idx * gmul[i] + goff[i];
         };
-        auto soffs = [&](uint32_t idx) __attribute__((always_inline)) -> uint32_t {
-            if constexpr (MREC == 64) return (idx << sshl) + soff;
-            else return idx * smul + soff;
+        auto soffs = [&](int i, uint32_t idx) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (MSHIFT) return (idx << sshl[i]) + soff[i];
+            else return idx * smul[i] + soff[i];
+        };
+        // the LDS-DMA of gather instruction i (lanes past piece MP inactive)
+        auto dma_in = [&](int i, uint32_t idx, int w, int ib) __attribute__((always_inline)) {
+            if (lane + 64 * i < 8 * GG::NG)
+                dma16_buf(vr, goffs(i, idx), (uint32_t)(uintptr_t)&sm.in[w][ib] + 1024u * (uint32_t)i);
         };
         auto gather = [&](int w, int g, int ib) __attribute__((always_inline)) {
-            const uint32_t idx = sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
-            if (lane < 8 * GG::NG) dma16_buf(vr, goffs(idx), (uint32_t)(uintptr_t)&sm.in[w][ib]);
+#pragma unroll
+            for (int i = 0; i < NGI; i++) dma_in(i, sm.tab[g & (TQ - 1)][8 * w + (lane & 7)][gsel[i]] & gmask[i], w, ib);
         };
         // the store of window g's slots 8w .. 8w+7: its row / check index, read
         // from window g's records one period before the store (the chain wave
         // restages that table slot in the store's period); tl: the tail window,
         // !live: the sink
-        auto store_idx = [&](int w, int g, bool tl, bool live) __attribute__((always_inline)) -> uint32_t {
-            const uint32_t rw = *(const uint32_t *)((const char *)&sm.tab[g & (TQ - 1)][8 * w + kl][0] + stw) & stm;
-            return live ? bfi(tl ? snk_tl : snk, (uint32_t)a.m, rw) : (uint32_t)a.m;
+        auto store_idx = [&](int i, int w, int g, bool tl, bool live) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t rw = *(const uint32_t *)((const char *)&sm.tab[g & (TQ - 1)][8 * w + kl][0] + stw[i]) & stm[i];
+            return live ? bfi(tl ? snk_tl[i] : snk[i], (uint32_t)a.m, rw) : (uint32_t)a.m;
         };
-        const int qp = q < MP + 1 ? q : MP + 1;   // lane q's piece of a slot's outputs (q > MP + 1: any, to the sink)
-        auto store_win = [&](int w, int g, uint32_t idx) __attribute__((always_inline)) {
-            rbuf_store_v4(__builtin_bit_cast(i32x4, sm.mst[g & 1][w][kl][qp]), vr, (int)soffs(idx), 0, 0);
+        auto store_win = [&](int i, int w, int g, uint32_t idx) __attribute__((always_inline)) {
+            rbuf_store_v4(__builtin_bit_cast(i32x4, sm.mst[g & 1][w][kl][qp[i]]), vr, (int)soffs(i, idx), 0, 0);
         };
         for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
             __syncthreads();   // prologue 1: tables and resident lines in LDS
@@ -1018,11 +1066,12 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 #pragma unroll
                     for (int l = 0; l < NLD; l++) pend[i][w][l] = make_uint4(0, 0, 0, 0);
             int uS = a.nw - 1;   // local index of window p-1 (the next period's stores)
-            uint32_t sidx[WS];   // the stores' indices (window p-2), read in period p-1
+            uint32_t sidx[WS][NSI];   // the stores' indices (window p-2), read in period p-1
             uint4 lop[WS][NLD];  // the line ops of period p (byte offsets, record words W_LOP ..), read in period p-1
 #pragma unroll
             for (int w = 0; w < WS; w++) {
-                sidx[w] = (uint32_t)a.m;
+#pragma unroll
+                for (int i = 0; i < NSI; i++) sidx[w][i] = (uint32_t)a.m;
 #pragma unroll
                 for (int l = 0; l < NLD; l++) lop[w][l] = *(const uint4 *)&sm.tab[0][8 * w + kl][GG::W_LOP + 4 * l];
             }
@@ -1042,8 +1091,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
                 constexpr int s = decltype(sc_)::value;   // p % NPD
                 if (STAMP) tx = stampL();
-                uint32_t gix[WS];
-                uint4 wbd[WS][NLD], std_[WS];
+                uint32_t gix[WS][NGI];
+                uint4 wbd[WS][NLD], std_[WS][NSI];
                 auto loads = [&]() __attribute__((always_inline)) {   // line loads of period p
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
@@ -1056,7 +1105,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 auto read_gix = [&]() __attribute__((always_inline)) {   // gather indices of window p+1+R
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
-                        gix[w] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + (lane & 7)][gsel] & gmask;
+#pragma unroll
+                        for (int i = 0; i < NGI; i++)
+                            gix[w][i] = sm.tab[(p + 1 + R) & (TQ - 1)][8 * w + (lane & 7)][gsel[i]] & gmask[i];
                     });
                 };
                 auto read_out = [&]() __attribute__((always_inline)) {   // writeback and store data
@@ -1064,12 +1115,13 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                         constexpr int w = decltype(wc)::value;
 #ifdef C3X_BANK_MEM
                         wbd[w][0] = *(const uint4 *)(lcb + 16 * lane);
-                        std_[w] = *(const uint4 *)((const char *)&sm.mst[(p - 2) & 1][w][0][0] + 16 * (lane & 31));
+                        std_[w][0] = *(const uint4 *)((const char *)&sm.mst[(p - 2) & 1][w][0][0] + 16 * (lane & 31));
 #else
 #pragma unroll
                         for (int l = 0; l < NLD; l++)
                             wbd[w][l] = *(const uint4 *)(lcb + (lop[w][l].w ^ lq));   // row q of the swizzled slot
-                        std_[w] = sm.mst[(p - 2) & 1][w][kl][qp];
+#pragma unroll
+                        for (int i = 0; i < NSI; i++) std_[w][i] = sm.mst[(p - 2) & 1][w][kl][qp[i]];
 #endif
                     });
                 };
@@ -1084,7 +1136,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
 #ifndef C3X_BANK_NODMA
-                        if (lane < 8 * GG::NG) dma16_buf(vr, goffs(gix[w]), (uint32_t)(uintptr_t)&sm.in[w][(p + 1 + R) % NI]);
+#pragma unroll
+                        for (int i = 0; i < NGI; i++) dma_in(i, gix[w][i], w, (p + 1 + R) % NI);
 #endif
                     });
                 };
@@ -1107,19 +1160,22 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 });
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // stores of window p-2 (sink before period 2)
                     constexpr int w = decltype(wc)::value;
-                    rbuf_store_v4(__builtin_bit_cast(i32x4, std_[w]), vr, (int)soffs(sidx[w]), 0, 0);
+#pragma unroll
+                    for (int i = 0; i < NSI; i++)
+                        rbuf_store_v4(__builtin_bit_cast(i32x4, std_[w][i]), vr, (int)soffs(i, sidx[w][i]), 0, 0);
                 });
                 // the indices of window p-1's stores and of the next period's line ops
                 static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
-                    sidx[w] = store_idx(w, p - 1, uS == a.tail, p >= 1);
+#pragma unroll
+                    for (int i = 0; i < NSI; i++) sidx[w][i] = store_idx(i, w, p - 1, uS == a.tail, p >= 1);
 #pragma unroll
                     for (int l = 0; l < NLD; l++)
                         lop[w][l] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][GG::W_LOP + 4 * l];
                 });
                 if (STAMP) sP[1] += stampL() - tx;
-                // the gathers of p-1: (NLD + 1) WS ops of p-1 and (2 NLD + 2) WS of p after them
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((3 * NLD + 3) * WS) : "memory");
+                // the gathers of p-1: (NLD + NSI) WS ops of p-1 and (2 NLD + NGI + NSI) WS of p after them
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((3 * NLD + NGI + 2 * NSI) * WS) : "memory");
                 if (STAMP) sA += stampL() - tx;
                 __syncthreads();
                 uS = (uS + 1 == a.nw) ? 0 : uS + 1;
@@ -1135,7 +1191,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             });
             // the stores of window G-1 (its post ran in period G)
             static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
-                store_win(decltype(wc)::value, G - 1, sidx[decltype(wc)::value]);
+#pragma unroll
+                for (int i = 0; i < NSI; i++) store_win(i, decltype(wc)::value, G - 1, sidx[decltype(wc)::value][i]);
             });
             __syncthreads();   // epilogue (the slab waves write the resident dirty lines back)
             if (!ET || !et_after(it)) break;
@@ -1153,7 +1210,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
-    constexpr bool LEAN = ET && GG::X > 8;
+    constexpr bool LEAN = (ET && GG::X > 8) || GG::X > 16;
     Slab3<D0, WS, R, NMS, LEAN> sl{sm,
                     a,
                     8 * sw + kl,
@@ -1414,32 +1471,40 @@ int launch_any(int d0, const Coop3Args &a, int grid, bool et, bool nms, bool sta
     case 7: return launch_d0<7>(a, grid, et, nms, stamped, s);
     case 10: return launch_d0<10>(a, grid, et, nms, stamped, s);
     case 14: return launch_d0<14>(a, grid, et, nms, stamped, s);
+    case 22: return launch_d0<22>(a, grid, et, nms, stamped, s);
+    case 27: return launch_d0<27>(a, grid, et, nms, stamped, s);
+    case 30: return launch_d0<30>(a, grid, et, nms, stamped, s);
     default: return -1;
     }
 }
 
-// per-degree constants at run time (first-group degrees 7, 10, 14)
+// per-degree constants at run time (first-group degrees 7, 10, 14, 22, 27, 30)
 template <template <int> class F>
 auto g3_at(int d0) -> decltype(F<7>::v)
 {
-    return d0 == 7 ? F<7>::v : d0 == 10 ? F<10>::v : F<14>::v;
+    return d0 == 7 ? F<7>::v : d0 == 10 ? F<10>::v : d0 == 14 ? F<14>::v : d0 == 22 ? F<22>::v : d0 == 27 ? F<27>::v
+                                                                                                             : F<30>::v;
 }
 template <int D> struct RecwOf { static constexpr int v = G3<D>::RECW; };
 template <int D> struct WsOf { static constexpr int v = G3<D>::WS; };
 template <int D> struct LcsOf { static constexpr int v = G3<D>::LCS; };
 template <int D> struct SmemOf { static constexpr size_t v = sizeof(Smem3<D, G3<D>::WS, 2>); };
+template <int D> struct DistOf { static constexpr int v = G3<D>::DIST; };
 int g3_recw(int d0) { return g3_at<RecwOf>(d0); }
 int g3_ws(int d0) { return g3_at<WsOf>(d0); }
 size_t g3_smem(int d0) { return g3_at<SmemOf>(d0); }
-bool g3_degree_ok(int d0) { return d0 == 7 || d0 == 10 || d0 == 14; }
-static_assert(SmemOf<7>::v + 512 <= 160 * 1024 && SmemOf<10>::v + 512 <= 160 * 1024 && SmemOf<14>::v + 512 <= 160 * 1024,
+int g3_dist(int d0) { return g3_at<DistOf>(d0); }
+bool g3_degree_ok(int d0) { return d0 == 7 || d0 == 10 || d0 == 14 || d0 == 22 || d0 == 27 || d0 == 30; }
+static_assert(SmemOf<7>::v + 512 <= 160 * 1024 && SmemOf<10>::v + 512 <= 160 * 1024 && SmemOf<14>::v + 512 <= 160 * 1024 &&
+                  SmemOf<22>::v + 512 <= 160 * 1024 && SmemOf<27>::v + 512 <= 160 * 1024 &&
+                  SmemOf<30>::v + 512 <= 160 * 1024,
               "LDS: the workgroup's Smem3 plus the ET kernel's static words fit 160 KB");
 int g3_lcs(int d0) { return g3_at<LcsOf>(d0); }
 
 }  // namespace
 
 // message bytes per check and 16-codeword group (G3::MREC): 64 for first-group
-// degree <= 8, 96 up to 16
+// degree <= 8, 96 up to 16, 128 up to 24, 160 up to 32
 int coop3_mrec(int d0) { return 32 * ((d0 + 7) / 8 + 1); }
 
 // OMS / MS as coop (coop_params_ok); NMS with factor <= 64 (msg_max <= 63: the
@@ -1468,13 +1533,14 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
     if (ws != g3_ws(D0) || r != 2)
         return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be %d for first-group degree %d, LDPC_COOP3_R 2",
                               g3_ws(D0), D0);
-    const int S = 8 * ws;
+    const int S = 8 * ws, dist = g3_dist(D0);
     CoopPlan &pl = o.pl;
     // dist 1: neighbouring windows share no information variable; the plan's
     // forwarding codes mark the reads of values written 2 .. r+3 windows
     // earlier, of which distance 2 (writer's post and reader's pre in the same
-    // period) puts writer and reader in slab wave 0
-    if (coop_build_plan(h, S, r + 2, 1, RECW, pl, true) != 0) return 1;
+    // period) puts writer and reader in slab wave 0.  dist 2 (WS = 2): windows
+    // u and u+2 share none either, so no pair needs a slot of its own
+    if (coop_build_plan(h, S, r + 2, dist, RECW, pl, true) != 0) return 1;
     const int nw = (int)pl.first.size();
     auto rec_at = [&](int u, int k) { return &pl.tab[((size_t)u * S + k) * RECW]; };
     auto code_at = [&](const uint32_t *rec, int j) { return (rec[D0 + 1 + j / 2] >> (16 * (j & 1))) & 0xFFFFu; };
@@ -1487,7 +1553,7 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
                 const uint32_t f = code_at(rec_at(u, k), j);
                 // forwarding code: dW << (6 + EB) | slot << EB | edge (coop.h; EB = 5 above 8 info edges)
                 const int EB = coop_fwd_eb(X);
-                if (f == COOP_FWD_NONE || (int)(f >> (6 + EB)) != 2) continue;
+                if (dist != 1 || f == COOP_FWD_NONE || (int)(f >> (6 + EB)) != 2) continue;
                 special[(size_t)u * S + k] = 1;
                 special[(size_t)((u + nw - 2) % nw) * S + ((f >> EB) & 63)] = 1;
             }
@@ -1537,7 +1603,7 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
                         const uint32_t v = rec[j];
                         if (pass == 1 && wu[v] >= 0) {
                             const int d = (u - wu[v] + nw) % nw;
-                            if (d == 1 || (d == 0 && nw > 1 && wk[v] != k))
+                            if ((d >= 1 && d <= dist) || (d == 0 && nw > 1 && wk[v] != k))
                                 return ldpc_set_error(LDPC_EINVAL, "coop3 plan: variable %u in windows %d and %d", v,
                                                       wu[v], u);
                             if (d == 2 && (k >= 8 || wk[v] >= 8))
@@ -1721,11 +1787,11 @@ __global__ void et_gather_k(const char *Vs, char *Vd, const int32_t *map, const 
                 }
             *(uint4 *)(d + (size_t)r * 16) = make_uint4(w[0], w[1], w[2], w[3]);
         } else {   // message record of check c: pair q's (MA0, MB) words, codeword 2q + h in half h of each,
-                   // then (mrec 96) the pairs' MA1 words
-            const int c = r - vrows;
-            uint32_t w[24];
+                   // then (mrec > 64) the pairs' MA1, MA2, .. words (8 each)
+            const int c = r - vrows, nw = mrec / 4;   // <= 40 words
+            uint32_t w[40];
 #pragma unroll
-            for (int i = 0; i < 24; i++) w[i] = 0;
+            for (int i = 0; i < 40; i++) w[i] = 0;
 #pragma unroll
             for (int i = 0; i < 16; i++)
                 if (src[i] >= 0) {
@@ -1734,15 +1800,15 @@ __global__ void et_gather_k(const char *Vs, char *Vd, const int32_t *map, const 
                     const uint32_t ma = ((const uint16_t *)(rec + 8 * qs))[hs], mb = ((const uint16_t *)(rec + 8 * qs + 4))[hs];
                     w[2 * qd] |= ma << (16 * hd);
                     w[2 * qd + 1] |= mb << (16 * hd);
-                    if (mrec > 64) w[16 + qd] |= (uint32_t)((const uint16_t *)(rec + 64 + 4 * qs))[hs] << (16 * hd);
+#pragma unroll
+                    for (int k = 1; k < 4; k++)
+                        if (64 + 32 * k <= mrec)
+                            w[8 + 8 * k + qd] |= (uint32_t)((const uint16_t *)(rec + 32 + 32 * k + 4 * qs))[hs] << (16 * hd);
                 }
             uint4 *o = (uint4 *)(d + vpart + (size_t)c * mrec);
 #pragma unroll
-            for (int k = 0; k < 4; k++) o[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-            if (mrec > 64) {
-                o[4] = make_uint4(w[16], w[17], w[18], w[19]);
-                o[5] = make_uint4(w[20], w[21], w[22], w[23]);
-            }
+            for (int k = 0; k < 10; k++)
+                if (4 * k < nw) o[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
         }
     }
 }
@@ -1890,7 +1956,9 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     }
     rc = launch_any(cc.d0, a, grid, et, nms, stamped, s);
     if (stamped) {
-        if (rc == 0) (cc.d0 == 7 ? report_stamps3<G3<7>::WS> : report_stamps3<G3<10>::WS>)(a.stamps, grid, s);
+        if (rc == 0)
+            (g3_ws(cc.d0) == 6 ? report_stamps3<6> : g3_ws(cc.d0) == 4 ? report_stamps3<4> : report_stamps3<2>)(a.stamps,
+                                                                                                            grid, s);
         (void)hipFree(a.stamps);
     }
     return rc;

@@ -347,94 +347,129 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     }
     // still too many: empty the least-used slots by moving each of their holds
     // into a gap of another slot (holds are cyclic arcs [tl + LC_PUT, tw]; one
-    // slot's arcs must not overlap), most-used targets first, until no slot
-    // can be emptied (the greedy cut above wastes slots near the cut)
+    // slot's arcs must not overlap), fullest targets first, or -- where no gap
+    // fits -- into a slot whose only hold in the way moves to a gap elsewhere
+    // (one ejection), until no slot can be emptied (the greedy cut above
+    // wastes slots near the cut)
     if (used + 1 > max_slots) {
-        // per slot: its residencies and a bitmap of the periods its holds occupy
-        const int NWD = (nw + 63) / 64;
-        std::vector<std::vector<int>> of(used + 1);
-        std::vector<std::vector<uint64_t>> occ(used + 1, std::vector<uint64_t>(NWD, 0));
-        auto span = [&](int i, auto &&f) {   // f(word, mask) over the periods of residency i's hold
+        const int NS1 = used + 1, NWB = (NS1 + 63) / 64;   // slots 1 .. used
+        std::vector<int> own((size_t)NS1 * nw, -1);          // residency holding slot t in period p
+        std::vector<uint64_t> freeb((size_t)nw * NWB, 0);    // per period: the slots free in it
+        std::vector<std::vector<int>> of(NS1);
+        for (int p = 0; p < nw; p++)
+            for (int t = 1; t < NS1; t++) freeb[(size_t)p * NWB + t / 64] |= 1ull << (t % 64);
+        auto span = [&](int i, auto &&f) {   // f(period) over residency i's hold
             const Res &R = rs[i];
             if (R.whole) {
-                for (int w = 0; w < NWD; w++) f(w, ~0ull);
+                for (int p = 0; p < nw; p++) f(p);
                 return;
             }
             const int a0 = cmod(R.tl + LC_PUT, nw), len = R.tw - (R.tl + LC_PUT);
-            for (int p = 0; p <= len; p++) {
-                const int q = (a0 + p) % nw;
-                f(q >> 6, 1ull << (q & 63));
-            }
+            for (int q = 0; q <= len; q++) f((a0 + q) % nw);
         };
-        auto fits = [&](int i, int t) {
-            bool ok = true;
-            span(i, [&](int w, uint64_t m) { ok = ok && !(occ[t][w] & m); });
-            return ok;
+        auto place = [&](int i, int t) {
+            span(i, [&](int p) {
+                own[(size_t)t * nw + p] = i;
+                freeb[(size_t)p * NWB + t / 64] &= ~(1ull << (t % 64));
+            });
+            rs[i].slot = t;
+            of[t].push_back(i);
         };
-        auto put = [&](int i, int t, bool set) {
-            span(i, [&](int w, uint64_t m) { occ[t][w] = set ? (occ[t][w] | m) : (occ[t][w] & ~m); });
+        auto unplace = [&](int i) {
+            const int t = rs[i].slot;
+            span(i, [&](int p) {
+                own[(size_t)t * nw + p] = -1;
+                freeb[(size_t)p * NWB + t / 64] |= 1ull << (t % 64);
+            });
+            of[t].erase(std::find(of[t].begin(), of[t].end(), i));
         };
-        for (int i = 0; i < (int)rs.size(); i++) {
-            of[rs[i].slot].push_back(i);
-            put(i, rs[i].slot, true);
+        // the fullest slot free over residency i's whole hold, other than x1 / x2; -1: none
+        std::vector<uint64_t> m(NWB);
+        auto home = [&](int i, int x1, int x2) -> int {
+            std::fill(m.begin(), m.end(), ~0ull);
+            span(i, [&](int p) {
+                for (int w = 0; w < NWB; w++) m[w] &= freeb[(size_t)p * NWB + w];
+            });
+            int best = -1;
+            for (int w = 0; w < NWB; w++)
+                for (uint64_t b = m[w]; b; b &= b - 1) {
+                    const int t = w * 64 + __builtin_ctzll(b);
+                    if (t == x1 || t == x2 || of[t].empty()) continue;
+                    if (best < 0 || of[t].size() > of[best].size()) best = t;
+                }
+            return best;
+        };
+        {
+            std::vector<int> tmp(rs.size());
+            for (int i = 0; i < (int)rs.size(); i++) tmp[i] = rs[i].slot;
+            for (int i = 0; i < (int)rs.size(); i++) place(i, tmp[i]);
         }
         for (bool progress = true; progress && used + 1 > max_slots;) {
             progress = false;
             std::vector<int> order;
-            for (int s2 = 1; s2 <= used; s2++)
+            for (int s2 = 1; s2 < NS1; s2++)
                 if (!of[s2].empty()) order.push_back(s2);
             std::sort(order.begin(), order.end(), [&](int x, int y) { return of[x].size() < of[y].size(); });
             for (int s2 : order) {
                 if (of[s2].empty() || used + 1 <= max_slots) continue;
-                // a home for every hold of slot s2 (the fullest slot it fits), or none moves
-                std::vector<std::pair<int, int>> moves;
+                std::vector<std::pair<int, int>> moves;   // (residency, slot it came from), for the rollback
                 bool ok = true;
-                for (int i : of[s2]) {
-                    int home = -1;
-                    for (int k = (int)order.size() - 1; k >= 0; k--) {   // fullest first
-                        const int t = order[k];
-                        if (t != s2 && !of[t].empty() && fits(i, t)) {
-                            home = t;
-                            break;
-                        }
+                const std::vector<int> holds = of[s2];
+                for (int i : holds) {
+                    int t = home(i, s2, -1);
+                    if (t >= 0) {
+                        unplace(i);
+                        place(i, t);
+                        moves.push_back({i, s2});
+                        continue;
                     }
-                    if (home < 0) {
+                    // one ejection: a slot where a single hold j is in the way and j fits elsewhere
+                    bool done = false;
+                    for (int t1 = 1; t1 < NS1 && !done; t1++) {
+                        if (t1 == s2 || of[t1].empty()) continue;
+                        int j = -1;
+                        bool single = true;
+                        span(i, [&](int p) {
+                            const int o2 = own[(size_t)t1 * nw + p];
+                            if (o2 >= 0 && o2 != j) {
+                                if (j >= 0) single = false;
+                                j = o2;
+                            }
+                        });
+                        if (!single || j < 0 || rs[j].whole) continue;
+                        const int t2 = home(j, s2, t1);
+                        if (t2 < 0) continue;
+                        unplace(j);
+                        place(j, t2);
+                        moves.push_back({j, t1});
+                        unplace(i);
+                        place(i, t1);
+                        moves.push_back({i, s2});
+                        done = true;
+                    }
+                    if (!done) {
                         ok = false;
                         break;
                     }
-                    put(i, home, true);
-                    moves.push_back({i, home});
                 }
                 if (!ok) {
-                    for (auto &mv : moves) put(mv.first, mv.second, false);
+                    for (auto it = moves.rbegin(); it != moves.rend(); ++it) {
+                        unplace(it->first);
+                        place(it->first, it->second);
+                    }
                     continue;
                 }
-                for (auto &mv : moves) {
-                    rs[mv.first].slot = mv.second;
-                    of[mv.second].push_back(mv.first);
-                }
-                of[s2].clear();
-                std::fill(occ[s2].begin(), occ[s2].end(), 0);
-                used--;   // (renumbered below)
+                used--;
                 progress = true;
             }
-            // renumber the slots in use densely (1 ..)
-            std::vector<int> ren(of.size(), 0);
-            int n2 = 0;
-            for (int s2 = 1; s2 < (int)of.size(); s2++)
-                if (!of[s2].empty()) ren[s2] = ++n2;
-            std::vector<std::vector<int>> of2(n2 + 1);
-            std::vector<std::vector<uint64_t>> occ2(n2 + 1);
-            for (int s2 = 1; s2 < (int)of.size(); s2++)
-                if (ren[s2]) occ2[ren[s2]].swap(occ[s2]);
-            for (int i = 0; i < (int)rs.size(); i++) {
-                rs[i].slot = ren[rs[i].slot];
-                of2[rs[i].slot].push_back(i);
-            }
-            of.swap(of2);
-            occ.swap(occ2);
-            used = n2;
         }
+        // renumber the slots in use densely (1 ..)
+        std::vector<int> ren(NS1, 0);
+        int n2 = 0;
+        for (int s2 = 1; s2 < NS1; s2++)
+            if (!of[s2].empty()) ren[s2] = ++n2;
+        for (Res &R : rs) R.slot = ren[R.slot];
+        used = n2;
     }
     o.slots = used + 1;
     o.residencies = (int)rs.size();

@@ -4,9 +4,10 @@ the coop kernel (5) with its XCD block remap on.
 bench.py --mixed decodes ONE 4096-codeword batch per GPU mixing DVB-S2 r1/2
 and the DVB-S2-shaped r3/4, r5/6 (codeword c has rate c % 3: 1366 / 1365 /
 1365 codewords), each rate at its own Eb/N0, 50 iterations at most, early
-termination on.  The per-rate sub-batches run coop3 (r1/2 at first-group
-degree 7, the shaped r3/4 at degree 14) and coop at grid 88 (the shaped
-r5/6, degree 22) -- grid % 8 == 0, so the XCD-aware workgroup remap is ON; the tests here check exactly those launches against the oracle's
+termination on.  The per-rate sub-batches run coop3 at grid 88 (r1/2 at
+first-group degree 7, the shaped r3/4 at degree 14, the shaped r5/6 at degree
+22) -- grid % 8 == 0, so the XCD-aware workgroup remap is ON; the tests here
+check exactly those launches (and the coop kernel's, forced) against the oracle's
 early-termination semantics (syndrome after every iteration; the reference's
 commented `arret` test, code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:551-553,
 as restated in oracle/ldpc_oracle.c; per-check recurrence :172-546).  The
@@ -54,9 +55,9 @@ def test_configs4_mixed_batch_as_benched_vs_oracle():
     """The whole configs[4] step of bench.py --mixed (MIXED_SETS["configs4"],
     MIXED_EBN0, batch 4096, 50 it, early termination, seed 2024): every
     codeword's hard decisions and iterations used equal the oracle's decode
-    under its own code; the kernels that ran are coop3 (r1/2) and coop with
-    the XCD remap on (grid 88 for 1365 / 1366 codewords); the shaped r3/4 on
-    coop3 (degree 14)."""
+    under its own code; every rate ran on coop3 (first-group degree 7, 14 and
+    22: the r5/6 sub-batch on the 2-slab-wave kernel) with the XCD remap on
+    (grid 88 for 1365 / 1366 codewords)."""
     torch = _torch()
     import bench
     from ldpcgputegra_amd.decoder import MixedDecoder
@@ -70,7 +71,7 @@ def test_configs4_mixed_batch_as_benched_vs_oracle():
     torch.cuda.synchronize()
     got_h, got_i, host = hard.cpu().numpy(), its.cpu().numpy(), llr.cpu().numpy()
     kernels = mx.last_kernels()
-    assert kernels == ["coop3", "coop3", "coop"], kernels
+    assert kernels == ["coop3", "coop3", "coop3"], kernels
     thr = O.host_threads()
     for c, name in enumerate(names):
         sel = np.where(ids == c)[0]
@@ -218,7 +219,7 @@ def test_configs4_mixed_staged_vs_oracle():
         got_h, got_i, kernels, stages = _mixed_decode(torch, names, llr, ids, iters)
     finally:
         restore()
-    assert kernels == ["coop3", "coop3", "coop"], kernels
+    assert kernels == ["coop3", "coop3", "coop3"], kernels
     assert stages[0] == 20, stages
     host = llr.cpu().numpy()
     thr = O.host_threads()
@@ -242,7 +243,7 @@ def test_configs4_mixed_staged_batch_as_benched():
     B, iters = 24576, 50
     ids, llr = _bench_mixed_inputs(torch, names, B, 2024, bench.MIXED_EBN0)
     got_h, got_i, kernels, stages = _mixed_decode(torch, names, llr, ids, iters)
-    assert kernels == ["coop3", "coop3", "coop"], kernels
+    assert kernels == ["coop3", "coop3", "coop3"], kernels
     assert stages[0] > 0, stages
     restore = _env(LDPC_COOP3_ET_STAGE_MIN=1 << 30)
     try:

@@ -1,14 +1,21 @@
-"""coop3 at first-group degree 10 (DVB-S2 r2/3, the reference's
-code/gpu_fixed/matrix/64800x21600 table) and 14 (the DVB-S2-shaped r3/4 of
-configs[4]): coop3_decode<10 | 14, 4, 2> -- 4 slab waves (one per SIMD) over
-windows of <= 32 checks, 8 / 12 information edges per check, two 16-bit
+"""coop3 beyond DVB-S2 r1/2: first-group degree 10 (DVB-S2 r2/3, the
+reference's code/gpu_fixed/matrix/64800x21600 table) and 14 (the DVB-S2-shaped
+r3/4 of configs[4]) -- coop3_decode<10 | 14, 4, 2>: 4 slab waves (one per SIMD)
+over windows of <= 32 checks, 8 / 12 information edges per check, two 16-bit
 edge-code words per codeword (96-B message records), 1 / 2 line loads per lane
-group and period -- against the oracle (the reference's recurrence, CDecoder_OMS_fixed_SSE.cpp:
-172-546; NMS CDecoder_NMS_fixed_SSE.cpp:188-240; early termination as the
-commented `arret` test, :551-553).  The reference ships no r2/3 decoder build
-(its x86 tree has no constantes_sse.h for 64800x21600), so the oracle --
-pinned on the 88 reference golden cases -- is the checker: soft output, hard
-decisions and iterations used, bit for bit."""
+group and period -- and first-group degree 22, 27, 30 (the shaped r5/6 of
+configs[4], the reference's r8/9 and r9/10, code/x86/Constantes/64800x7200 /
+64800x6480) -- coop3_decode<22 | 27 | 30, 2, 2>: 2 slab waves over windows of
+16 checks at plan distance 2, 20 / 25 / 28 information edges per check, 3 / 4
+edge-code words (128 / 160-B records), gathers and stores in two instructions
+per slot set, 3 / 4 line loads per lane group and period -- against the oracle
+(the reference's recurrence, CDecoder_OMS_fixed_SSE.cpp:172-546; NMS
+CDecoder_NMS_fixed_SSE.cpp:188-240; early termination as the commented
+`arret` test, :551-553).  The reference ships no r2/3 or shaped decoder build
+(its x86 tree has constantes_sse.h only for 64800x{32400,7200,6480}), so the
+oracle -- pinned on the 88 reference golden cases, which include r8/9 and
+r9/10 and run on coop3 in test_gpu_parity.py -- is the checker: soft output,
+hard decisions and iterations used, bit for bit."""
 import numpy as np
 import pytest
 
@@ -16,8 +23,9 @@ import oracle as O
 from ldpcgputegra_amd import ALGO_NMS, Code, Decoder, channel, default_params, load_table
 
 pytestmark = pytest.mark.gpu
-CODES = ["dvbs2_r2_3", "dvbs2shape_r3_4"]
-EBN0 = {"dvbs2_r2_3": (1.9, 2.3, 1.8, 2.2), "dvbs2shape_r3_4": (2.35, 2.6, 2.3, 2.8)}   # OMS ET, NMS ET, staged, full
+CODES = ["dvbs2_r2_3", "dvbs2shape_r3_4", "dvbs2shape_r5_6", "dvbs2_r8_9", "dvbs2_r9_10"]
+EBN0 = {"dvbs2_r2_3": (1.9, 2.3, 1.8, 2.2), "dvbs2shape_r3_4": (2.35, 2.6, 2.3, 2.8),   # OMS ET, NMS ET, staged, full
+        "dvbs2shape_r5_6": (3.4, 3.3, 3.4, 3.5), "dvbs2_r8_9": (4.3, 4.1, 4.3, 4.6), "dvbs2_r9_10": (4.4, 4.5, 4.4, 5.0)}
 
 
 def _run(CODE, llr, iters, params, batch=None, max_batch=None):
@@ -86,7 +94,7 @@ def test_r23_nms_fixed_vs_oracle(CODE):
 @pytest.mark.parametrize("CODE", CODES)
 def test_r23_staged_early_termination_vs_oracle(CODE, monkeypatch):
     """Staged early termination (compaction of the codewords still decoding
-    into 16-codeword groups, messages in the 96-B record layout), forced at a
+    into 16-codeword groups, messages in the 96 .. 160-B record layouts), forced at a
     small batch: equal to the oracle."""
     t = load_table(CODE)
     B, iters = 200, 30

@@ -2,11 +2,13 @@
 """Build-time guard for coop3's hand-counted `s_waitcnt vmcnt(36)`.
 
 coop3's memory wave (csrc/coop3.hip, `mperiod`) issues, per period, for each of
-the WS slab-wave sets (6 for DVB-S2 r1/2's kernel, 4 for the higher rates'),
-in this order: NLD line loads (all sets), one LDS-DMA gather (`buffer_load_dwordx4
-... lds`, inline asm the compiler does not count), NLD line writebacks and one
-store -- (2 NLD + 2) WS vector-memory instructions, NLD = ceil((D0 - 2) / 8) --
-and closes the period with vmcnt((3 NLD + 3) WS) right before its barrier:
+the WS slab-wave sets (6 for DVB-S2 r1/2's kernel, 4 for r2/3 and the shaped r3/4,
+2 for first-group degrees 22 .. 30), in this order: NLD line loads (all sets),
+NGI LDS-DMA gathers (`buffer_load_dwordx4 ... lds`, inline asm the compiler does
+not count), NLD line writebacks and NSI stores -- (2 NLD + NGI + NSI) WS
+vector-memory instructions, NLD = ceil((D0 - 2) / 8), NGI = NSI = 1 up to
+degree 16, 2 above -- and closes the period with vmcnt((3 NLD + NGI + 2 NSI) WS)
+right before its barrier:
 everything up to the previous period's gathers (and so its line loads) has
 landed.  That count is only right while the compiler emits exactly those 24
 instructions per period (no split, no extra load, no scratch spill).  This
@@ -102,7 +104,10 @@ def counts(name):
     m = WS_NAME.search(name)
     d0, ws = (int(m.group(1)), int(m.group(2))) if m else (7, 6)
     nld = (d0 - 2 + 7) // 8
-    return (2 * nld + 2) * ws, (3 * nld + 3) * ws, "L" * (nld * ws) + "G" * ws + "S" * ((nld + 1) * ws)
+    mp = 2 * ((d0 + 7) // 8 + 1)                            # message pieces per check (G3::MP)
+    ngi, nsi = (8 * (mp + 1) + 63) // 64, (mp + 2 + 7) // 8   # gather / store instructions per 8-slot set
+    return ((2 * nld + ngi + nsi) * ws, (3 * nld + ngi + 2 * nsi) * ws,
+            "L" * (nld * ws) + "G" * (ngi * ws) + "S" * ((nld + nsi) * ws))
 
 
 def check(isa, ops=None, vmcnt=None, min_regions=1, pattern="coop3_decode"):
@@ -161,8 +166,9 @@ def main():
         for e in errs:
             print("check_vmcnt: " + e, file=sys.stderr)
         return 1
-    print("check_vmcnt: ok (%d memory-wave periods checked: (2 NLD + 2) WS vector-memory ops in order, "
-          "vmcnt((3 NLD + 3) WS); degree 7: WS 6, NLD 1; 10: WS 4, NLD 1; 14: WS 4, NLD 2)" % n)
+    print("check_vmcnt: ok (%d memory-wave periods checked: (2 NLD + NGI + NSI) WS vector-memory ops in order, "
+          "vmcnt((3 NLD + NGI + 2 NSI) WS); degree 7: WS 6, NLD 1; 10: WS 4, NLD 1; 14: WS 4, NLD 2; 22: WS 2, "
+          "NLD 3, NGI = NSI = 2; 27, 30: WS 2, NLD 4, NGI = NSI = 2)" % n)
     return 0
 
 
