@@ -156,6 +156,12 @@ struct G3 {
 #ifndef LDPC_C3_BPRIO
 #define LDPC_C3_BPRIO 0
 #endif
+#ifndef LDPC_C3_XO16
+#define LDPC_C3_XO16 0        // experiment: chain inputs in xo as [step][codeword] u16 (a pair's two values in
+                              // one dword: one conflict-free ds_read_b32 per post instead of two ds_read_u16
+                              // 16 B apart) -- the chain's 8 ds_write_b16 per 8 steps instead of one
+                              // ds_write_b128 cost more than the post gains: same box 36.60 vs 34.93 ms (r05n)
+#endif
 #ifndef LDPC_C3_SWROT
 #define LDPC_C3_SWROT 0       // experiment: slab index = (the wave's slab position + SWROT) % WS (same-box
                               // A/B of 3 vs 0: -0.8 % on one box, +0.5 % on another)
@@ -186,9 +192,10 @@ struct alignas(16) Smem3 {
     uint32_t tab[TQ][S][G::RECW];     // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
-    uint4 xo[2][S / 8][CW];           // chain inputs Y, 8 steps x i16 per codeword   (chain -> post; a
-                                      // codeword swizzle c ^ (c >> 3) that removes the 2-way bank conflict of
-                                      // read_x measured 0.3 % slower, r05g)
+    uint4 xo[2][S / 8][CW];           // chain inputs Y (chain -> post): LDPC_C3_XO16 [step][codeword] i16 (a
+                                      // pair's two inputs in one dword), else [block][codeword][8 steps] (a
+                                      // codeword swizzle c ^ (c >> 3) that removed that layout's 2-way bank
+                                      // conflict of read_x measured 0.3 % slower, r05g)
     struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
         uint4 d[G::NG][8];            //   e < MP: message bytes 16e .. 16e+15, e = MP: the o-edge parity row
     } in[WS][NI];                     //   (NGI = 2: the second gather lands pieces 8 .. MP, 1 KB further)
@@ -360,6 +367,10 @@ struct Slab3 {
     }
     LDPC_DEV uint32_t read_x(int g, const St &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
+        if constexpr (LDPC_C3_XO16) {   // codewords 2q, 2q+1 of the step adjacent: one dword
+            const uint32_t d = *(const uint32_t *)((const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 2 * q);
+            return perm(d, d, 0x020d000du);
+        }
         const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 16 * q;
 #ifdef C3X_BANK_X
         const unsigned short *xz = (const unsigned short *)&sm.xo[g & 1][0][0] + 2 * lane;
@@ -634,6 +645,19 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
     const uint4 *cp = &sm.cst[buf][0][c & 1][c >> 1];
     constexpr int KST = 2 * NP;       // uint4 between steps
     uint4 kq[2][8];
+    // the x inputs of steps 8b .. 8b+7 (positions 0..7 of w) -> xo
+    auto put_x = [&](int b, const uint32_t (&v)[4]) __attribute__((always_inline)) {
+        if constexpr (LDPC_C3_XO16) {   // [step][codeword] u16
+            unsigned short *x16 = (unsigned short *)&sm.xo[buf][0][0] + c;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                x16[(8 * b + 2 * i) * CW] = (unsigned short)v[i];
+                x16[(8 * b + 2 * i + 1) * CW] = (unsigned short)(v[i] >> 16);
+            }
+        } else {
+            sm.xo[buf][b][c] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    };
 #pragma unroll
     for (int i = 0; i < 8; i++) kq[B0 & 1][i] = cp[(B0 * 8 + i) * KST];
 #pragma unroll
@@ -651,7 +675,7 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
             C3_STEP_SAME_NMS(w[2], kq[b & 1][4]);
             C3_STEP_CROSS_NMS(w[2], w[3], kq[b & 1][5]);
             C3_STEP_SAME_NMS(w[3], kq[b & 1][6]);
-            sm.xo[buf][b][c] = make_uint4(w[0], w[1], w[2], w[3]);
+            put_x(b, w);
             C3_STEP_CROSS_NMS(w[3], w[0], kq[b & 1][7]);
         } else {
             C3_STEP_SAME(w[0], kq[b & 1][0]);          // pos 0 -> 1
@@ -661,7 +685,7 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
             C3_STEP_SAME(w[2], kq[b & 1][4]);          // 4 -> 5
             C3_STEP_CROSS(w[2], w[3], kq[b & 1][5]);   // 5 -> 6
             C3_STEP_SAME(w[3], kq[b & 1][6]);          // 6 -> 7
-            sm.xo[buf][b][c] = make_uint4(w[0], w[1], w[2], w[3]);
+            put_x(b, w);
             C3_STEP_CROSS(w[3], w[0], kq[b & 1][7]);   // 7 -> 0 (the next block's first input)
         }
     }
@@ -1637,7 +1661,8 @@ static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vec
             uint32_t *rec = &out[((size_t)u * S + kk) * RECW];
             for (int j = 0; j < X; j++) rec[j] = lp.piece[((size_t)u * S + kk) * X + j];
             const uint32_t step = (src[D0] >> STEP_SHIFT) & 63u;   // (rows - k <= m < 65536: checked by coop3_plan_lc)
-            rec[W_X] = (src[X] - (uint32_t)k) | ((step >> 3) * (CW * 8) + (step & 7)) << 16;   // + xo index
+            const uint32_t xi = LDPC_C3_XO16 ? step * CW : (step >> 3) * (CW * 8) + (step & 7);   // xo index (u16)
+            rec[W_X] = (src[X] - (uint32_t)k) | xi << 16;
             rec[W_O] = (src[D0 - 1] - (uint32_t)k) | (step * 2 * NP * 16) << 16;              // + cst offset
             rec[W_META] = src[D0];
             // lane group kk's line ops (LcPlan::ops, S NLD per period: op sub * S + kk)
