@@ -156,6 +156,12 @@ struct G3 {
 #ifndef LDPC_C3_BPRIO
 #define LDPC_C3_BPRIO 0
 #endif
+#ifndef LDPC_C3_PRE_CHUNK_X
+#define LDPC_C3_PRE_CHUNK_X 8    // pres of checks with >= this many info edges: stage-major chunks, two min chains
+#endif
+#ifndef LDPC_C3_POST_CHUNK_X
+#define LDPC_C3_POST_CHUNK_X 8   // posts of checks with >= this many info edges run new_v in stage-major chunks
+#endif
 #ifndef LDPC_C3_XO16
 #define LDPC_C3_XO16 0        // experiment: chain inputs in xo as [step][codeword] u16 (a pair's two values in
                               // one dword: one conflict-free ds_read_b32 per post instead of two ds_read_u16
@@ -357,14 +363,6 @@ struct Slab3 {
         in.wx = rc.w(G::W_X);
         in.wo = rc.w(G::W_O);
     }
-    // LDS byte offset of this lane's pair of info edge j of window g (pre reads, post writes)
-    LDPC_DEV uint32_t ad_of(int g, const St &s, int j) const
-    {
-        if constexpr (G::KEEP_AD)
-            return s.ad[j];
-        else
-            return sm.tab[g & (TQ - 1)][k][j] + lwr;   // window g's records stay in the ring until its stores
-    }
     LDPC_DEV uint32_t read_x(int g, const St &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
         if constexpr (LDPC_C3_XO16) {   // codewords 2q, 2q+1 of the step adjacent: one dword
@@ -405,23 +403,60 @@ struct Slab3 {
             // the info edges' contributions stay unclamped (the saturated
             // 0x8000 below R(-128) included): the post uses only their sign
             // and |c| (abs_sat caps it at R(127) as the reference's clamp does)
-            static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
-                constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_sub_sat(v[J], old_msg2<J>(in.ma, t, K));
-                const uint32_t aj = abs_sat(c, c510);
-                s.c[J] = c;
-                if constexpr (!LEAN) s.a[J] = aj;
-                sacc ^= c;
-                if constexpr (J == 0) {   // a <= R(127): the first edge is min1
-                    min1 = aj;
-                } else if constexpr (J == 1) {
-                    min2 = pk_max(min1, aj);
-                    min1 = pk_min(min1, aj);
-                } else {
-                    min2 = pk_max(min1, pk_min(aj, min2));
-                    min1 = pk_min(min1, aj);
-                }
-            });
+            if constexpr (X < LDPC_C3_PRE_CHUNK_X) {
+                static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int J = decltype(jc)::value;
+                    const uint32_t c = pk_sub_sat(v[J], old_msg2<J>(in.ma, t, K));
+                    const uint32_t aj = abs_sat(c, c510);
+                    s.c[J] = c;
+                    if constexpr (!LEAN) s.a[J] = aj;
+                    sacc ^= c;
+                    if constexpr (J == 0) {   // a <= R(127): the first edge is min1
+                        min1 = aj;
+                    } else if constexpr (J == 1) {
+                        min2 = pk_max(min1, aj);
+                        min1 = pk_min(min1, aj);
+                    } else {
+                        min2 = pk_max(min1, pk_min(aj, min2));
+                        min1 = pk_min(min1, aj);
+                    }
+                });
+            } else {
+                // many info edges: contributions in stage-major chunks (as the
+                // post's new_v) and min1 / min2 as two interleaved chains (even
+                // / odd edges) merged at the end -- the exact smallest and second
+                // smallest of the union, ties included
+                constexpr int PC = 4;
+                uint32_t m1[2] = {R127, R127}, m2[2] = {R127, R127};
+                static_for<0, (X + PC - 1) / PC>([&](auto cc) __attribute__((always_inline)) {
+                    constexpr int J0 = decltype(cc)::value * PC, E = X - J0 < PC ? X - J0 : PC;
+                    uint32_t om[E], aj[E];
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        constexpr int e = decltype(ec)::value;
+                        om[e] = old_msg2<J0 + e>(in.ma, t, K);
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        constexpr int e = decltype(ec)::value;
+                        s.c[J0 + e] = pk_sub_sat(v[J0 + e], om[e]);
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        constexpr int e = decltype(ec)::value;
+                        aj[e] = abs_sat(s.c[J0 + e], c510);
+                        if constexpr (!LEAN) s.a[J0 + e] = aj[e];
+                        sacc ^= s.c[J0 + e];
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        constexpr int e = decltype(ec)::value, h = (J0 + e) & 1;
+                        m2[h] = pk_max(m1[h], pk_min(aj[e], m2[h]));
+                        m1[h] = pk_min(m1[h], aj[e]);
+                    });
+                });
+                min1 = pk_min(m1[0], m1[1]);
+                min2 = pk_min(pk_max(m1[0], m1[1]), pk_min(m2[0], m2[1]));
+            }
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
             const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg2<D0 - 1>(in.ma, t, K)), neg127);
@@ -543,6 +578,18 @@ struct Slab3 {
         auto put = [&](uint32_t ad, uint32_t v) __attribute__((always_inline)) {
             *(unsigned short *)(lcw() + ad) = (unsigned short)v;
         };
+        // !KEEP_AD: the info edges' line-cache offsets from the window's records
+        // (in the ring until its stores), all read here at once (uint4 reads: one
+        // LDS round trip, not one per edge: r05o stamps, degree 30, post 4264 of
+        // a 6777-cycle period with one ds_read_b32 per edge)
+        RecT rp;
+        if constexpr (!G::KEEP_AD) rp = read_rec(g);
+        auto ad_of = [&](int, const St &st, int j) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (G::KEEP_AD)
+                return st.ad[j];
+            else
+                return rp.w(j) + lwr;
+        };
         // edge J's code into MA[J / 8]
         uint32_t MA[G::NMA], MB;
 #pragma unroll
@@ -563,16 +610,57 @@ struct Slab3 {
                                     : pk_max(pk_sub(pk_min(min1, K.rmm), K.coff), 0u);
             uint32_t e1, e2;
             signed_csts(k1, k2, sacc ^ ((D0 & 1) ? SIGNS : 0u), e1, e2);
-            static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+            auto put_new = [&](auto jc, uint32_t n) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
-                const uint32_t aJ = LEAN ? abs_sat(s.c[J], K.c510) : s.a[LEAN ? 0 : J];
-                const uint32_t n = nv(jc, s.c[J], aJ, min1, e1, e2);
                 const uint32_t ad = ad_of(g, s, J);
                 if constexpr (FZ && FZ_REREAD)
                     put(ad, perm(n, *(const unsigned short *)(lcb() + ad), psel_raw));
                 else
                     put(ad, FZ ? perm(n, s.v[FZ_REREAD ? 0 : J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
-            });
+            };
+            if constexpr (X < LDPC_C3_POST_CHUNK_X) {
+                static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int J = decltype(jc)::value;
+                    const uint32_t aJ = LEAN ? abs_sat(s.c[J], K.c510) : s.a[LEAN ? 0 : J];
+                    put_new(jc, nv(jc, s.c[J], aJ, min1, e1, e2));
+                });
+            } else {
+                // 8 .. 28 info edges: new_v in chunks of PC edges, stage by stage
+                // behind scheduling barriers -- left alone the compiler ran the
+                // edges one after another (each a ~14-deep dependent chain: one
+                // wave per SIMD exposes every latency; r05o stamps: the post 2.2x
+                // the pre at degree 30)
+                constexpr int PC = 4;
+                static_for<0, (X + PC - 1) / PC>([&](auto cc) __attribute__((always_inline)) {
+                    constexpr int J0 = decltype(cc)::value * PC, E = X - J0 < PC ? X - J0 : PC;
+                    uint32_t av[E], nq[E], T[E], sc[E];
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        constexpr int e = decltype(ec)::value;
+                        av[e] = LEAN ? abs_sat(s.c[J0 + e], K.c510) : s.a[LEAN ? 0 : J0 + e];
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        constexpr int e = decltype(ec)::value;
+                        nq[e] = opaque(pk_sra15(pk_sub(min1, av[e])));   // -1: the edge gets cst2
+                        sc[e] = opaque(pk_sra15(s.c[J0 + e]));            // -1: c < 0
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        constexpr int e = decltype(ec)::value;
+                        T[e] = pk_add_sat(av[e], bfi(nq[e], e2, e1));   // R(|c| + eps cst), capped at R(127)
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        constexpr int e = decltype(ec)::value, J = J0 + e;
+                        MA[J >> 3] = add_code<J & 7>(MA[J >> 3], sc[e], nq[e]);
+                        T[e] = bfi(sc[e], pk_sub(K.c510, T[e]), T[e]);   // new_v's result
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                    static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
+                        put_new(std::integral_constant<int, J0 + decltype(ec)::value>{}, T[decltype(ec)::value]);
+                    });
+                });
+            }
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
             const uint32_t nx = nv(std::integral_constant<int, X>{}, cx, ax, min1, e1, e2);
@@ -1286,7 +1374,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         St3<D0, LEAN> st[NS];
         __syncthreads();   // prologue 1b: the memory wave's first gathers landed
         PreIn<D0> in;
-        Rec<D0> rcn = sl.read_rec(1 % a.nw);   // records of the next pre's window
+        // records of the next pre's window, read a period ahead (!KEEP_AD: read
+        // by the pre's period itself -- the VGPRs go to the window states)
+        Rec<D0> rcn = sl.read_rec(1 % a.nw);
         sl.read_pre(0, sl.read_rec(0), in);
         if (a.tail == 0)
             sl.template pre<true, ET>(0, in, st[0]);
@@ -1339,9 +1429,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                         t2 = stampL();
                     }
                     sl.template post<false, ET, MP1>(p - 1, xr, sp);
-                    sl.read_pre((s + 1) % NI, rcn, in);
+                    sl.read_pre((s + 1) % NI, GG::KEEP_AD ? rcn : sl.read_rec(p + 1), in);
                 }
-                rcn = sl.read_rec(p + 2);
+                if constexpr (GG::KEEP_AD) rcn = sl.read_rec(p + 2);
                 if (STAMP) t1 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(P1);
                 sl.template pre<false, ET, MP2>(p + 1, in, sn);
@@ -1355,8 +1445,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                         sl.template post<false, ET>(p - 1, xr, sp);
                 }
                 if (STAMP) t1 = t2 = t3 = stampL();
-                if (dpr) sl.read_pre((s + 1) % NI, rcn, in);
-                rcn = sl.read_rec(p + 2);
+                if (dpr) sl.read_pre((s + 1) % NI, GG::KEEP_AD ? rcn : sl.read_rec(p + 1), in);
+                if constexpr (GG::KEEP_AD) rcn = sl.read_rec(p + 2);
                 if (dpr) {
                     if (uB == a.tail)
                         sl.template pre<true, ET>(p + 1, in, sn);
