@@ -156,6 +156,9 @@ struct G3 {
 #ifndef LDPC_C3_BPRIO
 #define LDPC_C3_BPRIO 0
 #endif
+#ifndef LDPC_C3_PREFIRST
+#define LDPC_C3_PREFIRST 1       // plan distance 2 (WS = 2): pre of window p+1 before the post of window p-1
+#endif
 #ifndef LDPC_C3_PRE_CHUNK_X
 #define LDPC_C3_PRE_CHUNK_X 8    // pres of checks with >= this many info edges: stage-major chunks, two min chains
 #endif
@@ -1413,7 +1416,22 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             PreIn<D0> in;
             St3<D0, LEAN> &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
-            if (fast) {
+            if (fast && GG::DIST == 2 && LDPC_C3_PREFIRST) {
+                // plan distance 2 (one slab wave per SIMD): windows p-1 and p+1
+                // share no information variable, so the pre of window p+1 runs
+                // first and hides the wait for the chain's window p-1 outputs the
+                // post needs
+                sl.read_pre((s + 1) % NI, sl.read_rec(p + 1), in);
+                sl.template pre<false, ET>(p + 1, in, sn);
+                if (STAMP) t1 = stampL();
+                const uint32_t xr = sl.read_x(p - 1, sp);
+                if (STAMP) {
+                    asm volatile("" ::"v"(xr));
+                    t2 = stampL();
+                }
+                sl.template post<false, ET>(p - 1, xr, sp);
+                if (STAMP) t3 = stampL();
+            } else if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs), then reads and runs its pre
                 if (fair) {
@@ -1457,7 +1475,11 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             if (STAMP) {
                 const unsigned long long t5 = stampL();
                 sA += t5 - tx;
-                if (fast) {   // x wait, post (+ the pre's read issue), pre
+                if (fast && GG::DIST == 2 && LDPC_C3_PREFIRST) {   // pre first: x wait after it, post, pre
+                    sP[0] += t2 - t1;
+                    sP[1] += t3 - t2;
+                    sP[2] += t1 - tx;
+                } else if (fast) {   // x wait, post (+ the pre's read issue), pre
                     sP[0] += (t2 ? t2 : t1) - tx;
                     sP[1] += t1 - (t2 ? t2 : t1);
                     sP[2] += t3 - t1;
