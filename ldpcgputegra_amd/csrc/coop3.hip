@@ -157,7 +157,12 @@ struct G3 {
 #define LDPC_C3_BPRIO 0
 #endif
 #ifndef LDPC_C3_PREFIRST
-#define LDPC_C3_PREFIRST 1       // plan distance 2 (WS = 2): pre of window p+1 before the post of window p-1
+#define LDPC_C3_PREFIRST 1       // pre of window p+1 before the post of window p-1 in fast periods: 1 = plan
+                                 // distance 2 (WS = 2) kernels, 2 = also slab waves 1 .. of the 4-slab-wave
+                                 // kernels (distance-2 pairs are all in wave 0), 3 = also r1/2's; same box
+                                 // (r05u): 2 vs 1 r2/3 39.48 vs 38.98 ms, r3/4 32.63 vs 32.56, 3: r1/2 36.79
+                                 // vs 35.14 -- a wave that waits for its chain inputs late keeps the partner
+                                 // SIMD's chain / memory wave waiting on the barrier
 #endif
 #ifndef LDPC_C3_PRE_CHUNK_X
 #define LDPC_C3_PRE_CHUNK_X 8    // pres of checks with >= this many info edges: stage-major chunks, two min chains
@@ -1416,12 +1421,17 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             PreIn<D0> in;
             St3<D0, LEAN> &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
-            if (fast && GG::DIST == 2 && LDPC_C3_PREFIRST) {
+            const bool prefirst = fast && (GG::DIST == 2 ? LDPC_C3_PREFIRST >= 1
+                                                         : sw != 0 && LDPC_C3_PREFIRST >= (WS == 4 ? 2 : 3));
+            if (prefirst) {
                 // plan distance 2 (one slab wave per SIMD): windows p-1 and p+1
                 // share no information variable, so the pre of window p+1 runs
                 // first and hides the wait for the chain's window p-1 outputs the
-                // post needs
-                sl.read_pre((s + 1) % NI, sl.read_rec(p + 1), in);
+                // post needs; at distance 1 the same holds for every slab wave
+                // but wave 0 (the plan puts each distance-2 writer / reader pair
+                // there, and wave 0 keeps posting first)
+                sl.read_pre((s + 1) % NI, GG::KEEP_AD ? rcn : sl.read_rec(p + 1), in);
+                if constexpr (GG::KEEP_AD) rcn = sl.read_rec(p + 2);   // (the next period's pre, either order)
                 sl.template pre<false, ET>(p + 1, in, sn);
                 if (STAMP) t1 = stampL();
                 const uint32_t xr = sl.read_x(p - 1, sp);
@@ -1475,7 +1485,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             if (STAMP) {
                 const unsigned long long t5 = stampL();
                 sA += t5 - tx;
-                if (fast && GG::DIST == 2 && LDPC_C3_PREFIRST) {   // pre first: x wait after it, post, pre
+                if (prefirst) {   // pre first: x wait after it, post, pre
                     sP[0] += t2 - t1;
                     sP[1] += t3 - t2;
                     sP[2] += t1 - tx;
