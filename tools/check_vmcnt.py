@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Build-time guard for coop3's hand-counted `s_waitcnt vmcnt(36)`.
 
-coop3's memory wave (csrc/coop3.hip, `mperiod`) issues, per period, for each of
+coop3's memory wave (csrc/coop3_kernel.h, `mperiod`) issues, per period, for each of
 the WS slab-wave sets (6 for DVB-S2 r1/2's kernel, 4 for r2/3 and the shaped r3/4,
 2 for first-group degrees 22 .. 30), in this order: NLD line loads (all sets),
 NGI LDS-DMA gathers (`buffer_load_dwordx4 ... lds`, inline asm the compiler does
