@@ -87,6 +87,35 @@ __global__ void __launch_bounds__(256) interleave_grp_k(const int8_t *__restrict
     }
 }
 
+// the input transpose with 16-B loads on the frame-major side (n % 16 == 0,
+// a 16-B aligned buffer: every DVB-S2 code): one uint4 load per thread
+// instead of 16 byte loads (the byte version ran at 1.6 TB/s: 336 vs 135 us
+// per 4096 DVB-S2 codewords; the same change on the output side measured
+// 122 vs 114 us and was dropped)
+__global__ void __launch_bounds__(256) interleave_grp_vec_k(const int8_t *__restrict__ src, int8_t *__restrict__ dst,
+                                                            int n, int batch, size_t gbytes)
+{
+    __shared__ uint4 tile4[64][4];   // [codeword][16-node chunk]: row-contiguous 64 B
+    const int n0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+    {
+        const int r = threadIdx.x >> 2, c = threadIdx.x & 3, b = b0 + r, i = n0 + 16 * c;
+        tile4[r][c] = (b < batch && i < n) ? *(const uint4 *)(src + (size_t)b * n + i) : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const int8_t(*tile)[64] = (const int8_t(*)[64])&tile4[0][0];
+    const int gq = threadIdx.x >> 6, ni = threadIdx.x & 63;   // group of the tile, node
+    if (n0 + ni < n) {
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            w[d] = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[d] |= (uint32_t)(uint8_t)tile[16 * gq + 4 * d + j][ni] << (8 * j);
+        }
+        *(uint4 *)(dst + (size_t)(b0 / 16 + gq) * gbytes + (size_t)(n0 + ni) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 __global__ void __launch_bounds__(256) deinterleave_grp_k(const int8_t *__restrict__ V, uint8_t *__restrict__ hard,
                                                           int8_t *__restrict__ soft, int n, int batch, size_t gbytes)
 {
@@ -173,7 +202,18 @@ __global__ void __launch_bounds__(64) count_errors_k(const uint8_t *__restrict__
     const uint8_t *h = hard + (size_t)b * n;
     const uint8_t *r = ref ? ref + (size_t)b * n : nullptr;
     int errs = 0;
-    if ((n & 3) == 0 && (k & 3) == 0) {
+    if ((n & 15) == 0 && (k & 15) == 0 && ((uintptr_t)hard & 15) == 0 && ((uintptr_t)ref & 15) == 0) {
+        // 16-B loads, 4 in flight per lane (DVB-S2 r1/2: k = 32400 = 2025 x 16)
+        const uint4 *h16 = (const uint4 *)h, *r16 = (const uint4 *)r;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        auto e16 = [](uint4 a, uint4 q) {
+            return __builtin_popcount((a.x ^ q.x) & 0x01010101u) + __builtin_popcount((a.y ^ q.y) & 0x01010101u) +
+                   __builtin_popcount((a.z ^ q.z) & 0x01010101u) + __builtin_popcount((a.w ^ q.w) & 0x01010101u);
+        };
+        const int m = k / 16;
+#pragma unroll 4
+        for (int i = threadIdx.x; i < m; i += 64) errs += e16(h16[i], r16 ? r16[i] : z);
+    } else if ((n & 3) == 0 && (k & 3) == 0) {
         const uint32_t *h4 = (const uint32_t *)h, *r4 = (const uint32_t *)r;
         for (int i = threadIdx.x; i < k / 4; i += 64)
             errs += __builtin_popcount((h4[i] ^ (r4 ? r4[i] : 0u)) & 0x01010101u);
@@ -271,7 +311,10 @@ int launch_interleave_grp_i8(const int8_t *llr, int8_t *V, int n, int batch, int
                              hipStream_t s)
 {
     dim3 g((n + 63) / 64, (stride + 63) / 64);
-    hipLaunchKernelGGL(interleave_grp_k, g, dim3(256), 0, s, llr, V, n, batch, gbytes);
+    if (n % 16 == 0 && (uintptr_t)llr % 16 == 0)
+        hipLaunchKernelGGL(interleave_grp_vec_k, g, dim3(256), 0, s, llr, V, n, batch, gbytes);
+    else
+        hipLaunchKernelGGL(interleave_grp_k, g, dim3(256), 0, s, llr, V, n, batch, gbytes);
     return ok();
 }
 int launch_deinterleave_grp_i8(const int8_t *V, uint8_t *hard, int8_t *soft, int n, int batch, size_t gbytes,
