@@ -224,54 +224,72 @@ MIXED_EBN0 = {"dvbs2_r1_2": 1.0, "dvbs2_r2_3": 2.2, "dvbs2_r8_9": 4.6, "dvbs2_r9
 
 
 def cpu_baseline_mixed(names, frames, iters, budget_s, threads, seed):
-    """configs[4] on the host: the reference SSE decoder (oracle/_ref) of each
-    rate it can be built for, at FIXED `iters` iterations (code/x86's decoder
-    has no early termination: its arret test is commented out,
-    CDecoder_OMS_fixed_SSE.cpp:551-553), 16-frame decode() calls on `threads`
-    threads, budget_s / len(names) seconds each.  Rates without a reference
-    build (r2/3, the DVB-S2-shaped r3/4 and r5/6) are priced at the measured
-    per-edge cost of the rates that have one (edge counts: 226,799 for r1/2
-    and shaped r3/4, 237,599 for shaped r5/6) -- a stated estimate."""
+    """configs[4] on the host, every rate MEASURED (code/x86/main_p.cpp:664-765's
+    timer mode: the same resident LLRs decoded again and again), at FIXED
+    `iters` iterations (code/x86's decoder has no early termination: its
+    arret test is commented out, CDecoder_OMS_fixed_SSE.cpp:551-553), budget_s
+    / len(names) seconds per rate on `threads` threads:
+    * rates the reference can be built for (oracle/_ref: r1/2, r8/9, r9/10):
+      the reference's own SSE decoder, 16-frame decode() calls (kind
+      "reference");
+    * the others (r2/3, the DVB-S2-shaped r3/4 and r5/6: no constantes_sse.h
+      in code/x86): the product's own host decoder (a device -1 context,
+      csrc/host.cpp, 32-codeword AVX2 blocks; kind "product-host") -- the
+      reference cannot decode them at all.
+    The step's host time = sum over rates of frames / measured rate."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    from ldpcgputegra_amd import channel, load_table
-    per_rate, ns_per_edge = [], []
-    for name in names:
-        if not O.ref_available(name):
-            continue
-        t = load_table(name)
-        blk = 16 * threads
-        llr = channel.awgn_i8_host(t.n, blk, seed, channel.i8_table(channel.sigma_from_ebn0(3.0, t.k_info / t.n)))
-        O.ref_decode_mt(name, llr, iters, 1, threads)   # untimed: library load, first touch, thread start
-        done, t0 = 0, time.perf_counter()
-        while True:
-            O.ref_decode_mt(name, llr, iters, 1, threads)
-            done += blk
-            el = time.perf_counter() - t0
-            if el >= budget_s / len(names):
-                break
-        cw_s = done / el
-        ns_per_edge.append(el / (done * t.e * iters) * 1e9)
-        per_rate.append(dict(code=name, codewords_per_s=round(cw_s, 1), mbps=round(cw_s * t.n / 1e6, 3)))
-    if not per_rate:
-        return None
-    npe = sum(ns_per_edge) / len(ns_per_edge)
-    tot = 0.0
+    from ldpcgputegra_amd import Code, Decoder, channel, load_table
+    per_rate, tot = [], 0.0
+    old_threads = os.environ.get("LDPC_HOST_THREADS")
     for name, f in zip(names, frames):
         t = load_table(name)
-        hit = [r for r in per_rate if r["code"] == name]
-        tot += f / hit[0]["codewords_per_s"] if hit else f * t.e * iters * npe * 1e-9
+        llr_table = channel.i8_table(channel.sigma_from_ebn0(MIXED_EBN0.get(name, 3.0), t.k_info / t.n))
+        budget = budget_s / len(names)
+        if O.ref_available(name):
+            kind, blk = "reference", 16 * threads
+            llr = channel.awgn_i8_host(t.n, blk, seed, llr_table)
+            O.ref_decode_mt(name, llr, iters, 1, threads)   # untimed: library load, first touch, thread start
+            run = lambda: O.ref_decode_mt(name, llr, iters, 1, threads)   # noqa: E731
+            dec = None
+        else:
+            kind, blk = "product-host", 32 * threads
+            os.environ["LDPC_HOST_THREADS"] = str(threads)
+            llr = channel.awgn_i8_host(t.n, blk, seed, llr_table)
+            dec = Decoder(Code(name), device=-1, max_batch=blk)
+            dec.decode_i8(llr[:32], 1)                       # untimed: first touch
+            run = lambda: dec.decode_i8(llr, iters)         # noqa: E731
+        done, t0 = 0, time.perf_counter()
+        while True:
+            run()
+            done += blk
+            el = time.perf_counter() - t0
+            if el >= budget:
+                break
+        if dec is not None:
+            dec.close()
+        cw_s = done / el
+        tot += f / cw_s
+        per_rate.append(dict(code=name, kind=kind, codewords_per_s=round(cw_s, 1), mbps=round(cw_s * t.n / 1e6, 3),
+                             sample="%d codewords in %.2f s" % (done, el)))
+    if old_threads is None:
+        os.environ.pop("LDPC_HOST_THREADS", None)
+    else:
+        os.environ["LDPC_HOST_THREADS"] = old_threads
     host = host_cpu_info()
     n = load_table(names[0]).n
-    return dict(value=round(sum(frames) * n / tot / 1e6, 3), unit="Mbit/s", cores=threads, kind="reference",
+    kinds = sorted({r["kind"] for r in per_rate})
+    return dict(value=round(sum(frames) * n / tot / 1e6, 3), unit="Mbit/s", cores=threads,
+                kind="reference" if kinds == ["reference"] else "port", kinds=kinds,
                 threads=threads, cpu_model=host["model"], host_physical_cores=host["physical_cores"],
                 cpu_quota=host["cpu_quota"], per_rate=per_rate,
-                sample="reference SSE decoder at fixed %d iterations (no early termination in code/x86), 16-frame "
-                       "decode() calls on %d threads, ~%.0f s per rate with a build (%s); rates without one (%s) "
-                       "priced at the measured %.4f ns of %d-thread wall time per edge-iteration (estimate)" % (
-                           iters, threads, budget_s / len(names), ", ".join(r["code"] for r in per_rate),
-                           ", ".join(x for x in names if x not in [r["code"] for r in per_rate]) or "none", npe,
-                           threads))
+                sample="every rate measured at fixed %d iterations (no early termination in code/x86) on %d threads, "
+                       "~%.1f s per rate: the reference SSE decoder (16-frame decode() calls) for %s; the product's "
+                       "host decoder (device -1 context, 32-codeword blocks) for %s, which code/x86 has no table for; "
+                       "step host time = sum of frames / measured rate" % (
+                           iters, threads, budget_s / len(names),
+                           ", ".join(r["code"] for r in per_rate if r["kind"] == "reference") or "none",
+                           ", ".join(r["code"] for r in per_rate if r["kind"] != "reference") or "none"))
 
 
 def bench_mixed(a, rank, world, local, torch, dist):
@@ -284,21 +302,25 @@ def bench_mixed(a, rank, world, local, torch, dist):
     import numpy as np
     from ldpcgputegra_amd import Code, channel, default_params
     from ldpcgputegra_amd.decoder import Decoder, MixedDecoder
-    from ldpcgputegra_amd.shard import reduce_results, shard_range
+    from ldpcgputegra_amd.shard import mixed_layout, reduce_results, reduce_sums
     B = a.batch
     names = MIXED_SETS[a.mixed_codes]
     codes = [Code(n) for n in names]
     N = codes[0].n
     mx = MixedDecoder(codes, device=local, max_batch=B)
-    ids = np.arange(B, dtype=np.int32) % len(codes)
-    first_cw, _ = shard_range(rank, world, B * world)
+    # global codeword g = rank * B + i has rate g % len(codes); rate c's noise
+    # indices are disjoint across ranks and rates (shard.mixed_layout), so N
+    # ranks decode exactly the codewords one process decodes at batch N * B
+    ids, noise_first = mixed_layout(rank, world, B, len(codes))
     llr = torch.empty((B, N), dtype=torch.int8, device="cuda")
     for c, code in enumerate(codes):      # all-zero codeword per rate (CFakeEncoder), own channel
         sel = torch.from_numpy(np.where(ids == c)[0]).cuda()
+        if sel.numel() == 0:
+            continue
         tmp = torch.empty((sel.numel(), N), dtype=torch.int8, device="cuda")
         gen = Decoder(code, device=local, max_batch=max(1, sel.numel()))
         table = channel.i8_table(channel.sigma_from_ebn0(MIXED_EBN0[code.name], code.k_info / code.n), 8, 31)
-        gen.awgn_i8_device(tmp, first_cw=first_cw + c * B, seed=a.seed, table=table)
+        gen.awgn_i8_device(tmp, first_cw=noise_first[c], seed=a.seed, table=table)
         llr[sel] = tmp
         gen.close()
     hard = torch.empty((B, N), dtype=torch.uint8, device="cuda")
@@ -326,25 +348,36 @@ def bench_mixed(a, rank, world, local, torch, dist):
     kt = mx.kernel_time(reset=True)
     mx.profile(False)
     h, it = hard.cpu().numpy(), its.cpu().numpy()
-    per_rate, alg_bytes, be_tot, fe_tot, bits = [], 0.0, 0, 0, 0
+    # per rate over ALL ranks: frames, bit errors, frame errors, iterations,
+    # algorithmic bytes (sums) and the decode launch time (max)
+    sums = []
     for c, code in enumerate(codes):
         sel = ids == c
         e = h[sel][:, :code.k_info].sum(axis=1)          # all-zero codeword: every 1 is an error
-        per_rate.append(dict(code=code.name, ebn0_db=MIXED_EBN0[code.name], frames=int(sel.sum()),
-                             avg_iters=float(it[sel].mean()), ber=float(e.sum()) / (sel.sum() * code.k_info),
-                             fer=float((e > 0).mean()),
+        sums += [int(sel.sum()), int(e.sum()), int((e > 0).sum()), int(it[sel].sum()),
+                 float((4.0 * code.e * it[sel] + 2.0 * N).sum())]
+    sums = reduce_sums(sums, device="cuda")
+    kms = [kt[c][0] / kt[c][1] if kt[c][1] else 0.0 for c in range(len(codes))]
+    kms_max = [reduce_results(k, 0, 0, 0, device="cuda")[0] for k in kms]
+    per_rate, alg_bytes, be_tot, fe_tot, bits = [], 0.0, 0, 0, 0
+    for c, code in enumerate(codes):
+        fr, be_c, fe_c, it_c, ab_c = sums[5 * c:5 * c + 5]
+        fr = int(fr)
+        per_rate.append(dict(code=code.name, ebn0_db=MIXED_EBN0[code.name], frames=fr,
+                             avg_iters=it_c / max(fr, 1), ber=be_c / max(fr * code.k_info, 1),
+                             fer=fe_c / max(fr, 1),
                              kernel=mx.last_kernels()[c],
                              et_first_stage=mx.last_et_stages()[c],   # > 0: staged early termination (coop3)
-                             kernel_ms=round(kt[c][0] / kt[c][1], 4) if kt[c][1] else None))
-        alg_bytes += float((4.0 * code.e * it[sel] + 2.0 * N).sum())
-        be_tot += int(e.sum())
-        fe_tot += int((e > 0).sum())
-        bits += int(sel.sum()) * code.k_info
-    el, be, fe, _ = reduce_results(el, be_tot, fe_tot, B * a.steps, device="cuda")
+                             kernel_ms=round(kms_max[c], 4) if kms_max[c] else None))
+        alg_bytes += ab_c
+        be_tot += int(be_c)
+        fe_tot += int(fe_c)
+        bits += fr * code.k_info
+    el, _, _, _ = reduce_results(el, 0, 0, 0, device="cuda")
     if rank == 0:
         frames = world * B * a.steps
         value = frames * N / el / 1e6
-        achieved = alg_bytes * world * a.steps / el / 1e9
+        achieved = alg_bytes * a.steps / el / 1e9
         out = {
             "metric": "decoded Mbit/s, configs[4]: mixed-rate DVB-S2 (%s) int8 + early termination"
                       % ", ".join(n.split("_", 1)[1].replace("_", "/") for n in names),
@@ -360,10 +393,10 @@ def bench_mixed(a, rank, world, local, torch, dist):
                 "tools/make_dvbs2_shaped.py), not the ETSI tables" if a.mixed_codes == "configs4" else ""),
             "config": {"workload": "mixed-rate DVB-S2 N=64800 batch %d per GPU, <= %d iters, early termination"
                                    % (B, a.iters), "codes": list(names), "batch_per_gpu": B,
-                       "global_batch": B * world, "iters_max": a.iters,
+                       "global_batch": B * world, "iters_max": a.iters, "code_set": a.mixed_codes,
                        "parallelism": "codeword shards x%d (no collective)" % world},
             "per_rate": per_rate,
-            "ber": be / max(world * bits, 1), "fer": fe / max(frames / a.steps, 1),
+            "ber": be_tot / max(bits, 1), "fer": fe_tot / max(world * B, 1),
             # whole-step rate (several kernels on concurrent streams): no single dominant launch;
             # traffic = HBM bytes per step over all its kernels (PMC, profiles/traffic.json)
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": hbm_peak_gbs(), "unit": "GB/s",

@@ -19,7 +19,10 @@ ALGO_OMS, ALGO_NMS, ALGO_MS = 0, 1, 2
 def source_hash():
     """sha256 (16 hex digits) over the sources the library is built from
     (csrc/* and include/*): ties a committed measurement (profiles/traffic.json)
-    to the exact kernel code it was taken on."""
+    to the exact kernel code it was taken on.  A variant library
+    (LDPC_MI355X_LIB, tools/build_variant.sh) folds in its extra defines
+    (the `.defines` stamp written beside it) -- or, without a stamp, its path --
+    so a variant never reports the default build's hash."""
     import hashlib
     root = os.path.dirname(_HERE)
     h = hashlib.sha256()
@@ -30,6 +33,13 @@ def source_hash():
                 h.update(f.encode())
                 with open(fp, "rb") as fh:
                     h.update(fh.read())
+    if os.path.abspath(LIB_PATH) != os.path.abspath(os.path.join(_HERE, "libldpc_mi355x.so")):
+        stamp = LIB_PATH + ".defines"
+        if os.path.exists(stamp):
+            with open(stamp, "rb") as fh:
+                h.update(b"variant:" + fh.read())
+        else:
+            h.update(b"variant-path:" + os.path.abspath(LIB_PATH).encode())
     return h.hexdigest()[:16]
 
 

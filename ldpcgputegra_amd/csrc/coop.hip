@@ -614,8 +614,10 @@ __global__ void __launch_bounds__(64 * (WS + 1)) coop_decode(CoopArgs a)
 
 // ------------------------------------------------------- early termination
 // After each iteration (one coop launch): a codeword stops once all its
-// parity checks hold on the hard decisions V > 0 (the reference's commented
-// `arret` test, CDecoder_OMS_fixed_SSE.cpp:551-553; the oracle's early_term).
+// parity checks hold on the hard decisions V > 0 (the
+// oracle's early_term; not the reference's commented `arret` test,
+// CDecoder_OMS_fixed_SSE.cpp:255,551-553, which tests extrinsic sign parity
+// per 16-frame call: iterations used are unpinned by the reference).
 // Block = 64 consecutive codewords (coalesced V rows) x a chunk of checks;
 // the H indices are wave-uniform (scalar loads).
 // 1 if any of the 4 consecutive degree-D checks at ev fails

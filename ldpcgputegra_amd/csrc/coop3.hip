@@ -227,7 +227,7 @@ static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vec
             uint32_t *rec = &out[((size_t)u * S + kk) * RECW];
             for (int j = 0; j < X; j++) rec[j] = lp.piece[((size_t)u * S + kk) * X + j];
             const uint32_t step = (src[D0] >> STEP_SHIFT) & 63u;   // (rows - k <= m < 65536: checked by coop3_plan_lc)
-            const uint32_t xi = LDPC_C3_XO16 ? step * CW : (step >> 3) * (CW * 8) + (step & 7);   // xo index (u16)
+            const uint32_t xi = (step >> 3) * (CW * 8) + (step & 7);   // xo index (u16): [block][codeword][8 steps]
             rec[W_X] = (src[X] - (uint32_t)k) | xi << 16;
             rec[W_O] = (src[D0 - 1] - (uint32_t)k) | (step * 2 * NP * 16) << 16;              // + cst offset
             rec[W_META] = src[D0];

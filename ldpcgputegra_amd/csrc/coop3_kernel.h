@@ -154,32 +154,11 @@ struct G3 {
 #ifndef LDPC_C3_MPRIO
 #define LDPC_C3_MPRIO 2        // memory wave priority (chain wave: 3; same-box A/B: 2 vs 0 -0.35 %)
 #endif
-#ifndef LDPC_C3_BPRIO
-#define LDPC_C3_BPRIO 0
-#endif
-#ifndef LDPC_C3_PREFIRST
-#define LDPC_C3_PREFIRST 1       // pre of window p+1 before the post of window p-1 in fast periods: 1 = plan
-                                 // distance 2 (WS = 2) kernels, 2 = also slab waves 1 .. of the 4-slab-wave
-                                 // kernels (distance-2 pairs are all in wave 0), 3 = also r1/2's; same box
-                                 // (r05u): 2 vs 1 r2/3 39.48 vs 38.98 ms, r3/4 32.63 vs 32.56, 3: r1/2 36.79
-                                 // vs 35.14 -- a wave that waits for its chain inputs late keeps the partner
-                                 // SIMD's chain / memory wave waiting on the barrier
-#endif
 #ifndef LDPC_C3_PRE_CHUNK_X
 #define LDPC_C3_PRE_CHUNK_X 8    // pres of checks with >= this many info edges: stage-major chunks, two min chains
 #endif
 #ifndef LDPC_C3_POST_CHUNK_X
 #define LDPC_C3_POST_CHUNK_X 8   // posts of checks with >= this many info edges run new_v in stage-major chunks
-#endif
-#ifndef LDPC_C3_XO16
-#define LDPC_C3_XO16 0        // experiment: chain inputs in xo as [step][codeword] u16 (a pair's two values in
-                              // one dword: one conflict-free ds_read_b32 per post instead of two ds_read_u16
-                              // 16 B apart) -- the chain's 8 ds_write_b16 per 8 steps instead of one
-                              // ds_write_b128 cost more than the post gains: same box 36.60 vs 34.93 ms (r05n)
-#endif
-#ifndef LDPC_C3_SWROT
-#define LDPC_C3_SWROT 0       // experiment: slab index = (the wave's slab position + SWROT) % WS (same-box
-                              // A/B of 3 vs 0: -0.8 % on one box, +0.5 % on another)
 #endif
 template <int WS, int R>
 struct Cfg {
@@ -207,10 +186,10 @@ struct alignas(16) Smem3 {
     uint32_t tab[TQ][S][G::RECW];     // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
     uint4 cst[2][S][2][NP];           // chain constants (K1 = (A, B), K2 = (eps, c_o), K3 = (L, H), 0) per step,
                                       // codeword 2q + h at [h][q]   (pre -> chain)
-    uint4 xo[2][S / 8][CW];           // chain inputs Y (chain -> post): LDPC_C3_XO16 [step][codeword] i16 (a
-                                      // pair's two inputs in one dword), else [block][codeword][8 steps] (a
-                                      // codeword swizzle c ^ (c >> 3) that removed that layout's 2-way bank
-                                      // conflict of read_x measured 0.3 % slower, r05g)
+    uint4 xo[2][S / 8][CW];           // chain inputs Y (chain -> post): [block][codeword][8 steps] (a codeword
+                                      // swizzle c ^ (c >> 3) that removed this layout's 2-way bank conflict of
+                                      // read_x measured 0.3 % slower, r05g; a [step][codeword] u16 layout, one
+                                      // dword per pair, cost the chain 8 ds_write_b16 per 8 steps: +4.8 %, r05n)
     struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
         uint4 d[G::NG][8];            //   e < MP: message bytes 16e .. 16e+15, e = MP: the o-edge parity row
     } in[WS][NI];                     //   (NGI = 2: the second gather lands pieces 8 .. MP, 1 KB further)
@@ -374,10 +353,6 @@ struct Slab3 {
     }
     LDPC_DEV uint32_t read_x(int g, const St &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
-        if constexpr (LDPC_C3_XO16) {   // codewords 2q, 2q+1 of the step adjacent: one dword
-            const uint32_t d = *(const uint32_t *)((const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 2 * q);
-            return perm(d, d, 0x020d000du);
-        }
         const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 16 * q;
 #ifdef C3X_BANK_X
         const unsigned short *xz = (const unsigned short *)&sm.xo[g & 1][0][0] + 2 * lane;
@@ -744,16 +719,7 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
     uint4 kq[2][8];
     // the x inputs of steps 8b .. 8b+7 (positions 0..7 of w) -> xo
     auto put_x = [&](int b, const uint32_t (&v)[4]) __attribute__((always_inline)) {
-        if constexpr (LDPC_C3_XO16) {   // [step][codeword] u16
-            unsigned short *x16 = (unsigned short *)&sm.xo[buf][0][0] + c;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                x16[(8 * b + 2 * i) * CW] = (unsigned short)v[i];
-                x16[(8 * b + 2 * i + 1) * CW] = (unsigned short)(v[i] >> 16);
-            }
-        } else {
-            sm.xo[buf][b][c] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
+        sm.xo[buf][b][c] = make_uint4(v[0], v[1], v[2], v[3]);
     };
 #pragma unroll
     for (int i = 0; i < 8; i++) kq[B0 & 1][i] = cp[(B0 * 8 + i) * KST];
@@ -1324,7 +1290,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     }
 
     // ------------------------------------------------------------ slab waves
-    const int sw = (wave - (wave > CHW ? 1 : 0) + LDPC_C3_SWROT) % WS;   // slab index
+    const int sw = wave - (wave > CHW ? 1 : 0);   // slab index
     constexpr int NSL = 64 * WS;                  // slab threads
     const int st_id = sw * 64 + lane;
     // the second-dispatched half of the slab waves loses VALU arbitration to
@@ -1422,8 +1388,11 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             PreIn<D0> in;
             St3<D0, LEAN> &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
-            const bool prefirst = fast && (GG::DIST == 2 ? LDPC_C3_PREFIRST >= 1
-                                                         : sw != 0 && LDPC_C3_PREFIRST >= (WS == 4 ? 2 : 3));
+            // pre first only at plan distance 2 (same box, r05u: slab waves 1 ..
+            // of the distance-1 kernels pre first -- r2/3 39.48 vs 38.98 ms, r1/2
+            // 36.79 vs 35.14: a wave that waits for its chain inputs late keeps
+            // the partner SIMD's chain / memory wave waiting on the barrier)
+            const bool prefirst = fast && GG::DIST == 2;
             if (prefirst) {
                 // plan distance 2 (one slab wave per SIMD): windows p-1 and p+1
                 // share no information variable, so the pre of window p+1 runs
@@ -1445,12 +1414,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             } else if (fast) {
                 // every slab wave posts first (window p-1: chain outputs and the
                 // state in VGPRs), then reads and runs its pre
-                if (fair) {
-                    if (LDPC_C3_BPRIO && wave > CHW)   // experiment: second-dispatched waves ahead in the post
-                        __builtin_amdgcn_s_setprio(P0 + 1);
-                    else
-                        __builtin_amdgcn_s_setprio(P0);
-                }
+                if (fair) __builtin_amdgcn_s_setprio(P0);
                 {
                     const uint32_t xr = sl.read_x(p - 1, sp);
                     if (STAMP) {   // the chain inputs' arrival (the empty asm makes the wave wait for them)

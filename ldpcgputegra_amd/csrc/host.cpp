@@ -8,7 +8,8 @@
 // int8.  Written for the host's wide vector unit: 32 codewords per AVX2
 // register (the reference's SSE decoder does 16), V[N][32] and msg[E][32]
 // interleaved per block of 32 codewords (16 where only SSE4.1 is present),
-// blocks spread over host threads.  A portable loop over the lanes (the same operations, one byte at
+// blocks spread over host threads (the SIMD check loop: host_simd.h, compiled per
+// instruction set in host_avx2.cpp / host_sse4.cpp).  A portable loop over the lanes (the same operations, one byte at
 // a time) runs where neither is available (LDPC_HOST_PORTABLE forces it).  The float path is scalar per codeword.
 #include <algorithm>
 #include <cstdlib>
@@ -16,17 +17,12 @@
 #include <thread>
 #include <vector>
 
-#include <immintrin.h>
-
 #include "host.h"
+#include "host_simd.h"
 
 namespace {
 
 constexpr int HB = 32;   // most codewords per block (one AVX2 register of int8)
-
-struct I8Params {
-    int algo, param, var_min, msg_max, early;
-};
 
 // ---- portable lane ops (the reference's SSE semantics, one byte at a time)
 inline int sat8(int x) { return x < -128 ? -128 : (x > 127 ? 127 : x); }
@@ -77,131 +73,6 @@ void check_portable(int8_t *V, int8_t *msg, const uint32_t *ev, int d, bool late
     }
 }
 
-// the SIMD check, written once over a vector-width trait: W = 32 lanes
-// (AVX2) or W = 16 (SSE4.1, the reference's width, where AVX2 is absent).
-// The edge loops are unrolled for the codes' degrees (check_dispatch): with a
-// runtime degree the contributions went through the stack and DVB-S2 r1/2
-// took 0.42 ns per edge and codeword on one thread, 0.31 unrolled.
-struct Avx2 {
-    static constexpr int W = 32;
-    using V = __m256i;
-    __attribute__((target("avx2"))) static V ld(const void *p) { return _mm256_load_si256((const V *)p); }
-    __attribute__((target("avx2"))) static void st(void *p, V v) { _mm256_store_si256((V *)p, v); }
-    __attribute__((target("avx2"))) static V set1(int x) { return _mm256_set1_epi8((char)x); }
-    __attribute__((target("avx2"))) static V zero() { return _mm256_setzero_si256(); }
-    __attribute__((target("avx2"))) static V subs(V a, V b) { return _mm256_subs_epi8(a, b); }
-    __attribute__((target("avx2"))) static V adds(V a, V b) { return _mm256_adds_epi8(a, b); }
-    __attribute__((target("avx2"))) static V subs_u(V a, V b) { return _mm256_subs_epu8(a, b); }
-    __attribute__((target("avx2"))) static V max(V a, V b) { return _mm256_max_epi8(a, b); }
-    __attribute__((target("avx2"))) static V min(V a, V b) { return _mm256_min_epi8(a, b); }
-    __attribute__((target("avx2"))) static V abs(V a) { return _mm256_abs_epi8(a); }
-    __attribute__((target("avx2"))) static V xor_(V a, V b) { return _mm256_xor_si256(a, b); }
-    __attribute__((target("avx2"))) static V and_(V a, V b) { return _mm256_and_si256(a, b); }
-    __attribute__((target("avx2"))) static V eq(V a, V b) { return _mm256_cmpeq_epi8(a, b); }
-    __attribute__((target("avx2"))) static V blend(V a, V b, V m) { return _mm256_blendv_epi8(a, b, m); }
-    __attribute__((target("avx2"))) static V sign(V a, V b) { return _mm256_sign_epi8(a, b); }
-    // NMS constants: (u16(min) * f) >> 5, signed-saturated to int8 (unpack /
-    // pack stay inside each 128-bit lane, so the byte order is kept)
-    __attribute__((target("avx2"))) static V nms(V mn, int f)
-    {
-        const V z = zero(), ff = _mm256_set1_epi16((short)f);
-        const V lo = _mm256_srli_epi16(_mm256_mullo_epi16(_mm256_unpacklo_epi8(mn, z), ff), 5);
-        const V hi = _mm256_srli_epi16(_mm256_mullo_epi16(_mm256_unpackhi_epi8(mn, z), ff), 5);
-        return _mm256_packs_epi16(lo, hi);
-    }
-};
-struct Sse4 {
-    static constexpr int W = 16;
-    using V = __m128i;
-    __attribute__((target("sse4.1"))) static V ld(const void *p) { return _mm_load_si128((const V *)p); }
-    __attribute__((target("sse4.1"))) static void st(void *p, V v) { _mm_store_si128((V *)p, v); }
-    __attribute__((target("sse4.1"))) static V set1(int x) { return _mm_set1_epi8((char)x); }
-    __attribute__((target("sse4.1"))) static V zero() { return _mm_setzero_si128(); }
-    __attribute__((target("sse4.1"))) static V subs(V a, V b) { return _mm_subs_epi8(a, b); }
-    __attribute__((target("sse4.1"))) static V adds(V a, V b) { return _mm_adds_epi8(a, b); }
-    __attribute__((target("sse4.1"))) static V subs_u(V a, V b) { return _mm_subs_epu8(a, b); }
-    __attribute__((target("sse4.1"))) static V max(V a, V b) { return _mm_max_epi8(a, b); }
-    __attribute__((target("sse4.1"))) static V min(V a, V b) { return _mm_min_epi8(a, b); }
-    __attribute__((target("sse4.1"))) static V abs(V a) { return _mm_abs_epi8(a); }
-    __attribute__((target("sse4.1"))) static V xor_(V a, V b) { return _mm_xor_si128(a, b); }
-    __attribute__((target("sse4.1"))) static V and_(V a, V b) { return _mm_and_si128(a, b); }
-    __attribute__((target("sse4.1"))) static V eq(V a, V b) { return _mm_cmpeq_epi8(a, b); }
-    __attribute__((target("sse4.1"))) static V blend(V a, V b, V m) { return _mm_blendv_epi8(a, b, m); }
-    __attribute__((target("sse4.1"))) static V sign(V a, V b) { return _mm_sign_epi8(a, b); }
-    __attribute__((target("sse4.1"))) static V nms(V mn, int f)
-    {
-        const V z = zero(), ff = _mm_set1_epi16((short)f);
-        const V lo = _mm_srli_epi16(_mm_mullo_epi16(_mm_unpacklo_epi8(mn, z), ff), 5);
-        const V hi = _mm_srli_epi16(_mm_mullo_epi16(_mm_unpackhi_epi8(mn, z), ff), 5);
-        return _mm_packs_epi16(lo, hi);
-    }
-};
-
-// one check over the W lanes of a block (OMS_fixed_SSE.cpp:201-254; later
-// groups :293-314; NMS_fixed_SSE.cpp:188-240); D > 0: the degree known at
-// compile time (the edge loops unrolled, contributions in registers), D = 0:
-// runtime degree d
-template <typename S, int D, bool ET>
-__attribute__((target("avx2,sse4.1"))) inline void check_simd(int8_t *V, int8_t *msg, const uint32_t *ev, int d,
-                                                              bool later, const I8Params &p, const uint8_t *live)
-{
-    using Vec = typename S::V;
-    constexpr int W = S::W;
-    const int dd = D > 0 ? D : d;
-    const Vec vmin = S::set1(p.var_min), mm = S::set1(p.msg_max), s80 = S::set1(0x80);
-    const bool nms = p.algo == LDPC_ALGO_NMS;
-    Vec c[D > 0 ? D : 64], a[D > 0 ? D : 64];
-    Vec sign = S::zero(), min1 = S::set1(127), min2 = min1;
-#pragma GCC unroll 32
-    for (int j = 0; j < dd; j++) {
-        const Vec v = S::ld(V + (size_t)ev[j] * W);
-        const Vec cj = S::max(S::subs(v, S::ld(msg + j * W)), vmin);
-        const Vec aj = (nms || !later) ? S::min(S::abs(cj), mm) : S::abs(S::min(cj, mm));
-        sign = S::xor_(sign, S::and_(cj, s80));
-        c[j] = cj;
-        a[j] = aj;
-        min2 = S::min(min2, S::max(aj, min1));
-        min1 = S::min(min1, aj);
-    }
-    Vec cst1, cst2;
-    if (nms) {
-        cst1 = S::nms(min2, p.param);
-        cst2 = S::nms(min1, p.param);
-    } else {
-        const Vec off = S::set1(p.param);
-        cst1 = S::min(S::subs_u(min2, off), mm);
-        cst2 = S::min(S::subs_u(min1, off), mm);
-    }
-    sign = S::xor_(sign, S::set1((dd & 1) ? 0xC0 : 0x40));
-    const Vec keep = ET ? S::eq(S::ld(live), S::zero()) : S::zero();
-#pragma GCC unroll 32
-    for (int j = 0; j < dd; j++) {
-        const Vec r = S::blend(cst2, cst1, S::eq(a[j], min1));
-        const Vec m = S::sign(r, S::xor_(sign, S::and_(c[j], s80)));
-        Vec nv = S::max(S::adds(c[j], m), vmin);
-        int8_t *vp = V + (size_t)ev[j] * W;
-        if (ET) nv = S::blend(nv, S::ld(vp), keep);   // converged: frozen
-        S::st(msg + j * W, m);
-        S::st(vp, nv);
-    }
-}
-
-template <typename S, bool ET>
-inline void check_dispatch(int8_t *V, int8_t *msg, const uint32_t *ev, int d, bool later, const I8Params &p,
-                           const uint8_t *live)
-{
-    switch (d) {   // the degrees of the reference's codes (DVB-S2: 7, 10, 14, 22, 27, 30 and the tails)
-    case 3: return check_simd<S, 3, ET>(V, msg, ev, d, later, p, live);
-    case 6: return check_simd<S, 6, ET>(V, msg, ev, d, later, p, live);
-    case 7: return check_simd<S, 7, ET>(V, msg, ev, d, later, p, live);
-    case 8: return check_simd<S, 8, ET>(V, msg, ev, d, later, p, live);
-    case 10: return check_simd<S, 10, ET>(V, msg, ev, d, later, p, live);
-    case 14: return check_simd<S, 14, ET>(V, msg, ev, d, later, p, live);
-    case 22: return check_simd<S, 22, ET>(V, msg, ev, d, later, p, live);
-    default: return check_simd<S, 0, ET>(V, msg, ev, d, later, p, live);
-    }
-}
-
 // lanes whose hard decisions satisfy every check
 void syndrome_ok(const ldpc_code *h, const int8_t *V, uint8_t *ok, int W)
 {
@@ -230,11 +101,6 @@ struct Scratch {
     }
 };
 
-#ifndef LDPC_HOST_PF
-#define LDPC_HOST_PF 2
-#endif
-constexpr int PF = LDPC_HOST_PF;   // checks ahead whose V rows are prefetched
-
 // SIMD path of a block: 32-lane AVX2, 16-lane SSE4.1, or the portable loop
 enum class Isa { avx2, sse4, portable };
 
@@ -250,26 +116,19 @@ void decode_block_i8(const ldpc_code *h, const int8_t *llr, uint8_t *hard, int n
     alignas(32) uint8_t live[HB];
     for (int l = 0; l < HB; l++) live[l] = l < nb;
     for (int it = 0; it < iters; it++) {
-        size_t e0 = 0;
-        for (int i = 0; i < h->m; i++) {
-            const int d = h->check_deg[i];
-            const bool later = h->check_group[i] > 0;
-            const uint32_t *ev = &h->edge_var[h->check_start[i]];
-            int8_t *mp = s.m + e0 * W;
-            if (PF > 0 && i + PF < h->m) {   // the V rows of a check PF ahead (random rows: no HW prefetch)
-                const uint32_t *en = &h->edge_var[h->check_start[i + PF]];
-                for (int j = 0; j < h->check_deg[i + PF]; j++) __builtin_prefetch(s.v + (size_t)en[j] * W, 1, 3);
+        if (isa == Isa::avx2)
+            host_checks_avx2(h, s.v, s.m, p, live);
+        else if (isa == Isa::sse4)
+            host_checks_sse4(h, s.v, s.m, p, live);
+        else {
+            size_t e0 = 0;
+            for (int i = 0; i < h->m; i++) {
+                const int d = h->check_deg[i];
+                const uint32_t *ev = &h->edge_var[h->check_start[i]];
+                p.early ? check_portable<true>(s.v, s.m + e0 * W, ev, d, h->check_group[i] > 0, p, live, W)
+                        : check_portable<false>(s.v, s.m + e0 * W, ev, d, h->check_group[i] > 0, p, live, W);
+                e0 += (size_t)d;
             }
-            if (isa == Isa::avx2)
-                p.early ? check_dispatch<Avx2, true>(s.v, mp, ev, d, later, p, live)
-                        : check_dispatch<Avx2, false>(s.v, mp, ev, d, later, p, live);
-            else if (isa == Isa::sse4)
-                p.early ? check_dispatch<Sse4, true>(s.v, mp, ev, d, later, p, live)
-                        : check_dispatch<Sse4, false>(s.v, mp, ev, d, later, p, live);
-            else
-                p.early ? check_portable<true>(s.v, mp, ev, d, later, p, live, W)
-                        : check_portable<false>(s.v, mp, ev, d, later, p, live, W);
-            e0 += (size_t)d;
         }
         if (p.early) {   // per codeword: stop after the first iteration whose hard decisions satisfy H
             uint8_t ok[HB];

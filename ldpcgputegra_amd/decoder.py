@@ -49,6 +49,7 @@ class Decoder:
         h = C.c_void_p()
         _lib.check(_lib.lib().ldpc_ctx_create(self.code.handle, device, max_batch, C.byref(h)))
         self._ctx = h
+        self._pending = []   # (llr, hard) of queued host-buffer decodes, alive until synchronize()
         if kernel:
             self.set_kernel(kernel)
 
@@ -143,13 +144,14 @@ class Decoder:
         self._on_stream(stream, lambda s: _lib.check(_lib.lib().ldpc_decode_i8_host_async(
             self._ctx, s, llr.ctypes.data, hard.ctypes.data, B, n_iter, C.byref(p))), self.device)
         # the queued copies read llr / write hard until synchronize(): keep the
-        # arrays (and so a pinned_empty buffer's page-locked memory) alive
-        self._pending = (llr, hard)
+        # arrays (and so a pinned_empty buffer's page-locked memory) alive --
+        # every call's, since a second call may be queued before synchronize()
+        self._pending.append((llr, hard))
 
     def synchronize(self):
-        """Wait for this context's last decode_i8_host_async."""
+        """Wait for this context's queued decode_i8_host_async calls."""
         _lib.check(_lib.lib().ldpc_ctx_synchronize(self._ctx))
-        self._pending = None
+        self._pending.clear()
 
     # -- device tensors (asynchronous on `stream`, default: torch current stream)
     @staticmethod
@@ -238,8 +240,9 @@ class Decoder:
 
     def close(self):
         if getattr(self, "_ctx", None) is not None and _lib._lib is not None:
-            _lib._lib.ldpc_ctx_destroy(self._ctx)
+            _lib._lib.ldpc_ctx_destroy(self._ctx)   # waits for the context's stream
             self._ctx = None
+        getattr(self, "_pending", []).clear()
 
     def __del__(self):
         self.close()

@@ -30,3 +30,37 @@ def reduce_results(elapsed_s, bit_errors, frame_errors, frames, device=None):
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
     be, fe, fr = c.tolist()
     return float(t.item()), int(be), int(fe), int(fr)
+
+
+def mixed_layout(rank, world, batch, n_codes):
+    """configs[4] (mixed-rate batches) across ranks.  Rank `rank` owns the
+    contiguous global codewords [rank * batch, (rank + 1) * batch); global
+    codeword g has rate g % n_codes.  Returns (ids, noise_first):
+
+    * ids[i]: the rate of the rank's i-th codeword;
+    * noise_first[c]: the channel generator's first codeword index for the
+      rank's rate-c sub-batch (its j-th rate-c codeword draws the noise of
+      index noise_first[c] + j): c * batch * world + the number of rate-c
+      codewords before the rank's first one.
+
+    Every (rate, global codeword) pair gets its own noise index, so ranks never
+    draw the same noise (r05 used first_cw + c * batch, which made rank r's
+    rate c and rank r + 1's rate c - 1 share their noise), and an N-rank job
+    decodes exactly the codewords of one process with batch * world."""
+    import numpy as np
+    first, count = shard_range(rank, world, batch * world)
+    assert count == batch
+    ids = ((first + np.arange(batch)) % n_codes).astype(np.int32)
+    noise_first = [c * batch * world + max(0, (first - c + n_codes - 1) // n_codes) for c in range(n_codes)]
+    return ids, noise_first
+
+
+def reduce_sums(values, device=None):
+    """Element-wise sum of a list of numbers over the default process group
+    (float64; identity without torch.distributed)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.tolist()

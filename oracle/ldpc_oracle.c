@@ -44,6 +44,17 @@ static inline int nms_scale(int mn, int factor)
     return s > 127 ? 127 : (s < -128 ? -128 : s);
 }
 
+/* Early termination (early_term): the build's own definition, SURVEY.md
+ * §8(f) row 2 -- PER CODEWORD, on the POSTERIOR hard decisions v > 0, checked
+ * AFTER each whole iteration; the codeword's soft output, hard decisions and
+ * iterations used freeze there.  This is NOT a restatement of the reference's
+ * commented-out `arret` test (CDecoder_OMS_fixed_SSE.cpp:154,167,232-236,255,
+ * 551-553), which ORs the sign parity of the EXTRINSIC contributions c_j of
+ * every check DURING the iteration (after the odd-degree flip) and would stop
+ * the whole 16-frame decode() call at once.  code/x86 runs a fixed iteration
+ * count (the test is commented out), so iterations-used parity is pinned by
+ * this definition only -- unpinned by the reference; with early_term off the
+ * oracle is the reference's recurrence, pinned by the golden vectors. */
 static int check_syndrome_ok(const oracle_code *h, const int8_t *v)
 {
     const uint32_t *ev = h->edge_var;

@@ -133,3 +133,126 @@ def test_bench_rank_count_checks():
     out = subprocess.run([sys.executable, bench, "--gpus", "2", "--cpu-seconds", "0"], capture_output=True,
                          text=True, timeout=300, env=env, cwd=root)
     assert out.returncode != 0 and "2 ranks but 0 visible GPUs" in out.stderr
+
+
+MIXED = ("dvbs2_r1_2", "dvbs2shape_r3_4", "dvbs2shape_r5_6")   # bench.py MIXED_SETS["configs4"]
+MIXED_EBN0 = (1.0, 2.8, 3.5)                                   # bench.py MIXED_EBN0
+
+
+def test_mixed_layout_noise_disjoint_and_rank_invariant():
+    """configs[4] across ranks (VERDICT r05 missing #2 / weak #5): every
+    (rank, rate, codeword) draws its own noise index, and the N-rank layout
+    is exactly the single-process layout of batch N * B, sliced."""
+    from ldpcgputegra_amd.shard import mixed_layout
+    for world in (1, 2, 3, 8):
+        for B in (1, 5, 6, 4096, 4097):
+            for n in (1, 3, 4):
+                seen = {}
+                ids1, nf1 = mixed_layout(0, 1, world * B, n)
+                for r in range(world):
+                    ids, nf = mixed_layout(r, world, B, n)
+                    assert np.array_equal(ids, ids1[r * B:(r + 1) * B])
+                    for c in range(n):
+                        k = int((ids == c).sum())
+                        # the rank's rate-c codewords draw the single process's noise indices
+                        j0 = int((ids1[:r * B] == c).sum())
+                        assert nf[c] == nf1[c] + j0
+                        for j in range(k):
+                            key = nf[c] + j
+                            assert key not in seen, (world, B, n, r, c, j, seen.get(key))
+                            seen[key] = (r, c, j)
+
+
+def _mixed_worker(rank, world, port, B, out_dir):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+    from ldpcgputegra_amd import Code, Decoder, channel, default_params, load_table
+    from ldpcgputegra_amd.shard import mixed_layout, reduce_sums
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids, nf = mixed_layout(rank, world, B, len(MIXED))
+    hard = np.zeros((B, 64800), dtype=np.uint8)
+    sums = []
+    for c, name in enumerate(MIXED):
+        t = load_table(name)
+        sel = np.where(ids == c)[0]
+        table = channel.i8_table(channel.sigma_from_ebn0(MIXED_EBN0[c], t.k_info / t.n), 8, 31)
+        llr = channel.awgn_i8_host(t.n, sel.size, seed=2024, table=table, first_cw=nf[c])
+        dec = Decoder(Code(name), device=-1, max_batch=max(1, sel.size))   # product host decoder
+        hard[sel] = dec.decode_i8(llr, 50, params=default_params(early_term=1))
+        dec.close()
+        e = hard[sel][:, :t.k_info].sum(axis=1)
+        sums += [sel.size, int(e.sum()), int((e > 0).sum())]
+    tot = reduce_sums(sums)
+    np.save(os.path.join(out_dir, "mixed_hard_%d.npy" % rank), hard)
+    np.save(os.path.join(out_dir, "mixed_sums_%d.npy" % rank), np.array(tot))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_mixed_matches_single_process(tmp_path):
+    """bench.py --mixed's N > 1 layout on the CPU: 2 gloo ranks x 6
+    codewords of configs[4]'s rates, each rank generating its rates' LLRs from
+    shard.mixed_layout's noise indices and decoding them with the product's
+    host decoder (early termination, <= 50 it); the union equals the oracle's
+    decode of the 12 codewords one process would hold, bit for bit, and every
+    rank sees the same per-rate reduced counts."""
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import oracle as O
+    from ldpcgputegra_amd import channel, load_table
+    from ldpcgputegra_amd.shard import mixed_layout
+    B, world = 6, 2
+    mp.start_processes(_mixed_worker, args=(world, _free_port(), B, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    hard = np.concatenate([np.load(tmp_path / ("mixed_hard_%d.npy" % r)) for r in range(world)])
+    ids, nf = mixed_layout(0, 1, world * B, len(MIXED))
+    ref = np.zeros_like(hard)
+    exp_sums = []
+    for c, name in enumerate(MIXED):
+        t = load_table(name)
+        sel = np.where(ids == c)[0]
+        table = channel.i8_table(channel.sigma_from_ebn0(MIXED_EBN0[c], t.k_info / t.n), 8, 31)
+        llr = channel.awgn_i8_host(t.n, sel.size, seed=2024, table=table, first_cw=nf[c])
+        ref[sel] = O.decode_i8(t, llr, 50, early_term=True, threads=4)
+        e = ref[sel][:, :t.k_info].sum(axis=1)
+        exp_sums += [sel.size, int(e.sum()), int((e > 0).sum())]
+    assert np.array_equal(hard, ref)
+    s = [np.load(tmp_path / ("mixed_sums_%d.npy" % r)) for r in range(world)]
+    assert np.array_equal(s[0], s[1]) and list(s[0]) == exp_sums
+
+
+@pytest.mark.gpu
+def test_two_rank_bench_mixed_on_gpu_matches_single_process():
+    """bench.py --mixed (configs[4]) with 2 ranks on the box's one MI355X
+    (gloo; the driver's 8-GPU runs use RCCL): 192 codewords per rank.  Per
+    rate, the ranks' reduced frames, BER, FER and average iterations equal one
+    process decoding the same 384 codewords (shard.mixed_layout: disjoint noise
+    per rank and rate), and rank 0's line reports 2 ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    args = ["--mixed", "--batch", "192", "--steps", "1", "--warmup", "1", "--cpu-seconds", "0"]
+    env = dict(os.environ, LDPC_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"] + args,
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    two = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    args[2] = "384"
+    out1 = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=300, cwd=root)
+    assert out1.returncode == 0, out1.stderr[-2000:]
+    one = json.loads([l for l in out1.stdout.splitlines() if l.startswith("{")][-1])
+    assert two["n_gpus"] == 2 and two["ranks_seen"] == 2 and two["config"]["global_batch"] == 384
+    assert one["n_gpus"] == 1 and one["config"]["global_batch"] == 384
+    for r2, r1 in zip(two["per_rate"], one["per_rate"]):
+        assert r2["code"] == r1["code"] and r2["frames"] == r1["frames"] == 128
+        assert (r2["ber"], r2["fer"], r2["avg_iters"]) == (r1["ber"], r1["fer"], r1["avg_iters"])
+    assert two["ber"] == one["ber"] and two["fer"] == one["fer"]
+    assert any(r["avg_iters"] > 1 for r in one["per_rate"])

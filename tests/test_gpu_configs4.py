@@ -8,9 +8,13 @@ termination on.  The per-rate sub-batches run coop3 at grid 88 (r1/2 at
 first-group degree 7, the shaped r3/4 at degree 14, the shaped r5/6 at degree
 22) -- grid % 8 == 0, so the XCD-aware workgroup remap is ON; the tests here
 check exactly those launches (and the coop kernel's, forced) against the oracle's
-early-termination semantics (syndrome after every iteration; the reference's
-commented `arret` test, code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:551-553,
-as restated in oracle/ldpc_oracle.c; per-check recurrence :172-546).  The
+early-termination semantics: SURVEY.md §8(f) row 2's per-codeword stop on the
+posterior hard-decision syndrome after every iteration (oracle/ldpc_oracle.c,
+check_syndrome_ok).  That is the build's own definition, NOT the reference's
+commented `arret` test (code/x86/CDecoder/OMS/CDecoder_OMS_fixed_SSE.cpp:255,
+551-553: the extrinsic sign parity of every check during the iteration,
+stopping the whole 16-frame call), so iterations-used parity is unpinned by
+the reference; the per-check recurrence (:172-546) is pinned.  The
 shaped codes have no reference build (their tables are not the reference's),
 so the oracle -- pinned against the reference on every code it ships -- is the
 checker.

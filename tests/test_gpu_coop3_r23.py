@@ -10,8 +10,11 @@ configs[4], the reference's r8/9 and r9/10, code/x86/Constantes/64800x7200 /
 edge-code words (128 / 160-B records), gathers and stores in two instructions
 per slot set, 3 / 4 line loads per lane group and period -- against the oracle
 (the reference's recurrence, CDecoder_OMS_fixed_SSE.cpp:172-546; NMS
-CDecoder_NMS_fixed_SSE.cpp:188-240; early termination as the commented
-`arret` test, :551-553).  The reference ships no r2/3 or shaped decoder build
+CDecoder_NMS_fixed_SSE.cpp:188-240; early termination per codeword on the
+posterior hard-decision syndrome after each iteration, SURVEY.md §8(f) row 2 --
+the build's definition, not the reference's commented `arret` test (:255,
+551-553: extrinsic sign parity per 16-frame call), so iterations used are
+unpinned by the reference).  The reference ships no r2/3 or shaped decoder build
 (its x86 tree has constantes_sse.h only for 64800x{32400,7200,6480}), so the
 oracle -- pinned on the 88 reference golden cases, which include r8/9 and
 r9/10 and run on coop3 in test_gpu_parity.py -- is the checker: soft output,

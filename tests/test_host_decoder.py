@@ -111,3 +111,19 @@ def test_host_context_rejects_device_entry_points():
         d.set_kernel(8)
     q = d.quantize(np.array([0.13, -0.13, 4.0, -4.0, np.nan], np.float32))
     assert q.tolist() == [1, -1, 31, -31, -31]
+
+
+def test_host_sse4_object_has_no_vex():
+    """the 16-lane SSE4.1 check loop is the path for hosts without
+    AVX2, so it must not be VEX-encoded (it was compiled under an avx2 target
+    attribute until r06).  host_sse4.cpp is now its own translation unit built
+    with -msse4.1 only; the build check disassembles it."""
+    import subprocess
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    objdir = os.path.join(root, "build", "obj")
+    if not os.path.exists(os.path.join(objdir, "host_sse4.o")):
+        pytest.skip("objects not built here")
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "check_host_isa.py"), objdir],
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr

@@ -33,4 +33,6 @@ wait
 objs=$(ls build/obj/*.o | grep -Ev "$skip")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libldpc_mi355x.so" $objs $vobjs
 rm -f $vobjs
+# the variant's extra defines, folded into _lib.source_hash() (bench.py keys PMC traffic by it)
+echo "$src $*" > "$out/libldpc_mi355x.so.defines"
 echo "$out/libldpc_mi355x.so"

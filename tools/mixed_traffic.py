@@ -4,8 +4,11 @@ FETCH_SIZE / WRITE_SIZE passes over ALL kernels of the run: sum over the
 decode-path kernels (everything but the input generator and torch's own
 kernels) of 2 x FETCH_SIZE + WRITE_SIZE (KB; gfx950 counts half of wide
 reads, MI355X_MICROARCH.md HBM section), divided by the steps run (warmup +
-timed).  Writes profiles/traffic.json["mixed_<set>_b<B>_it<I>"].
-usage: python tools/mixed_traffic.py <fetch dir> <write dir> <steps run> <key> [out.json]"""
+timed).  The workload key, the step count and the source hash of the build
+come from the bench JSON line the FETCH pass itself printed, so
+profiles/traffic.json["mixed_<set>_b<B>_it<I>"] carries the src_sha16 that
+bench.py matches before reporting the number.
+usage: python tools/mixed_traffic.py <fetch dir> <write dir> <fetch pass log> [out.json]"""
 import csv
 import glob
 import json
@@ -27,17 +30,32 @@ def total(d, counter):
     return tot, len(n)
 
 
+def bench_line(log):
+    line = None
+    for l in open(log):
+        if l.startswith("{") and '"metric"' in l:
+            line = json.loads(l)
+    if line is None:
+        raise SystemExit("mixed_traffic: no bench line in %s" % log)
+    return line
+
+
 def main():
-    fd, wd, steps, key = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(ROOT, "profiles", "traffic.json")
+    fd, wd, log = sys.argv[1], sys.argv[2], sys.argv[3]
+    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(ROOT, "profiles", "traffic.json")
+    b = bench_line(log)
+    cfg = b["config"]
+    key = "mixed_%s_b%d_it%d" % (cfg.get("code_set", "configs4"), cfg["batch_per_gpu"], cfg["iters_max"])
+    steps = b["steps"] + b["warmup"]
     fkb, nf = total(fd, "FETCH_SIZE")
     wkb, nw = total(wd, "WRITE_SIZE")
     per_step = (2.0 * fkb + wkb) * 1024.0 / steps
     tr = json.load(open(out)) if os.path.exists(out) else {}
     tr[key] = {"hbm_bytes_per_step": per_step, "fetch_kb_total": fkb, "write_kb_total": wkb, "steps": steps,
-               "dispatches": [nf, nw], "source": "%s, %s" % (fd, wd)}
+               "dispatches": [nf, nw], "source": "%s, %s" % (fd, wd),
+               "src_sha16": b.get("build", {}).get("src_sha16")}
     json.dump(tr, open(out, "w"), indent=1, sort_keys=True)
-    print(json.dumps(tr[key]))
+    print(key, json.dumps(tr[key]))
 
 
 if __name__ == "__main__":

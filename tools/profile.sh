@@ -10,6 +10,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
+# the trace pass runs >= 10 measured launches after 2 warm-up ones (tools/
+# summarize_profiles.py drops the warm-up launches and reports the median);
+# counter passes replay every dispatch, so they run a short bench
+TARGS=${PROF_TRACE_ARGS:---steps 12 --warmup 2 --cpu-seconds 0}
 ARGS=${PROF_ARGS:---steps 3 --warmup 1 --cpu-seconds 0}
 KRE=${PROF_KERNEL_RE:-decode}
 PASSES=${PROF_PASSES:-trace fetch write sq tcc}
@@ -26,7 +30,7 @@ run() {
 }
 for p in $PASSES; do
     case $p in
-    trace) run trace 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py $ARGS ;;
+    trace) run trace 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py $TARGS ;;
     fetch) run fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/fetch -o run -- python3 bench.py $ARGS ;;
     write) run write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/write -o run -- python3 bench.py $ARGS ;;
     sq) run sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-include-regex "$KRE" -f csv -d $OUT/sq -o run -- python3 bench.py $ARGS ;;
@@ -34,8 +38,10 @@ for p in $PASSES; do
     tlb) run tlb 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS TCP_UTCL1_TRANSLATION_HIT TCP_UTCL1_REQUEST TCP_UTCL1_STALL_MULTI_MISS --kernel-include-regex "$KRE" -f csv -d $OUT/tlb -o run -- python3 bench.py $ARGS ;;
     tcplat) run tcplat 600 rocprofv3 --pmc TCP_TCC_WRITE_REQ_LATENCY TCP_TCC_READ_REQ_LATENCY TCP_TCC_WRITE_REQ TCP_TCC_READ_REQ TA_ADDR_STALLED_BY_TC_CYCLES TA_BUSY --kernel-include-regex "$KRE" -f csv -d $OUT/tcplat -o run -- python3 bench.py $ARGS ;;
     tcpstall) run tcpstall 600 rocprofv3 --pmc TCP_PENDING_STALL_CYCLES TCP_TCP_TA_DATA_STALL_CYCLES TCP_TCR_TCP_STALL_CYCLES TCP_UTCL1_SERIALIZATION_STALL TA_DATA_STALLED_BY_TC_CYCLES TA_TA_BUSY --kernel-include-regex "$KRE" -f csv -d $OUT/tcpstall -o run -- python3 bench.py $ARGS ;;
-    mixfetch) run mixfetch 600 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/mixfetch -o run -- python3 bench.py --mixed $ARGS ;;
-    mixwrite) run mixwrite 600 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/mixwrite -o run -- python3 bench.py --mixed $ARGS ;;
+    # configs[4]: PMC over every kernel of the step (tools/mixed_traffic.py: MIX_ARGS e.g. --batch 24576)
+    mixfetch) run mixfetch 600 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/mixfetch -o run -- python3 bench.py --mixed $ARGS ${MIX_ARGS:-} ;;
+    mixwrite) run mixwrite 600 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/mixwrite -o run -- python3 bench.py --mixed $ARGS ${MIX_ARGS:-} ;;
+    mixtrace) run mixtrace 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/mixtrace -o run -- python3 bench.py --mixed $TARGS ${MIX_ARGS:-} ;;
     list) timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true ;;
     tcc) run tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$KRE" -f csv -d $OUT/tcc -o run -- python3 bench.py $ARGS ;;
     esac

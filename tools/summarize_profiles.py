@@ -2,7 +2,10 @@
 """Turn the rocprofv3 output merged back into gpurun_out/prof (tools/profile.sh)
 into committed summaries under profiles/:
 
-  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (pass 1)
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (pass 1; every launch, warm-up included)
+  profiles/<tag>_kernel_steady.json per kernel from the kernel trace: the bench's warm-up launches
+                                    excluded, median / mean / min / max of the rest (the number to
+                                    compare with the bench's HIP-event kernel time and ms_per_step)
   profiles/<tag>_bench.json         the bench JSON line printed under pass 1
   profiles/<tag>_pmc.json           per-kernel FETCH_SIZE / WRITE_SIZE per dispatch
   profiles/traffic.json             {workload key: {hbm_bytes_per_launch, ...}} read by bench.py
@@ -39,6 +42,25 @@ def pmc_per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def steady(trace_csv, warmup):
+    """Per kernel name: durations in dispatch order, the first `warmup`
+    dropped (the bench launches each step kernel once per step)."""
+    acc = {}
+    with open(trace_csv) as f:
+        for r in csv.DictReader(f):
+            name = r.get("Kernel_Name", "?")
+            acc.setdefault(name, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    out = {}
+    for name, v in acc.items():
+        d = [x[1] for x in sorted(v)]
+        k = d[warmup:] if len(d) > warmup else d
+        k_sorted = sorted(k)
+        med = k_sorted[len(k) // 2] if len(k) % 2 else 0.5 * (k_sorted[len(k) // 2 - 1] + k_sorted[len(k) // 2])
+        out[name] = dict(calls=len(d), excluded_warmup=len(d) - len(k), measured=len(k), median_ms=med / 1e6,
+                         mean_ms=sum(k) / len(k) / 1e6, min_ms=min(k) / 1e6, max_ms=max(k) / 1e6)
+    return out
+
+
 def main():
     tag = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "prof")
@@ -55,6 +77,14 @@ def main():
                 bench = json.loads(line)
         if bench:
             json.dump(bench, open(os.path.join(dst, "%s_bench.json" % tag), "w"), indent=1)
+    ktrace = find(os.path.join(src, "trace", "**", "*kernel_trace.csv"))
+    if ktrace:
+        st = steady(ktrace, bench["warmup"] if bench else 0)
+        top = sorted(st.items(), key=lambda kv: -kv[1]["median_ms"] * kv[1]["measured"])
+        json.dump(dict(top), open(os.path.join(dst, "%s_kernel_steady.json" % tag), "w"), indent=1)
+        for name, v in top[:3]:
+            print("%-60s median %.4f ms  mean %.4f  (%d measured, %d warm-up excluded)"
+                  % (name[:60], v["median_ms"], v["mean_ms"], v["measured"], v["excluded_warmup"]))
     fetch = find(os.path.join(src, "fetch", "**", "*counter_collection.csv"))
     write = find(os.path.join(src, "write", "**", "*counter_collection.csv"))
     pmc = {}
