@@ -154,6 +154,25 @@ struct G3 {
 #ifndef LDPC_C3_MPRIO
 #define LDPC_C3_MPRIO 2        // memory wave priority (chain wave: 3; same-box A/B: 2 vs 0 -0.35 %)
 #endif
+#ifndef LDPC_C3_STAGGER
+#define LDPC_C3_STAGGER 1        // WS = 6: the second-dispatched slab waves (3 .. 5, beside waves 0 .. 2 on the
+                                 // same SIMDs) run the pre of window p+1 before the post of window p-1: the two
+                                 // waves of a SIMD out of phase (MI355X_MICROARCH.md, "try a stagger")
+#endif
+#ifndef LDPC_C3_CHAIN_B128
+#define LDPC_C3_CHAIN_B128 1     // chain constants read as ds_read_b128 (4 LDS cycles per wave-instruction)
+                                 // instead of the b96 the compiler narrows the 12-B records to (8 cycles)
+#endif
+#ifndef LDPC_C3_XEARLY
+#define LDPC_C3_XEARLY 1         // pre-first slab waves read their chain inputs (x) at the period start, with
+                                 // the pre's inputs, instead of after the pre (r06d same box: 33.41 vs 33.88 ms;
+                                 // the post-first waves 1, 2 issuing their pre's reads beside the x read
+                                 // 34.40, the memory wave's gather-index reads before its loads 34.06)
+#endif
+#ifndef LDPC_C3_CHAIN_SKIP
+#define LDPC_C3_CHAIN_SKIP 0     // the chain skips a window's trailing pass-through steps (inactive slots: the
+                                 // plan fills ~44.9 of r1/2's 48), their count in slot 0's meta bits 28..30
+#endif
 #ifndef LDPC_C3_PRE_CHUNK_X
 #define LDPC_C3_PRE_CHUNK_X 8    // pres of checks with >= this many info edges: stage-major chunks, two min chains
 #endif
@@ -351,6 +370,13 @@ struct Slab3 {
         in.wx = rc.w(G::W_X);
         in.wo = rc.w(G::W_O);
     }
+    // the chain inputs' two LDS loads alone (x_of packs them: a read issued early, used late)
+    LDPC_DEV uint2 read_x_raw(int g, const St &s) const
+    {
+        const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 16 * q;
+        return make_uint2(xs[0], xs[8]);
+    }
+    LDPC_DEV static uint32_t x_of(uint2 x) { return perm(x.y, x.x, 0x040d000du); }
     LDPC_DEV uint32_t read_x(int g, const St &s) const   // chain inputs of this slot, codewords 2q, 2q+1 -> R pair
     {
         const unsigned short *xs = (const unsigned short *)&sm.xo[g & 1][0][0] + s.xs + 16 * q;
@@ -544,6 +570,8 @@ struct Slab3 {
         r1.y = perm(COV, EPS, 0x07060302u);
         r0.z = perm(H, L, 0x05040100u);
         r1.z = perm(H, L, 0x07060302u);
+        // (12-B ds_write_b96 stores of the three used dwords measured 1.7 %
+        // slower than these 16-B ones, r06c)
         r0.w = r1.w = 0;
         uint4 *cp = (uint4 *)((char *)&sm.cst[cb][0][0][q] + (in.wo >> 16));
         cp[0] = r0;
@@ -676,6 +704,13 @@ struct Slab3 {
     }
 };
 
+// LDPC_C3_CHAIN_B128: the step also names the record's 4th dword (unused), so
+// its constants are read by one ds_read_b128
+#if LDPC_C3_CHAIN_B128
+#define C3_KW(KV) (KV).w
+#else
+#define C3_KW(KV) 0u
+#endif
 // one chain step: input = half IH of xin, output = half OH of xout (the other
 // half of xout is kept); c = (K1, K2, K3) of the step
 #define C3_STEP_SAME(XW, KV)                                                                   \
@@ -683,13 +718,13 @@ struct Slab3 {
                  "v_med3_i16 %1, %1, %3, %1 op_sel:[0,1,1,0]\n\t"                             \
                  "v_med3_i16 %0, %1, %4, %4 op_sel:[0,0,1,1]"                                 \
                  : "+v"(XW), "=&v"(tmp)                                                       \
-                 : "v"((KV).x), "v"((KV).y), "v"((KV).z))
+                 : "v"((KV).x), "v"((KV).y), "v"((KV).z), "v"(C3_KW(KV)))
 #define C3_STEP_CROSS(XI, XO, KV)                                                              \
     asm volatile("v_pk_mad_i16 %1, %2, %4, %3 op_sel:[1,0,0] op_sel_hi:[1,0,1]\n\t"           \
                  "v_med3_i16 %1, %1, %4, %1 op_sel:[0,1,1,0]\n\t"                             \
                  "v_med3_i16 %0, %1, %5, %5 op_sel:[0,0,1,0]"                                 \
                  : "+v"(XO), "=&v"(tmp)                                                       \
-                 : "v"(XI), "v"((KV).x), "v"((KV).y), "v"((KV).z))
+                 : "v"(XI), "v"((KV).x), "v"((KV).y), "v"((KV).z), "v"(C3_KW(KV)))
 
 // NMS: (t, t + 31) = eps f Y + (A, B); >> 5; median with c_o; clamp [L, H]
 #define C3_STEP_SAME_NMS(XW, KV)                                                               \
@@ -712,7 +747,7 @@ struct Slab3 {
 // its output goes to position k+1, so after step 8j+6 positions 0..7 hold the
 // inputs of steps 8j .. 8j+7: the x inputs post needs, stored as one uint4.
 template <int WS, int R, int B0, int B1, bool NMS = false, typename SMT>
-LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
+LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4], uint32_t npv = 0)
 {
     const uint4 *cp = &sm.cst[buf][0][c & 1][c >> 1];
     constexpr int KST = 2 * NP;       // uint4 between steps
@@ -723,6 +758,27 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
     };
 #pragma unroll
     for (int i = 0; i < 8; i++) kq[B0 & 1][i] = cp[(B0 * 8 + i) * KST];
+    // step J of a block (position J -> J + 1)
+    auto step = [&](auto jc, const uint4 (&kb)[8]) __attribute__((always_inline)) {
+        constexpr int J = decltype(jc)::value;
+        uint32_t tmp;
+        if constexpr (J % 2 == 0) {
+            if constexpr (NMS) C3_STEP_SAME_NMS(w[J / 2], kb[J]);
+            else C3_STEP_SAME(w[J / 2], kb[J]);
+        } else {
+            if constexpr (NMS) C3_STEP_CROSS_NMS(w[J / 2], w[(J / 2 + 1) & 3], kb[J]);
+            else C3_STEP_CROSS(w[J / 2], w[(J / 2 + 1) & 3], kb[J]);
+        }
+    };
+    // LDPC_C3_CHAIN_SKIP: the last block of a window with RR real steps (the
+    // rest pass-through: Y' = Y): their x inputs, then the last output
+    // (position RR) moved to position 0, the next window's first input
+    auto partial = [&](auto rc, int b, const uint4 (&kb)[8]) __attribute__((always_inline)) {
+        constexpr int RR = decltype(rc)::value;
+        static_for<0, RR>([&](auto jc) __attribute__((always_inline)) { step(jc, kb); });
+        put_x(b, w);
+        w[0] = (RR & 1) ? w[RR >> 1] >> 16 : w[RR >> 1];
+    };
 #pragma unroll
     for (int b = B0; b < B1; b++) {
         if (b + 1 < B1) {
@@ -730,6 +786,21 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
             for (int i = 0; i < 8; i++) kq[(b + 1) & 1][i] = cp[((b + 1) * 8 + i) * KST];
         }
         uint32_t tmp;
+        if (LDPC_C3_CHAIN_SKIP && b == B1 - 1) {
+            const uint32_t np = __builtin_amdgcn_readfirstlane(npv >> 28) & 7u;   // trailing pass-through steps
+            if (np != 0) {
+                switch (np) {
+                case 1: partial(std::integral_constant<int, 7>{}, b, kq[b & 1]); break;
+                case 2: partial(std::integral_constant<int, 6>{}, b, kq[b & 1]); break;
+                case 3: partial(std::integral_constant<int, 5>{}, b, kq[b & 1]); break;
+                case 4: partial(std::integral_constant<int, 4>{}, b, kq[b & 1]); break;
+                case 5: partial(std::integral_constant<int, 3>{}, b, kq[b & 1]); break;
+                case 6: partial(std::integral_constant<int, 2>{}, b, kq[b & 1]); break;
+                default: partial(std::integral_constant<int, 1>{}, b, kq[b & 1]); break;
+                }
+                continue;
+            }
+        }
         if constexpr (NMS) {
             C3_STEP_SAME_NMS(w[0], kq[b & 1][0]);
             C3_STEP_CROSS_NMS(w[0], w[1], kq[b & 1][1]);
@@ -1030,7 +1101,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             if (STAMP && it == 0) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
                 if (STAMP) tx = stamp3();
-                if (p < G && cl) chain_window3<WS, R, 0, NB, NMS>(sm, p & 1, c, w4);
+                if (p < G && cl)
+                    chain_window3<WS, R, 0, NB, NMS>(sm, p & 1, c, w4,
+                                                      LDPC_C3_CHAIN_SKIP ? sm.tab[p & (TQ - 1)][0][GG::W_META] : 0u);
                 if (STAMP) sP[0] += stamp3() - tx;
                 stage(un, (p + KAHEAD) & (TQ - 1));
                 un = (un + 1 == a.nw) ? 0 : un + 1;
@@ -1392,19 +1465,24 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             // of the distance-1 kernels pre first -- r2/3 39.48 vs 38.98 ms, r1/2
             // 36.79 vs 35.14: a wave that waits for its chain inputs late keeps
             // the partner SIMD's chain / memory wave waiting on the barrier)
-            const bool prefirst = fast && GG::DIST == 2;
+            const bool stag = LDPC_C3_STAGGER && WS == 6 && wave > CHW;
+            const bool prefirst = fast && (GG::DIST == 2 || stag);
             if (prefirst) {
+                if (stag && fair) __builtin_amdgcn_s_setprio(P0);
                 // plan distance 2 (one slab wave per SIMD): windows p-1 and p+1
                 // share no information variable, so the pre of window p+1 runs
                 // first and hides the wait for the chain's window p-1 outputs the
                 // post needs; at distance 1 the same holds for every slab wave
                 // but wave 0 (the plan puts each distance-2 writer / reader pair
                 // there, and wave 0 keeps posting first)
+                uint2 xe = make_uint2(0, 0);
+                if (LDPC_C3_XEARLY) xe = sl.read_x_raw(p - 1, sp);   // x issued first: it lands with the pre's inputs
                 sl.read_pre((s + 1) % NI, GG::KEEP_AD ? rcn : sl.read_rec(p + 1), in);
                 if constexpr (GG::KEEP_AD) rcn = sl.read_rec(p + 2);   // (the next period's pre, either order)
                 sl.template pre<false, ET>(p + 1, in, sn);
                 if (STAMP) t1 = stampL();
-                const uint32_t xr = sl.read_x(p - 1, sp);
+                if (stag && fair) __builtin_amdgcn_s_setprio(P1);
+                const uint32_t xr = LDPC_C3_XEARLY ? Slab3<D0, WS, R, NMS, LEAN>::x_of(xe) : sl.read_x(p - 1, sp);
                 if (STAMP) {
                     asm volatile("" ::"v"(xr));
                     t2 = stampL();
