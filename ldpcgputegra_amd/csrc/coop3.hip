@@ -80,10 +80,15 @@ template <int D> struct WsOf { static constexpr int v = G3<D>::WS; };
 template <int D> struct LcsOf { static constexpr int v = G3<D>::LCS; };
 template <int D> struct SmemOf { static constexpr size_t v = sizeof(Smem3<D, G3<D>::WS, 2>); };
 template <int D> struct DistOf { static constexpr int v = G3<D>::DIST; };
+template <int D> struct SOf { static constexpr int v = G3<D>::S; };
+template <int D> struct XrOf { static constexpr int v = G3<D>::XR; };
+template <int D> struct MrecOf { static constexpr int v = G3<D>::MREC; };
 int g3_recw(int d0) { return g3_at<RecwOf>(d0); }
 int g3_ws(int d0) { return g3_at<WsOf>(d0); }
 size_t g3_smem(int d0) { return g3_at<SmemOf>(d0); }
 int g3_dist(int d0) { return g3_at<DistOf>(d0); }
+int g3_s(int d0) { return g3_at<SOf>(d0); }
+int g3_xr(int d0) { return g3_at<XrOf>(d0); }
 bool g3_degree_ok(int d0) { return d0 == 7 || d0 == 10 || d0 == 14 || d0 == 22 || d0 == 27 || d0 == 30; }
 static_assert(SmemOf<7>::v + 512 <= 160 * 1024 && SmemOf<10>::v + 512 <= 160 * 1024 && SmemOf<14>::v + 512 <= 160 * 1024 &&
                   SmemOf<22>::v + 512 <= 160 * 1024 && SmemOf<27>::v + 512 <= 160 * 1024 &&
@@ -94,8 +99,8 @@ int g3_lcs(int d0) { return g3_at<LcsOf>(d0); }
 }  // namespace
 
 // message bytes per check and 16-codeword group (G3::MREC): 64 for first-group
-// degree <= 8, 96 up to 16, 128 up to 24, 160 up to 32
-int coop3_mrec(int d0) { return 32 * ((d0 + 7) / 8 + 1); }
+// degree <= 8, 96 up to 16, 160 for the two-lanes-per-check degrees 22 .. 30
+int coop3_mrec(int d0) { return g3_degree_ok(d0) ? g3_at<MrecOf>(d0) : 32 * ((d0 + 7) / 8 + 1); }
 
 // OMS / MS as coop (coop_params_ok); NMS with factor <= 64 (msg_max <= 63: the
 // products fit the i16 halves)
@@ -123,7 +128,7 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
     if (ws != g3_ws(D0) || r != 2)
         return ldpc_set_error(LDPC_EINVAL, "LDPC_COOP3_WS must be %d for first-group degree %d, LDPC_COOP3_R 2",
                               g3_ws(D0), D0);
-    const int S = 8 * ws, dist = g3_dist(D0);
+    const int S = g3_s(D0), dist = g3_dist(D0);
     CoopPlan &pl = o.pl;
     // dist 1: neighbouring windows share no information variable; the plan's
     // forwarding codes mark the reads of values written 2 .. r+3 windows
@@ -219,7 +224,8 @@ int coop3_plan_host(const ldpc_code *h, int ws, int r, Coop3Host &o)
 static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vector<uint32_t> &out)
 {
     const int S = ho.S, nw = ho.nw, D0 = ho.d0, X = D0 - 2, RECW = ho.recw;
-    const int W_X = X, W_O = X + 1, W_META = X + 2, NLD = (X + 7) / 8, W_LOP = RECW - 4 * NLD;   // G3
+    const int XR = g3_xr(D0);   // info words: X, or 2 XH for the two-lanes-per-check degrees (sinks past X: 0)
+    const int W_X = XR, W_O = XR + 1, W_META = XR + 2, NLD = (X + 7) / 8, W_LOP = RECW - 4 * NLD;   // G3
     out.assign((size_t)nw * S * RECW, 0);
     for (int u = 0; u < nw; u++)
         for (int kk = 0; kk < S; kk++) {
@@ -365,7 +371,7 @@ __global__ void et_select_k(const int32_t *its, int n, const int *n_dev, const i
 // message halves of the codewords map[16 g2 + i] (i < 16; the padding past
 // count gets zeros)
 __global__ void et_gather_k(const char *Vs, char *Vd, const int32_t *map, const int *count, int vrows, int mrows,
-                            size_t gstride, size_t vpart, int mrec)
+                            size_t gstride, size_t vpart, int mrec, bool half)
 {
     const int g2 = blockIdx.y, nlive = *count;
     if (16 * g2 >= nlive) return;
@@ -384,7 +390,8 @@ __global__ void et_gather_k(const char *Vs, char *Vd, const int32_t *map, const 
                 }
             *(uint4 *)(d + (size_t)r * 16) = make_uint4(w[0], w[1], w[2], w[3]);
         } else {   // message record of check c: pair q's (MA0, MB) words, codeword 2q + h in half h of each,
-                   // then (mrec > 64) the pairs' MA1, MA2, .. words (8 each)
+                   // then (mrec > 64) the pairs' MA1, MA2, .. words (8 each); half (two lanes per check,
+                   // mrec 160): [8 pairs][W0, W1], [8 pairs][W2, W3], [8 pairs][MB]
             const int c = r - vrows, nw = mrec / 4;   // <= 40 words
             uint32_t w[40];
 #pragma unroll
@@ -394,6 +401,16 @@ __global__ void et_gather_k(const char *Vs, char *Vd, const int32_t *map, const 
                 if (src[i] >= 0) {
                     const char *rec = Vs + (size_t)(src[i] >> 4) * gstride + vpart + (size_t)c * mrec;
                     const int qs = (src[i] & 15) >> 1, hs = src[i] & 1, qd = i >> 1, hd = i & 1;
+                    auto half_of = [&](int byte) { return (uint32_t)((const uint16_t *)(rec + byte))[hs] << (16 * hd); };
+                    if (half) {
+#pragma unroll
+                        for (int k = 0; k < 2; k++) {
+                            w[2 * qd + k] |= half_of(8 * qs + 4 * k);
+                            w[16 + 2 * qd + k] |= half_of(64 + 8 * qs + 4 * k);
+                        }
+                        w[32 + qd] |= half_of(128 + 4 * qs);
+                        continue;
+                    }
                     const uint32_t ma = ((const uint16_t *)(rec + 8 * qs))[hs], mb = ((const uint16_t *)(rec + 8 * qs + 4))[hs];
                     w[2 * qd] |= ma << (16 * hd);
                     w[2 * qd + 1] |= mb << (16 * hd);
@@ -526,7 +543,7 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
             hipLaunchKernelGGL(et_select_k, dim3((S + 255) / 256), dim3(256), 0, s, src_its, L.batch, src_n, src_map,
                                sel, map[b], count + st);
             hipLaunchKernelGGL(et_gather_k, dim3(64, grid), dim3(256), 0, s, src, buf[b], sel, count + st, L.n + 8,
-                               L.m + 1, L.vgroup, vpart, mrec);
+                               L.m + 1, L.vgroup, vpart, mrec, cc.d0 >= 22);
             if (hipGetLastError() != hipSuccess) return -1;
             // the compacted codewords from iteration `done` on: no XCD remap
             // (the live groups are the first ones), the batch read on the device

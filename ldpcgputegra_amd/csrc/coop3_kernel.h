@@ -115,38 +115,55 @@ constexpr int TQ = 8;               // window-table slots in LDS
 // codeword and check.
 //
 // First-group degrees 22, 27, 30 (the shaped r5/6, r8/9, r9/10: 20 to 28
-// information edges) run WS = 2 slab waves (S = 16: the records, messages and
-// line-op words of larger windows would not leave the line cache the ~700
-// live lines these codes need), each alone on its SIMD, with the window plan
-// at distance 2 (windows u and u+2 share no information variable either --
-// at S = 16 this costs these codes no window -- so no slot permutation is
-// needed), |c| recomputed in the post and the info edges' line-cache offsets
-// re-read there from the window's records (VGPRs: 3 window states of ~30
-// contributions each).  Their gathers (9 / 11 pieces per slot) and stores
-// (10 / 12) take two 64-lane instructions per 8-slot set.
+// information edges; HALF) put TWO LANES ON EACH CHECK: lane h of a pair
+// reduces info edges [h XH, h XH + XH) (XH = 10 / 14 / 14, even; r8/9's half
+// 1 carries 3 sink entries, neutralised as c = R(127)), one DPP quad_perm
+// [1,0,3,2] exchange merges min1 / min2 / the sign parity, and the x / o
+// edges and the chain constants are computed identically in both lanes.  So
+// 4 slab waves (one per SIMD) of 4 slots each cover the S = 16 window -- the
+// records, messages and line-op words of larger windows would not leave the
+// line cache the ~700 live lines these codes need -- with the window plan at
+// distance 2 (windows u and u+2 share no information variable either: at S =
+// 16 this costs these codes no window, so no slot permutation is needed).
+// Records: words [h XH, h XH + XH) are half h's info offsets (sinks past X);
+// messages, MREC = 160: [8 pairs][W0, W1] (half 0), [8 pairs][W2, W3] (half
+// 1), [8 pairs][MB]: each half's two words hold code slots 0 .. XH-1 (its
+// info edges), 14 (the x edge) and 15 (the o edge / the tail's last edge).
+// The memory wave keeps its 8-slot sets (NSET = 2): its gathers (11 pieces
+// per slot) and stores (12) take two 64-lane instructions per set, as at
+// degree 30 before (r05: 2 slab waves of 8 slots, one lane per check, two
+// SIMDs idle beside the chain and memory waves).
 template <int D0_>
 struct G3 {
     static constexpr int D0 = D0_, X = D0 - 2;                 // check degree, information edges per check
-    static constexpr int NMA = (D0 + 7) / 8;                   // edge-code words per codeword pair
-    static constexpr int MREC = 32 * (NMA + 1);                // message bytes per check and group
+    static constexpr bool HALF = D0 >= 22;                     // two lanes per check (see above)
+    static constexpr int XH = HALF ? ((X + 1) / 2 + 1) / 2 * 2 : X;   // info edges per lane
+    static constexpr int XR = HALF ? 2 * XH : X;               // info words in a record
+    static constexpr int NMA = HALF ? 4 : (D0 + 7) / 8;        // edge-code words per codeword pair
+    static constexpr int NW = HALF ? 2 : NMA;                  // edge-code words a lane holds
+    static constexpr int MREC = HALF ? 160 : 32 * (NMA + 1);   // message bytes per check and group
     static constexpr int MP = MREC / 16;                       // message pieces (16 B) per check
     static constexpr int NG = MP + 1;                          // pieces gathered per slot (+ the o-edge parity row)
     static constexpr int NGI = (8 * NG + 63) / 64;             // gather instructions per 8-slot set
     static constexpr int NSI = (MP + 2 + 7) / 8;               // store instructions per 8-slot set (MP + 2 pieces)
-    static constexpr int W_X = X, W_O = X + 1, W_META = X + 2;
+    static constexpr int W_X = XR, W_O = XR + 1, W_META = XR + 2;
     static constexpr int NLD = (X + 7) / 8;                    // line loads / writebacks per lane group and
                                                                // period (a window touches ~S X / 8 new lines)
     static constexpr int W_LOP = (W_META + 1 + 3) / 4 * 4;     // line-op words (NLD uint4)
     static constexpr int RECW = W_LOP + 4 * NLD;               // slot record words
     static constexpr int NR = (W_META + 1 + 3) / 4;            // uint4 a pre reads of its record
-    static constexpr int WS = D0 == 7 ? 6 : D0 <= 14 ? 4 : 2;  // slab waves: S = 8 WS checks per window (r1/2's
-                                                               // windows fill 45 of 48, r2/3's 30 of 32)
-    static constexpr int DIST = WS == 2 ? 2 : 1;               // windows closer than DIST + 1 share no info variable
-    static constexpr bool KEEP_AD = X <= 16;                   // info edges' LDS offsets kept from pre to post
-    static constexpr int LCS = D0 == 7 ? 752 : D0 == 10 ? 848 : D0 == 14 ? 784 : D0 == 22 ? 960 : D0 == 27 ? 912 : 896;
+    static constexpr int WS = D0 == 7 ? 6 : (D0 <= 14 || HALF) ? 4 : 2;   // slab waves (r1/2's windows fill 45
+                                                               // of 48 slots, r2/3's 30 of 32)
+    static constexpr int SPW = HALF ? 4 : 8;                   // slots per slab wave: S = SPW WS checks per window
+    static constexpr int S = SPW * WS;
+    static constexpr int NSET = S / 8;                         // the memory wave's 8-slot sets
+    static constexpr int DIST = (WS == 2 || HALF) ? 2 : 1;     // windows closer than DIST + 1 share no info variable
+    static constexpr bool KEEP_AD = XH <= 16 && !HALF;        // info edges' LDS offsets kept from pre to post (HALF: re-read)
+    static constexpr int LCS = D0 == 7 ? 752 : D0 == 10 ? 848 : D0 == 14 ? 784 : D0 == 22 ? 944 : 896;
                                                                // line-cache slots (128 B each; slot 0 the sink): what
                                                                // the 160 KB of LDS leave beside the rest
     static_assert(NMA <= 4 && NGI <= 2 && NSI <= 2 && LCS <= 1023, "message pieces / slot field");
+    static_assert(!HALF || (XH % 2 == 0 && XH <= 14 && 2 * XH >= X), "HALF: code slots 14, 15 are the x / o edges");
 };
 #ifndef LDPC_C3_MSLEEP
 #define LDPC_C3_MSLEEP 4      // memory wave: s_sleep (x 64 cycles) after its line loads, before its LDS burst
@@ -179,9 +196,9 @@ struct G3 {
 #ifndef LDPC_C3_POST_CHUNK_X
 #define LDPC_C3_POST_CHUNK_X 8   // posts of checks with >= this many info edges run new_v in stage-major chunks
 #endif
-template <int WS, int R>
+template <int WS, int R, int SPW = 8>
 struct Cfg {
-    static constexpr int S = 8 * WS;                   // checks per window
+    static constexpr int S = SPW * WS;                 // checks per window
     static constexpr int KAHEAD = R + 2 + DPER;        // tables staged KAHEAD windows ahead of the chain
     static constexpr int NI = R + 1;                   // LDS-DMA input windows in flight per slab wave
     static constexpr int NS = R + 1 < 3 ? 3 : R + 1;   // window states in VGPRs (pre at p-1, post at p+1)
@@ -198,8 +215,9 @@ struct Cfg {
 
 template <int D0, int WS, int R>
 struct alignas(16) Smem3 {
-    using CF = Cfg<WS, R>;
+    using CF = Cfg<WS, R, G3<D0>::SPW>;
     using G = G3<D0>;
+    static constexpr int NSET = G::NSET;
     static constexpr int S = CF::S, NI = CF::NI;
     uint4 lc[G::LCS][8];              // line cache: slot = 8 V rows x 16 codewords (LcPlan; slot 0: the sink)
     uint32_t tab[TQ][S][G::RECW];     // slot records, window g in slot g % TQ (LDS-DMA by the chain wave)
@@ -209,10 +227,10 @@ struct alignas(16) Smem3 {
                                       // swizzle c ^ (c >> 3) that removed this layout's 2-way bank conflict of
                                       // read_x measured 0.3 % slower, r05g; a [step][codeword] u16 layout, one
                                       // dword per pair, cost the chain 8 ds_write_b16 per 8 steps: +4.8 %, r05n)
-    struct In {                       // one window's inputs of one slab wave, landed by LDS-DMA (lane 8e + slot):
+    struct In {                       // one window's inputs of one 8-slot set, landed by LDS-DMA (lane 8e + slot):
         uint4 d[G::NG][8];            //   e < MP: message bytes 16e .. 16e+15, e = MP: the o-edge parity row
-    } in[WS][NI];                     //   (NGI = 2: the second gather lands pieces 8 .. MP, 1 KB further)
-    uint4 mst[2][WS][8][G::MP + 2];   // window g's outputs per slab wave in mst[g & 1], per slot: its new
+    } in[NSET][NI];                   //   (NGI = 2: the second gather lands pieces 8 .. MP, 1 KB further)
+    uint4 mst[2][NSET][8][G::MP + 2]; // window g's outputs per 8-slot set in mst[g & 1], per slot: its new
                                       // messages (pieces 0..MP-1), the x edge's new V (piece MP) and the
                                       // tail's last edge's (MP + 1), 16 codewords each (posted in period
                                       // g+1, stored by the memory wave in period g+2: lane q its piece q)
@@ -246,14 +264,14 @@ struct Coop3Args {
 // post but recomputed there (abs_sat / abs_r of c, 2 VALU per edge)
 template <int D0, bool LEAN = false>
 struct St3 {                          // one window's state from pre to post (R / C pairs)
-    static constexpr int X = D0 - 2, NMA = G3<D0>::NMA;
-    uint32_t c[D0 - 1];               // contributions (info, o); tail: new V
-    uint32_t a[LEAN ? 1 : D0 - 1];    // |c| (not clipped: min1 / min2 are, where the constants are made)
+    static constexpr int X = D0 - 2, XL = G3<D0>::XH, NW = G3<D0>::NW;   // (XL: this lane's info edges)
+    uint32_t c[XL + 1];               // contributions (info, o); tail: new V
+    uint32_t a[LEAN ? 1 : XL + 1];    // |c| (not clipped: min1 / min2 are, where the constants are made)
     uint32_t mn1, mn2, sacc, mx;      // min1 / min2 / sign parity over info + o; x-edge old message
                                       // tail: mn1 = MA0, mn2 = MB, mat = MA1 ..
-    uint32_t mat[NMA > 1 ? NMA - 1 : 1];
+    uint32_t mat[NW > 1 ? NW - 1 : 1];
     uint32_t xs;                      // the slot's chain step: u16 index of its x input in xo[buf]
-    uint32_t ad[G3<D0>::KEEP_AD ? X : 1];   // the info edges' pair addresses in the line cache (pre reads, post
+    uint32_t ad[G3<D0>::KEEP_AD ? XL : 1];   // the info edges' pair addresses in the line cache (pre reads, post
                                       // writes; !KEEP_AD: the post re-reads them from the window's records)
     uint32_t v[X > 8 ? 1 : X];        // FZ (early termination): the info edges' V as read (R pairs; X > 8:
                                       // re-read from LDS by the post, Slab3::FZ_REREAD)
@@ -279,7 +297,7 @@ LDPC_DEV uint32_t nms_c(uint32_t r, uint32_t f) { return (pk_mul_lo(pk_ashr8(r),
 LDPC_DEV uint32_t pk_shl5(uint32_t a) { return us(sv(a) << (short)5); }
 
 // a window's records of one slot as a pre reads them: words 0 .. W_META
-template <int D0>
+template <int D0, bool H = G3<D0>::HALF>
 struct Rec {
     uint4 r[G3<D0>::NR];
     LDPC_DEV uint32_t w(int i) const
@@ -288,13 +306,20 @@ struct Rec {
         return (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
     }
 };
+// HALF: this lane's half of the info offsets (words h XH ..) and W_X, W_O, W_META
+template <int D0>
+struct Rec<D0, true> {
+    using G = G3<D0>;
+    uint32_t e[G::XH], wx, wo, meta;
+    LDPC_DEV uint32_t w(int i) const { return i == G::W_X ? wx : i == G::W_O ? wo : i == G::W_META ? meta : e[i]; }
+};
 // what a pre reads from LDS
 template <int D0>
 struct PreIn {
-    static constexpr int X = D0 - 2, NMA = G3<D0>::NMA;
-    uint32_t v[D0 - 1];               // raw V dwords (info edges from the line cache, the o edge from In)
-    uint32_t ad[G3<D0>::KEEP_AD ? X : 1];   // the info pairs' byte offsets in the line cache
-    uint32_t ma[NMA], mb;             // old message record of this pair (MA0 .. MA(NMA-1), MB)
+    static constexpr int X = D0 - 2, XL = G3<D0>::XH, NW = G3<D0>::NW;
+    uint32_t v[XL + 1];               // raw V dwords (info edges from the line cache, the o edge from In)
+    uint32_t ad[G3<D0>::KEEP_AD ? XL : 1];   // the info pairs' byte offsets in the line cache
+    uint32_t ma[NW], mb;              // old message record of this pair (MA0 .. MA(NW-1), MB; HALF: this half's)
     uint32_t meta, wx, wo;            // record words W_META, W_X, W_O
 };
 
@@ -312,10 +337,13 @@ struct Slab3 {
     using St = St3<D0, LEAN>;
     using RecT = Rec<D0>;
     using In = PreIn<D0>;
-    static constexpr int S = SM::S, X = G::X;
+    static constexpr int S = SM::S, X = G::X, XL = G::XH;   // XL: this lane's info edges (HALF: half of them)
+    static constexpr int SX = G::HALF ? 14 : X;           // code slot of the x edge
+    static constexpr int SO = G::HALF ? 15 : D0 - 1;      // code slot of the o edge
+    static constexpr int SL = G::HALF ? 15 : X;           // the tail check's last edge
     SM &sm;
     const Coop3Args &a;
-    int k, kl, q, w, lane, tail;      // slot, slot in this wave, codeword pair, wave, lane
+    int k, kl, q, w, lane, tail;      // slot, slot in its 8-slot set, codeword pair, 8-slot set, lane
     uint32_t usel;                    // v_perm selector: this pair's two bytes of a V dword -> R pair
     PkK K;
     uint32_t fk;                      // NMS factor per half (value form)
@@ -333,6 +361,10 @@ struct Slab3 {
     // the post re-reads it from the line cache, where it is unchanged until
     // this post writes it (no other window between this pre and post touches it)
     static constexpr bool FZ_REREAD = X > 8;
+    // HALF: this lane's half h of its check, -1 in half 1 (its sink entries
+    // past X: c = R(127), no sign, never a minimum), the byte offset of its
+    // pair's MB word in an In record
+    uint32_t h = 0, hm = 0, mbrd = 0;
 
     LDPC_DEV const char *lcb() const { return (const char *)&sm.lc[0][0]; }
     LDPC_DEV char *lcw() const { return (char *)&sm.lc[0][0]; }
@@ -340,10 +372,25 @@ struct Slab3 {
     // ---- reads
     LDPC_DEV RecT read_rec(int g) const
     {
-        const uint4 *r = (const uint4 *)&sm.tab[g & (TQ - 1)][k][0];
         RecT o;
+        if constexpr (G::HALF) {   // words h XH .. h XH + XH - 1 (8-B aligned: XH even), then W_X, W_O, W_META
+            const uint32_t *rw = &sm.tab[g & (TQ - 1)][k][0];
+            const uint2 *e2 = (const uint2 *)(rw + XL * h);
 #pragma unroll
-        for (int i = 0; i < G::NR; i++) o.r[i] = r[i];
+            for (int i = 0; i < XL / 2; i++) {
+                const uint2 d = e2[i];
+                o.e[2 * i] = d.x;
+                o.e[2 * i + 1] = d.y;
+            }
+            const uint4 m = *(const uint4 *)(rw + G::W_X);
+            o.wx = m.x;
+            o.wo = m.y;
+            o.meta = m.z;
+        } else {
+            const uint4 *r = (const uint4 *)&sm.tab[g & (TQ - 1)][k][0];
+#pragma unroll
+            for (int i = 0; i < G::NR; i++) o.r[i] = r[i];
+        }
         return o;
     }
     // pre inputs of the window whose records are rc (its gathers landed in in[w][ib])
@@ -352,20 +399,27 @@ struct Slab3 {
         const char *inb = (const char *)&sm.in[w][ib];
         if constexpr (G::KEEP_AD) {
 #pragma unroll
-            for (int j = 0; j < X; j++) in.ad[j] = rc.w(j) + lwr;
+            for (int j = 0; j < XL; j++) in.ad[j] = rc.w(j) + lwr;
         }
 #pragma unroll
-        for (int j = 0; j < X; j++) in.v[j] = *(const uint32_t *)(lcb() + rc.w(j) + lrd);   // the dword holding this lane's pair
-        in.v[X] = *(const uint32_t *)(inb + prd);
+        for (int j = 0; j < XL; j++) in.v[j] = *(const uint32_t *)(lcb() + rc.w(j) + lrd);   // the dword holding this lane's pair
+        in.v[XL] = *(const uint32_t *)(inb + prd);
+        if constexpr (G::HALF) {   // this half's (W0, W1) / (W2, W3) of the pair, and MB
+            const uint2 mm = *(const uint2 *)(inb + mrd);
+            in.ma[0] = mm.x;
+            in.ma[1] = mm.y;
+            in.mb = *(const uint32_t *)(inb + mbrd);
+        } else {
 #ifdef C3X_BANK_MM   // bank-conflict attribution (timing-only builds, results wrong): conflict-free address
-        const uint2 mm = *(const uint2 *)(inb + 8 * lane);
+            const uint2 mm = *(const uint2 *)(inb + 8 * lane);
 #else
-        const uint2 mm = *(const uint2 *)(inb + mrd);
+            const uint2 mm = *(const uint2 *)(inb + mrd);
 #endif
-        in.ma[0] = mm.x;
-        in.mb = mm.y;
+            in.ma[0] = mm.x;
+            in.mb = mm.y;
 #pragma unroll
-        for (int i = 1; i < G::NMA; i++) in.ma[i] = *(const uint32_t *)(inb + m1rd + 256 * (i - 1));   // [8 pairs][MAi]
+            for (int i = 1; i < G::NMA; i++) in.ma[i] = *(const uint32_t *)(inb + m1rd + 256 * (i - 1));   // [8 pairs][MAi]
+        }
         in.meta = rc.w(G::W_META);
         in.wx = rc.w(G::W_X);
         in.wo = rc.w(G::W_O);
@@ -389,19 +443,37 @@ struct Slab3 {
         return perm(x1, x0, 0x040d000du);   // chain values are in [-127, 127]
     }
 
+    // HALF: min1 / min2 / the sign parity of the other lane of this check
+    // (lane ^ 1, DPP quad_perm [1,0,3,2]) merged in: the exact smallest and
+    // second smallest of the union of both halves' |c|, ties included
+    LDPC_DEV static uint32_t swap1(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true); }
+    LDPC_DEV static void merge(uint32_t &min1, uint32_t &min2, uint32_t &sacc)
+    {
+        const uint32_t m1p = swap1(min1), m2p = swap1(min2), sp = swap1(sacc);
+        min2 = pk_min(pk_max(min1, m1p), pk_min(min2, m2p));
+        min1 = pk_min(min1, m1p);
+        sacc ^= sp;
+    }
+
     // pre of window g: chain constants -> cst[g & 1], state -> s
     template <bool TL, bool FZ_ = false, int MP = -1>
     LDPC_DEV void pre(int g, const In &in, St &s) const
     {
         constexpr bool FZ = FZ_;
         const uint32_t meta = in.meta;
-        uint32_t v[D0 - 1];
+        uint32_t v[XL + 1];
 #pragma unroll
-        for (int j = 0; j <= X; j++) v[j] = unpack_v(in.v[j], usel);
+        for (int j = 0; j <= XL; j++) v[j] = unpack_v(in.v[j], usel);
         if constexpr (G::KEEP_AD) {
 #pragma unroll
-            for (int j = 0; j < X; j++) s.ad[j] = in.ad[j];
+            for (int j = 0; j < XL; j++) s.ad[j] = in.ad[j];
         }
+        // HALF: half 1's entries past X are sinks (r8/9: 25 = 14 + 11 + 3): c = R(127)
+        auto sink = [&](auto jc, uint32_t c) __attribute__((always_inline)) -> uint32_t {
+            constexpr int J = decltype(jc)::value;
+            if constexpr (G::HALF && J < XL && J >= X - XL) return bfi(hm, R127, c);
+            else return c;
+        };
         const MsgTab t = msg_tab(in.mb);
         const uint32_t neg127 = K.neg127, c510 = K.c510;
         uint32_t min1 = R127, min2 = R127, sacc = 0;
@@ -413,8 +485,8 @@ struct Slab3 {
             // the info edges' contributions stay unclamped (the saturated
             // 0x8000 below R(-128) included): the post uses only their sign
             // and |c| (abs_sat caps it at R(127) as the reference's clamp does)
-            if constexpr (X < LDPC_C3_PRE_CHUNK_X) {
-                static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+            if constexpr (XL < LDPC_C3_PRE_CHUNK_X) {
+                static_for<0, XL>([&](auto jc) __attribute__((always_inline)) {
                     constexpr int J = decltype(jc)::value;
                     const uint32_t c = pk_sub_sat(v[J], old_msg2<J>(in.ma, t, K));
                     const uint32_t aj = abs_sat(c, c510);
@@ -438,8 +510,8 @@ struct Slab3 {
                 // smallest of the union, ties included
                 constexpr int PC = 4;
                 uint32_t m1[2] = {R127, R127}, m2[2] = {R127, R127};
-                static_for<0, (X + PC - 1) / PC>([&](auto cc) __attribute__((always_inline)) {
-                    constexpr int J0 = decltype(cc)::value * PC, E = X - J0 < PC ? X - J0 : PC;
+                static_for<0, (XL + PC - 1) / PC>([&](auto cc) __attribute__((always_inline)) {
+                    constexpr int J0 = decltype(cc)::value * PC, E = XL - J0 < PC ? XL - J0 : PC;
                     uint32_t om[E], aj[E];
                     static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
                         constexpr int e = decltype(ec)::value;
@@ -448,7 +520,7 @@ struct Slab3 {
                     __builtin_amdgcn_sched_barrier(0);
                     static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
                         constexpr int e = decltype(ec)::value;
-                        s.c[J0 + e] = pk_sub_sat(v[J0 + e], om[e]);
+                        s.c[J0 + e] = sink(std::integral_constant<int, J0 + e>{}, pk_sub_sat(v[J0 + e], om[e]));
                     });
                     __builtin_amdgcn_sched_barrier(0);
                     static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
@@ -467,16 +539,17 @@ struct Slab3 {
                 min1 = pk_min(m1[0], m1[1]);
                 min2 = pk_min(pk_max(m1[0], m1[1]), pk_min(m2[0], m2[1]));
             }
+            if constexpr (G::HALF) merge(min1, min2, sacc);   // the other half's info edges
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             const uint32_t kb = sacc ^ ((D0 & 1) ? SIGNS : 0u);
-            const uint32_t cor = pk_max(pk_sub_sat(v[X], old_msg2<D0 - 1>(in.ma, t, K)), neg127);
+            const uint32_t cor = pk_max(pk_sub_sat(v[XL], old_msg2<SO>(in.ma, t, K)), neg127);
             const uint32_t ao = abs_r(cor, c510);
-            s.c[X] = cor;
-            if constexpr (!LEAN) s.a[X] = ao;
+            s.c[XL] = cor;
+            if constexpr (!LEAN) s.a[XL] = ao;
             s.sacc = sacc ^ cor;
             s.mn2 = pk_max(min1, pk_min(ao, min2));
             s.mn1 = pk_min(min1, ao);
-            const uint32_t mx = old_msg2<X>(in.ma, t, K);
+            const uint32_t mx = old_msg2<SX>(in.ma, t, K);
             s.mx = mx;
             // chain constants in value form (R >> 8, C >> 8), both codewords at once
             COV = pk_ashr8(cor);
@@ -502,48 +575,55 @@ struct Slab3 {
 #pragma unroll
                     for (int j = 0; j < X; j++) s.v[j] = v[j];
                 }
-                const uint32_t VO = pk_ashr8(v[X]);
+                const uint32_t VO = pk_ashr8(v[XL]);
                 L = bfi(fm, VO, L);
                 H = bfi(fm, VO, H);
             }
         } else {
             // the tail check (later degree group: a = |min(c, msg_max)|,
             // OMS_fixed_SSE.cpp:293,314) has no chain input: finish it here
-            uint32_t avl[LEAN ? X + 1 : 1];   // LEAN: the tail's |c| (used in this pre only), else in s.a
+            uint32_t avl[LEAN ? XL + 1 : 1];   // LEAN: the tail's |c| (used in this pre only), else in s.a
             auto av = [&](int j) __attribute__((always_inline)) -> uint32_t & { return LEAN ? avl[LEAN ? j : 0] : s.a[LEAN ? 0 : j]; };
-            static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
-                constexpr int J = decltype(jc)::value;
-                const uint32_t c = pk_max(pk_sub_sat(v[J], old_msg2<J>(in.ma, t, K)), neg127);
-                // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2
-                const uint32_t aj = NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510);
+            // edge J (value index; code slot CS): its contribution into min1 / min2 / sacc
+            auto tail_edge = [&](auto jc, auto csc) __attribute__((always_inline)) {
+                constexpr int J = decltype(jc)::value, CS = decltype(csc)::value;
+                const uint32_t c = sink(jc, pk_max(pk_sub_sat(v[J], old_msg2<CS>(in.ma, t, K)), neg127));
+                // OMS: a = |min(c, msg_max)| (later group); NMS: min(|c|, msg_max), clipped in min1 / min2;
+                // a sink's a = R(127), never a minimum (|min(R(127), msg_max)| would be msg_max)
+                const uint32_t aj = sink(jc, NMS ? abs_r(c, c510) : abs_r(pk_min(c, K.rmm), c510));
                 s.c[J] = c;
                 av(J) = aj;
                 sacc ^= c;
                 min2 = pk_max(min1, pk_min(aj, min2));
                 min1 = pk_min(min1, aj);
-            });
+            };
+            static_for<0, XL>([&](auto jc) __attribute__((always_inline)) { tail_edge(jc, jc); });
+            if constexpr (G::HALF) merge(min1, min2, sacc);   // the other half's info edges
+            tail_edge(std::integral_constant<int, XL>{}, std::integral_constant<int, SL>{});   // the last edge
             const uint32_t k1 = NMS ? nms_c(pk_min(min2, K.rmm), fk)
                                     : pk_min(pk_max(pk_sub(min2, K.coff), 0u), K.rmm) & HIBYTES;
             const uint32_t k2 = NMS ? nms_c(pk_min(min1, K.rmm), fk)
                                     : pk_min(pk_max(pk_sub(min1, K.coff), 0u), K.rmm) & HIBYTES;
-            uint32_t e1, e2, MAn[G::NMA];
+            uint32_t e1, e2, MAn[G::NW];
 #pragma unroll
-            for (int i = 0; i < G::NMA; i++) MAn[i] = 0;
+            for (int i = 0; i < G::NW; i++) MAn[i] = 0;
             signed_csts(k1, k2, sacc ^ (((D0 - 1) & 1) ? SIGNS : 0u), e1, e2);
-            static_for<0, X + 1>([&](auto jc) __attribute__((always_inline)) {
-                constexpr int J = decltype(jc)::value;
-                s.c[J] = new_v_later<J & 7>(s.c[J], av(J), min1, e1, e2, MAn[J >> 3], neg127);
+            auto tail_new = [&](auto jc, auto csc) __attribute__((always_inline)) {
+                constexpr int J = decltype(jc)::value, CS = decltype(csc)::value;
+                s.c[J] = new_v_later<CS & 7>(s.c[J], av(J), min1, e1, e2, MAn[CS >> 3], neg127);
                 if constexpr (FZ) s.c[J] = bfi(fm, v[J], s.c[J]);   // converged codewords keep their V
-            });
+            };
+            static_for<0, XL>([&](auto jc) __attribute__((always_inline)) { tail_new(jc, jc); });
+            tail_new(std::integral_constant<int, XL>{}, std::integral_constant<int, SL>{});
             s.mx = 0;
             s.sacc = 0;
             s.mn1 = MAn[0];
 #pragma unroll
-            for (int i = 1; i < G::NMA; i++) s.mat[i - 1] = MAn[i];
+            for (int i = 1; i < G::NW; i++) s.mat[i - 1] = MAn[i];
             s.mn2 = perm(e2, e1, 0x07030501u);
             // the chain passes V[p_0] (the tail's last edge) on: A = B = c_o = L = H = y
             // (NMS: A = 32 y, B = 32 y + 31)
-            const uint32_t Y = pk_ashr8(s.c[X]);
+            const uint32_t Y = pk_ashr8(s.c[XL]);
             A = B = COV = L = H = Y;
             if constexpr (NMS) {
                 A = pk_shl5(Y);
@@ -574,8 +654,10 @@ struct Slab3 {
         // slower than these 16-B ones, r06c)
         r0.w = r1.w = 0;
         uint4 *cp = (uint4 *)((char *)&sm.cst[cb][0][0][q] + (in.wo >> 16));
-        cp[0] = r0;
-        cp[NP] = r1;
+        if (!G::HALF || h == 0) {   // HALF: both lanes of a check hold the same constants
+            cp[0] = r0;
+            cp[NP] = r1;
+        }
     }
 
     // post of window g (x inputs xr): new info V pairs -> the line cache (at
@@ -603,9 +685,10 @@ struct Slab3 {
                 return rp.w(j) + lwr;
         };
         // edge J's code into MA[J / 8]
-        uint32_t MA[G::NMA], MB;
+        uint32_t MA[G::NW], MB;
 #pragma unroll
-        for (int i = 0; i < G::NMA; i++) MA[i] = 0;
+        for (int i = 0; i < G::NW; i++) MA[i] = 0;
+        const bool lead = !G::HALF || h == 0;   // HALF: the x / tail edges' V and MB are the same in both lanes
         auto nv = [&](auto jc, uint32_t c, uint32_t av, uint32_t min1, uint32_t e1, uint32_t e2)
                       __attribute__((always_inline)) -> uint32_t {
             constexpr int J = decltype(jc)::value;
@@ -630,8 +713,8 @@ struct Slab3 {
                 else
                     put(ad, FZ ? perm(n, s.v[FZ_REREAD ? 0 : J], psel) : pack_v(n));   // FZ: pack_v of new / old per codeword
             };
-            if constexpr (X < LDPC_C3_POST_CHUNK_X) {
-                static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+            if constexpr (XL < LDPC_C3_POST_CHUNK_X) {
+                static_for<0, XL>([&](auto jc) __attribute__((always_inline)) {
                     constexpr int J = decltype(jc)::value;
                     const uint32_t aJ = LEAN ? abs_sat(s.c[J], K.c510) : s.a[LEAN ? 0 : J];
                     put_new(jc, nv(jc, s.c[J], aJ, min1, e1, e2));
@@ -643,8 +726,8 @@ struct Slab3 {
                 // wave per SIMD exposes every latency; r05o stamps: the post 2.2x
                 // the pre at degree 30)
                 constexpr int PC = 4;
-                static_for<0, (X + PC - 1) / PC>([&](auto cc) __attribute__((always_inline)) {
-                    constexpr int J0 = decltype(cc)::value * PC, E = X - J0 < PC ? X - J0 : PC;
+                static_for<0, (XL + PC - 1) / PC>([&](auto cc) __attribute__((always_inline)) {
+                    constexpr int J0 = decltype(cc)::value * PC, E = XL - J0 < PC ? XL - J0 : PC;
                     uint32_t av[E], nq[E], T[E], sc[E];
                     static_for<0, E>([&](auto ec) __attribute__((always_inline)) {
                         constexpr int e = decltype(ec)::value;
@@ -675,32 +758,40 @@ struct Slab3 {
             }
             if constexpr (MP >= 0) __builtin_amdgcn_s_setprio(MP);   // mid-phase wave priority (fast periods)
             // x edge: for converged codewords the chain passed V[p_{i-1}] unchanged
-            const uint32_t nx = nv(std::integral_constant<int, X>{}, cx, ax, min1, e1, e2);
-            *sx = (unsigned short)(FZ ? perm(nx, xr, psel) : pack_v(nx));
+            const uint32_t nx = nv(std::integral_constant<int, SX>{}, cx, ax, min1, e1, e2);
+            if (lead) *sx = (unsigned short)(FZ ? perm(nx, xr, psel) : pack_v(nx));
             // the o edge: its code only (the next check rewrites V[o] as its x edge)
-            const uint32_t aO = LEAN ? abs_r(s.c[X], K.c510) : s.a[LEAN ? 0 : X];
-            msg_code<(D0 - 1) & 7>(s.c[X], aO, min1, MA[(D0 - 1) >> 3]);
+            const uint32_t aO = LEAN ? abs_r(s.c[XL], K.c510) : s.a[LEAN ? 0 : XL];
+            msg_code<SO & 7>(s.c[XL], aO, min1, MA[SO >> 3]);
             MB = perm(e2, e1, 0x07030501u);
         } else {
-            static_for<0, X>([&](auto jc) __attribute__((always_inline)) {
+            static_for<0, XL>([&](auto jc) __attribute__((always_inline)) {
                 constexpr int J = decltype(jc)::value;
                 put(ad_of(g, s, J), pack_v(s.c[J]));
             });
-            *sx = (unsigned short)pack_v(xr);       // V of the last group-0 check's o edge
-            *so = (unsigned short)pack_v(s.c[X]);   // the tail's last edge
+            if (lead) {
+                *sx = (unsigned short)pack_v(xr);        // V of the last group-0 check's o edge
+                *so = (unsigned short)pack_v(s.c[XL]);   // the tail's last edge
+            }
             MA[0] = s.mn1;
             MB = s.mn2;
 #pragma unroll
-            for (int i = 1; i < G::NMA; i++) MA[i] = s.mat[i - 1];
+            for (int i = 1; i < G::NW; i++) MA[i] = s.mat[i - 1];
         }
+        if constexpr (G::HALF) {   // [8 pairs][W0, W1] (half 0), [8 pairs][W2, W3] (half 1), [8 pairs][MB]
+            char *mr = (char *)&sm.mst[g & 1][w][kl][0];
+            *(uint2 *)(mr + 64 * h + 8 * q) = make_uint2(MA[0], MA[1]);
+            if (lead) *(uint32_t *)(mr + 128 + 4 * q) = MB;
+        } else {
 #ifdef C3X_BANK_MST
-        *(uint2 *)((char *)&sm.mst[g & 1][w][0][0] + 8 * lane) = make_uint2(MA[0], MB);
+            *(uint2 *)((char *)&sm.mst[g & 1][w][0][0] + 8 * lane) = make_uint2(MA[0], MB);
 #else
-        *(uint2 *)((char *)&sm.mst[g & 1][w][kl][0] + 8 * q) = make_uint2(MA[0], MB);
+            *(uint2 *)((char *)&sm.mst[g & 1][w][kl][0] + 8 * q) = make_uint2(MA[0], MB);
 #endif
 #pragma unroll
-        for (int i = 1; i < G::NMA; i++)   // [8 pairs][MAi]: pieces 4 + 2 (i - 1) ..
-            *(uint32_t *)((char *)&sm.mst[g & 1][w][kl][4 + 2 * (i - 1)] + 4 * q) = MA[i];
+            for (int i = 1; i < G::NMA; i++)   // [8 pairs][MAi]: pieces 4 + 2 (i - 1) ..
+                *(uint32_t *)((char *)&sm.mst[g & 1][w][kl][4 + 2 * (i - 1)] + 4 * q) = MA[i];
+        }
     }
 };
 
@@ -881,7 +972,7 @@ template <int D0, int WS, int R, bool STAMP, bool ET = false, bool NMS = false>
 __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 {
     using SM = Smem3<D0, WS, R>;
-    using CF = Cfg<WS, R>;
+    using CF = Cfg<WS, R, G3<D0>::SPW>;
     using GG = G3<D0>;
     constexpr int S = CF::S, KAHEAD = CF::KAHEAD, U = CF::U, CHW = CF::CHW, NB = CF::NB;
     __shared__ SM sm;
@@ -1125,10 +1216,11 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     const int kl = lane >> 3, q = lane & 7;
 
     if (wave == MW) {
+        constexpr int NST = GG::NSET;   // the 8-slot sets (= WS but for HALF: 4 slab waves of 4 slots)
         if (LDPC_C3_MPRIO > 0) __builtin_amdgcn_s_setprio(LDPC_C3_MPRIO);
         // ------------------------------------------------------------ memory wave
         // Every vector-memory operation of the workgroup, per period p for each
-        // slab wave's set of 8 slots (w = 0..WS-1), in this order: the line
+        // slab wave's set of 8 slots (w = 0..NST-1), in this order: the line
         // loads of period p (8 lines per set, into VGPRs); the LDS-DMA gathers
         // of window p+1+R (messages + o-edge parity rows); the line writebacks
         // of period p (slot -> VGPRs -> HBM); the stores of window p-2
@@ -1211,25 +1303,25 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 #pragma unroll
             for (int i = 0; i <= R; i++)   // window i -> in[w][i]   (nw > R + 3)
 #pragma unroll
-                for (int w = 0; w < WS; w++) gather(w, i, i);
+                for (int w = 0; w < NST; w++) gather(w, i, i);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();   // prologue 1b: the first windows' gathers landed
             __syncthreads();   // prologue 2
             if (STAMP && it == 0) t0 = stamp3();
             constexpr int NPD = LC_PUT + 1;
             constexpr int NLD = GG::NLD;
-            uint4 pend[NPD][WS][NLD];   // line loads of periods p-LC_PUT .. p (written to their slots LC_PUT periods on)
+            uint4 pend[NPD][NST][NLD];   // line loads of periods p-LC_PUT .. p (written to their slots LC_PUT periods on)
 #pragma unroll
             for (int i = 0; i < NPD; i++)
 #pragma unroll
-                for (int w = 0; w < WS; w++)
+                for (int w = 0; w < NST; w++)
 #pragma unroll
                     for (int l = 0; l < NLD; l++) pend[i][w][l] = make_uint4(0, 0, 0, 0);
             int uS = a.nw - 1;   // local index of window p-1 (the next period's stores)
-            uint32_t sidx[WS][NSI];   // the stores' indices (window p-2), read in period p-1
-            uint4 lop[WS][NLD];  // the line ops of period p (byte offsets, record words W_LOP ..), read in period p-1
+            uint32_t sidx[NST][NSI];   // the stores' indices (window p-2), read in period p-1
+            uint4 lop[NST][NLD];  // the line ops of period p (byte offsets, record words W_LOP ..), read in period p-1
 #pragma unroll
-            for (int w = 0; w < WS; w++) {
+            for (int w = 0; w < NST; w++) {
 #pragma unroll
                 for (int i = 0; i < NSI; i++) sidx[w][i] = (uint32_t)a.m;
 #pragma unroll
@@ -1237,24 +1329,24 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             }
             // period p, vector memory in this order: the line loads of period
             // p, the gathers of window p+1+R, the line writebacks of period p,
-            // the stores of window p-2 (4 WS ops: 24 at WS = 6); vmcnt(6 WS) =
-            // 4 WS + 2 WS at its end completes everything up to the gathers of period p-1
+            // the stores of window p-2 (4 NST ops: 24 at NST = 6); vmcnt(6 NST) =
+            // 4 NST + 2 NST at its end completes everything up to the gathers of period p-1
             // (the pre of window p+2 reads them next period) and so the line
             // loads of period p-1 (the slot writes of period p+1 take those of
             // period p+1-LC_PUT = p-1), and a writeback two periods after its
             // issue (its line is loaded again >= 3 periods later,
             // linecache.cpp).  The count holds only while the compiler emits
-            // exactly these 4 WS vector-memory instructions per period:
+            // exactly these 4 NST vector-memory instructions per period:
             // tools/check_vmcnt.py (run by __graft_entry__.build) checks the
             // ISA.  The compiler's own waits for the line loads it tracks (it
             // does not see the LDS-DMA gathers) are stricter than needed.
             auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
                 constexpr int s = decltype(sc_)::value;   // p % NPD
                 if (STAMP) tx = stampL();
-                uint32_t gix[WS][NGI];
-                uint4 wbd[WS][NLD], std_[WS][NSI];
+                uint32_t gix[NST][NGI];
+                uint4 wbd[NST][NLD], std_[NST][NSI];
                 auto loads = [&]() __attribute__((always_inline)) {   // line loads of period p
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
                         static_for<0, NLD>([&](auto lc) __attribute__((always_inline)) {
                             constexpr int l = decltype(lc)::value;
@@ -1263,7 +1355,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     });
                 };
                 auto read_gix = [&]() __attribute__((always_inline)) {   // gather indices of window p+1+R
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
 #pragma unroll
                         for (int i = 0; i < NGI; i++)
@@ -1271,7 +1363,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     });
                 };
                 auto read_out = [&]() __attribute__((always_inline)) {   // writeback and store data
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
 #ifdef C3X_BANK_MEM
                         wbd[w][0] = *(const uint4 *)(lcb + 16 * lane);
@@ -1286,14 +1378,14 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     });
                 };
                 auto slot_writes = [&]() __attribute__((always_inline)) {   // lines loaded in period p-LC_PUT
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
 #pragma unroll
                         for (int l = 0; l < NLD; l++) *(uint4 *)(lcb + (lop[w][l].z ^ lq)) = pend[(s + 1) % NPD][w][l];
                     });
                 };
                 auto gathers = [&]() __attribute__((always_inline)) {
-                    static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                    static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {
                         constexpr int w = decltype(wc)::value;
 #ifndef C3X_BANK_NODMA
 #pragma unroll
@@ -1311,21 +1403,21 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 read_out();
                 gathers();
                 slot_writes();
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // writebacks of period p
+                static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {   // writebacks of period p
                     constexpr int w = decltype(wc)::value;
                     static_for<0, NLD>([&](auto lc) __attribute__((always_inline)) {
                         constexpr int l = decltype(lc)::value;
                         rbuf_store_v4(__builtin_bit_cast(i32x4, wbd[w][l]), vr, (int)(lop[w][l].y + lq), 0, 0);
                     });
                 });
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {   // stores of window p-2 (sink before period 2)
+                static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {   // stores of window p-2 (sink before period 2)
                     constexpr int w = decltype(wc)::value;
 #pragma unroll
                     for (int i = 0; i < NSI; i++)
                         rbuf_store_v4(__builtin_bit_cast(i32x4, std_[w][i]), vr, (int)soffs(i, sidx[w][i]), 0, 0);
                 });
                 // the indices of window p-1's stores and of the next period's line ops
-                static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+                static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {
                     constexpr int w = decltype(wc)::value;
 #pragma unroll
                     for (int i = 0; i < NSI; i++) sidx[w][i] = store_idx(i, w, p - 1, uS == a.tail, p >= 1);
@@ -1334,8 +1426,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                         lop[w][l] = *(const uint4 *)&sm.tab[(p + 1) & (TQ - 1)][8 * w + kl][GG::W_LOP + 4 * l];
                 });
                 if (STAMP) sP[1] += stampL() - tx;
-                // the gathers of p-1: (NLD + NSI) WS ops of p-1 and (2 NLD + NGI + NSI) WS of p after them
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((3 * NLD + NGI + 2 * NSI) * WS) : "memory");
+                // the gathers of p-1: (NLD + NSI) NST ops of p-1 and (2 NLD + NGI + NSI) NST of p after them
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((3 * NLD + NGI + 2 * NSI) * NST) : "memory");
                 if (STAMP) sA += stampL() - tx;
                 __syncthreads();
                 uS = (uS + 1 == a.nw) ? 0 : uS + 1;
@@ -1350,7 +1442,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                     mperiod(std::integral_constant<int, decltype(jc)::value>{}, p + decltype(jc)::value);
             });
             // the stores of window G-1 (its post ran in period G)
-            static_for<0, WS>([&](auto wc) __attribute__((always_inline)) {
+            static_for<0, NST>([&](auto wc) __attribute__((always_inline)) {
 #pragma unroll
                 for (int i = 0; i < NSI; i++) store_win(i, decltype(wc)::value, G - 1, sidx[decltype(wc)::value][i]);
             });
@@ -1370,25 +1462,37 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     // its SIMD partner; static priority evens them out (MI355X_MICROARCH.md,
     // "Two waves per SIMD", item 4)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
-    constexpr bool LEAN = (ET && GG::X > 8) || GG::X > 16;
+    constexpr bool LEAN = (ET && GG::XH > 8) || GG::XH > 16 || GG::HALF;   // HALF: |c| recomputed in the post (VGPRs)
+    // lanes: one lane per check, lane = 8 slot + pair (slot k = 8 sw + kl in
+    // set sw); HALF: lane = 16 slot + 2 pair + half (slot k = 4 sw + kls,
+    // in set k >> 3 at k & 7)
+    const int sk = GG::HALF ? 4 * sw + (lane >> 4) : 8 * sw + kl;   // this lane's slot
+    const int sq = GG::HALF ? (lane >> 1) & 7 : q;                  // its codeword pair
+    const int skl = sk & 7, sset = sk >> 3;                          // its set and slot in the set
     Slab3<D0, WS, R, NMS, LEAN> sl{sm,
                     a,
-                    8 * sw + kl,
-                    kl,
-                    q,
-                    sw,
+                    sk,
+                    skl,
+                    sq,
+                    sset,
                     lane,
                     a.tail,
-                    0x010d000du + (uint32_t)(lane & 1) * 0x02000200u,
+                    0x010d000du + (uint32_t)(sq & 1) * 0x02000200u,
                     PkK{opaque(RNEG127), opaque(R0), opaque(C510), opaque(a.rmm), opaque(a.coff), opaque(0x03000300u),
                         opaque(0x040c000cu)},
                     opaque(a.nmsf),
                     Vg,
-                    (uint32_t)(4 * (q >> 1)),
-                    (uint32_t)(2 * q),
-                    (uint32_t)(((q >> 1) * 8 + kl) * 16 + (q & 1) * 8),
-                    (uint32_t)((8 * GG::MP + kl) * 16 + 4 * (q >> 1)),
-                    (uint32_t)(((4 + (q >> 2)) * 8 + kl) * 16 + (q & 3) * 4)};
+                    (uint32_t)(4 * (sq >> 1)),
+                    (uint32_t)(2 * sq),
+                    GG::HALF ? (uint32_t)(((4 * (lane & 1) + (sq >> 1)) * 8 + skl) * 16 + (sq & 1) * 8)
+                             : (uint32_t)(((sq >> 1) * 8 + skl) * 16 + (sq & 1) * 8),
+                    (uint32_t)((8 * GG::MP + skl) * 16 + 4 * (sq >> 1)),
+                    (uint32_t)(((4 + (sq >> 2)) * 8 + skl) * 16 + (sq & 3) * 4)};
+    if constexpr (GG::HALF) {
+        sl.h = (uint32_t)(lane & 1);
+        sl.hm = (lane & 1) ? 0xFFFFFFFFu : 0u;
+        sl.mbrd = (uint32_t)(((8 + (sq >> 2)) * 8 + skl) * 16 + (sq & 3) * 4);   // record byte 128 + 4 q
+    }
     auto next = [&](int &u) __attribute__((always_inline)) { u = (u + 1 == a.nw) ? 0 : u + 1; };
     for (int it = 0;; it++) {   // one segment (ET: one iteration per segment)
         if (STAMP) tseg = stamp3();
@@ -1414,7 +1518,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         __syncthreads();   // prologue 1: tables and resident lines in LDS
         if constexpr (ET) {   // codewords 2q (low half) and 2q+1 (high half) of this lane: converged?
             const int valid = min(CW, max(0, batch - wg * CW));
-            const uint32_t conv = (((1u << valid) - 1u) & ~et_sh[0]) >> (2 * q);
+            const uint32_t conv = (((1u << valid) - 1u) & ~et_sh[0]) >> (2 * sq);
             sl.fm = ((conv & 1u) ? 0x0000FFFFu : 0u) | ((conv & 2u) ? 0xFFFF0000u : 0u);
             sl.psel = 0x0c0c0000u | ((conv & 2u) ? 0x0300u : 0x0700u) | ((conv & 1u) ? 0x01u : 0x05u);
             sl.psel_raw = 0x0c0c0000u | ((conv & 2u) ? 0x0100u : 0x0700u) | ((conv & 1u) ? 0x00u : 0x05u);

@@ -500,24 +500,44 @@ int lc_build_plan(const std::vector<uint32_t> &tab, int recw, int nw, int S, int
     struct Acc {
         int res, row;
     };
+    // two lanes per check (first-group degree >= 22, coop3_kernel.h G3::HALF):
+    // instruction j of slab wave w serves slots 4w + 2h, 4w + 2h + 1 in 32-lane
+    // half h, each with its info entries j (lane half 0) and XH + j (lane half 1)
+    const int XH = D0 >= 22 ? ((X + 1) / 2 + 1) / 2 * 2 : 0;
     std::vector<std::vector<Acc>> groups;
-    for (int u = 0; u < nw; u++)
+    auto acc_of = [&](int u, int kk, int j, std::vector<Acc> &g) -> bool {
+        const uint32_t *r = rec_at(u, kk);
+        if (!(r[D0] & COOP_M_ACT) || j >= X) {
+            g.push_back({-1, 0});
+            return true;
+        }
+        const int id = res_id_at(r[j] / 8, cmod(u - 1, nw));
+        if (id < 0) return false;
+        g.push_back({id, (int)(r[j] % 8)});
+        return true;
+    };
+    for (int u = 0; u < nw; u++) {
+        if (XH > 0) {
+            for (int w = 0; w < S / 4; w++)
+                for (int hh = 0; hh < 2; hh++)
+                    for (int j = 0; j < XH; j++) {
+                        std::vector<Acc> g;
+                        for (int i = 0; i < 2; i++)
+                            if (!acc_of(u, 4 * w + 2 * hh + i, j, g) || !acc_of(u, 4 * w + 2 * hh + i, XH + j, g))
+                                return lc_fail(__LINE__);
+                        groups.push_back(g);
+                    }
+            continue;
+        }
         for (int w = 0; w < S / 8; w++)
             for (int hh = 0; hh < 2; hh++)
                 for (int j = 0; j < X; j++) {
                     std::vector<Acc> g;
-                    for (int i = 0; i < 4; i++) {
-                        const uint32_t *r = rec_at(u, 8 * w + 4 * hh + i);
-                        if (!(r[D0] & COOP_M_ACT)) {
-                            g.push_back({-1, 0});
-                            continue;
-                        }
-                        const int id = res_id_at(r[j] / 8, cmod(u - 1, nw));
-                        if (id < 0) return lc_fail(__LINE__);
-                        g.push_back({id, (int)(r[j] % 8)});
-                    }
+                    for (int i = 0; i < 4; i++)
+                        if (!acc_of(u, 8 * w + 4 * hh + i, j, g)) return lc_fail(__LINE__);
                     groups.push_back(g);
                 }
+    }
     auto pos_of = [&](const Acc &a) { return a.res < 0 ? 0 : (a.row ^ rs[a.res].z); };
     // extra LDS cycles of one group: the most distinct pieces in one position, minus 1
     auto extra = [&](const std::vector<Acc> &g) -> int {

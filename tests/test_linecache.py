@@ -41,19 +41,22 @@ def test_dvbs2shape_r3_4_plan_fits_and_replays():
     assert lc is not None and 2 <= lc["slots"] <= lc["max_slots"] == 784
 
 
-@pytest.mark.parametrize("name,slots", [("dvbs2shape_r5_6", 960), ("dvbs2_r8_9", 912), ("dvbs2_r9_10", 896)])
+@pytest.mark.parametrize("name,slots", [("dvbs2shape_r5_6", 944), ("dvbs2_r8_9", 896), ("dvbs2_r9_10", 896)])
 def test_degree_22_to_30_plans_fit_and_replay(name, slots):
     """First-group degree 22 / 27 / 30 (the shaped r5/6, the reference's
     r8/9 and r9/10: 20 .. 28 information edges per check, S = 16 windows at
     plan distance 2, 3 / 4 line loads per lane group and period): ~700 .. 840
     lines live at once, so the plan needs the packed chains, the slot
-    elimination and -- for r9/10 -- its one-hold ejections to fit the kernel's
-    line cache; it replays, and the swizzle spreads the bank groups."""
+    elimination and its one-hold ejections to fit the kernel's line cache
+    (r06: 944 / 896 / 896 slots beside the two-lanes-per-check kernel's
+    160-B message records); it replays, and the swizzle spreads the bank
+    groups of the two-lane accesses (instruction j of a slab wave: 2 slots x
+    info entries j and XH + j per 32-lane half)."""
     lc = Code(name).coop3_line_cache()
     assert lc is not None and 2 <= lc["slots"] <= lc["max_slots"] == slots
     assert 0 < lc["epilogue"] <= lc["prologue"] < lc["slots"]
     b = Code(name).coop3_lc_banks()
-    assert b["swizzled"] < 0.05 * b["plain"]
+    assert b["swizzled"] < 0.1 * b["plain"]
 
 
 @pytest.mark.parametrize("name", ["576x288", "1944x972"])

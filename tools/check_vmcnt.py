@@ -104,7 +104,9 @@ def counts(name):
     m = WS_NAME.search(name)
     d0, ws = (int(m.group(1)), int(m.group(2))) if m else (7, 6)
     nld = (d0 - 2 + 7) // 8
-    mp = 2 * ((d0 + 7) // 8 + 1)                            # message pieces per check (G3::MP)
+    half = d0 >= 22                                          # two lanes per check: 4 slab waves of 4 slots
+    mp = 10 if half else 2 * ((d0 + 7) // 8 + 1)            # message pieces per check (G3::MP)
+    ws = 2 if half else ws                                   # the memory wave's 8-slot sets (G3::NSET)
     ngi, nsi = (8 * (mp + 1) + 63) // 64, (mp + 2 + 7) // 8   # gather / store instructions per 8-slot set
     return ((2 * nld + ngi + nsi) * ws, (3 * nld + ngi + 2 * nsi) * ws,
             "L" * (nld * ws) + "G" * (ngi * ws) + "S" * ((nld + nsi) * ws))
@@ -167,8 +169,8 @@ def main():
             print("check_vmcnt: " + e, file=sys.stderr)
         return 1
     print("check_vmcnt: ok (%d memory-wave periods checked: (2 NLD + NGI + NSI) WS vector-memory ops in order, "
-          "vmcnt((3 NLD + NGI + 2 NSI) WS); degree 7: WS 6, NLD 1; 10: WS 4, NLD 1; 14: WS 4, NLD 2; 22: WS 2, "
-          "NLD 3, NGI = NSI = 2; 27, 30: WS 2, NLD 4, NGI = NSI = 2)" % n)
+          "vmcnt((3 NLD + NGI + 2 NSI) WS); degree 7: WS 6, NLD 1; 10: WS 4, NLD 1; 14: WS 4, NLD 2; 22: 2 sets, "
+          "NLD 3, NGI = NSI = 2; 27, 30: 2 sets, NLD 4, NGI = NSI = 2)" % n)
     return 0
 
 
