@@ -190,6 +190,9 @@ struct G3 {
 #define LDPC_C3_CHAIN_SKIP 0     // the chain skips a window's trailing pass-through steps (inactive slots: the
                                  // plan fills ~44.9 of r1/2's 48), their count in slot 0's meta bits 28..30
 #endif
+#ifndef LDPC_C3_HALF_KA
+#define LDPC_C3_HALF_KA 1        // HALF, fixed iterations: info offsets kept pre -> post, records read a period ahead
+#endif
 #ifndef LDPC_C3_PRE_CHUNK_X
 #define LDPC_C3_PRE_CHUNK_X 8    // pres of checks with >= this many info edges: stage-major chunks, two min chains
 #endif
@@ -262,7 +265,7 @@ struct Coop3Args {
 
 // LEAN (early termination at degree 14: VGPRs): |c| is not kept from pre to
 // post but recomputed there (abs_sat / abs_r of c, 2 VALU per edge)
-template <int D0, bool LEAN = false>
+template <int D0, bool LEAN = false, bool KA = G3<D0>::KEEP_AD>
 struct St3 {                          // one window's state from pre to post (R / C pairs)
     static constexpr int X = D0 - 2, XL = G3<D0>::XH, NW = G3<D0>::NW;   // (XL: this lane's info edges)
     uint32_t c[XL + 1];               // contributions (info, o); tail: new V
@@ -271,7 +274,7 @@ struct St3 {                          // one window's state from pre to post (R 
                                       // tail: mn1 = MA0, mn2 = MB, mat = MA1 ..
     uint32_t mat[NW > 1 ? NW - 1 : 1];
     uint32_t xs;                      // the slot's chain step: u16 index of its x input in xo[buf]
-    uint32_t ad[G3<D0>::KEEP_AD ? XL : 1];   // the info edges' pair addresses in the line cache (pre reads, post
+    uint32_t ad[KA ? XL : 1];         // the info edges' pair addresses in the line cache (pre reads, post
                                       // writes; !KEEP_AD: the post re-reads them from the window's records)
     uint32_t v[X > 8 ? 1 : X];        // FZ (early termination): the info edges' V as read (R pairs; X > 8:
                                       // re-read from LDS by the post, Slab3::FZ_REREAD)
@@ -314,11 +317,11 @@ struct Rec<D0, true> {
     LDPC_DEV uint32_t w(int i) const { return i == G::W_X ? wx : i == G::W_O ? wo : i == G::W_META ? meta : e[i]; }
 };
 // what a pre reads from LDS
-template <int D0>
+template <int D0, bool KA = G3<D0>::KEEP_AD>
 struct PreIn {
     static constexpr int X = D0 - 2, XL = G3<D0>::XH, NW = G3<D0>::NW;
     uint32_t v[XL + 1];               // raw V dwords (info edges from the line cache, the o edge from In)
-    uint32_t ad[G3<D0>::KEEP_AD ? XL : 1];   // the info pairs' byte offsets in the line cache
+    uint32_t ad[KA ? XL : 1];         // the info pairs' byte offsets in the line cache
     uint32_t ma[NW], mb;              // old message record of this pair (MA0 .. MA(NW-1), MB; HALF: this half's)
     uint32_t meta, wx, wo;            // record words W_META, W_X, W_O
 };
@@ -330,13 +333,14 @@ LDPC_DEV uint32_t old_msg2(const uint32_t (&MA)[NMA], const MsgTab &t, const PkK
     return old_msg<J & 7>(MA[J >> 3], t, K.m3, K.c4);
 }
 
-template <int D0, int WS, int R, bool NMS = false, bool LEAN = false>
+template <int D0, int WS, int R, bool NMS = false, bool LEAN = false, bool KA_ = G3<D0>::KEEP_AD>
 struct Slab3 {
     using SM = Smem3<D0, WS, R>;
     using G = G3<D0>;
-    using St = St3<D0, LEAN>;
+    static constexpr bool KA = KA_;   // info offsets kept from pre to post, the next pre's records read a period ahead
+    using St = St3<D0, LEAN, KA>;
     using RecT = Rec<D0>;
-    using In = PreIn<D0>;
+    using In = PreIn<D0, KA>;
     static constexpr int S = SM::S, X = G::X, XL = G::XH;   // XL: this lane's info edges (HALF: half of them)
     static constexpr int SX = G::HALF ? 14 : X;           // code slot of the x edge
     static constexpr int SO = G::HALF ? 15 : D0 - 1;      // code slot of the o edge
@@ -397,7 +401,7 @@ struct Slab3 {
     LDPC_DEV void read_pre(int ib, const RecT &rc, In &in) const
     {
         const char *inb = (const char *)&sm.in[w][ib];
-        if constexpr (G::KEEP_AD) {
+        if constexpr (KA) {
 #pragma unroll
             for (int j = 0; j < XL; j++) in.ad[j] = rc.w(j) + lwr;
         }
@@ -464,7 +468,7 @@ struct Slab3 {
         uint32_t v[XL + 1];
 #pragma unroll
         for (int j = 0; j <= XL; j++) v[j] = unpack_v(in.v[j], usel);
-        if constexpr (G::KEEP_AD) {
+        if constexpr (KA) {
 #pragma unroll
             for (int j = 0; j < XL; j++) s.ad[j] = in.ad[j];
         }
@@ -677,9 +681,9 @@ struct Slab3 {
         // LDS round trip, not one per edge: r05o stamps, degree 30, post 4264 of
         // a 6777-cycle period with one ds_read_b32 per edge)
         RecT rp;
-        if constexpr (!G::KEEP_AD) rp = read_rec(g);
+        if constexpr (!KA) rp = read_rec(g);
         auto ad_of = [&](int, const St &st, int j) __attribute__((always_inline)) -> uint32_t {
-            if constexpr (G::KEEP_AD)
+            if constexpr (KA)
                 return st.ad[j];
             else
                 return rp.w(j) + lwr;
@@ -1463,13 +1467,19 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     // "Two waves per SIMD", item 4)
     if (a.slab_prio == 1 && wave > CHW) __builtin_amdgcn_s_setprio(1);
     constexpr bool LEAN = (ET && GG::XH > 8) || GG::XH > 16 || GG::HALF;   // HALF: |c| recomputed in the post (VGPRs)
+    // HALF: the info offsets kept from pre to post and the next pre's records
+    // read a period ahead where the VGPRs allow (not the early-termination
+    // kernels: their syndrome code's registers)
+    // (same box, r06g: shaped r5/6 37.94 vs 38.55 ms re-reading; r9/10 28.37
+    // vs 28.26, so degree 22 only)
+    constexpr bool KA = GG::KEEP_AD || (LDPC_C3_HALF_KA && GG::HALF && !ET && GG::XH <= 10);
     // lanes: one lane per check, lane = 8 slot + pair (slot k = 8 sw + kl in
     // set sw); HALF: lane = 16 slot + 2 pair + half (slot k = 4 sw + kls,
     // in set k >> 3 at k & 7)
     const int sk = GG::HALF ? 4 * sw + (lane >> 4) : 8 * sw + kl;   // this lane's slot
     const int sq = GG::HALF ? (lane >> 1) & 7 : q;                  // its codeword pair
     const int skl = sk & 7, sset = sk >> 3;                          // its set and slot in the set
-    Slab3<D0, WS, R, NMS, LEAN> sl{sm,
+    Slab3<D0, WS, R, NMS, LEAN, KA> sl{sm,
                     a,
                     sk,
                     skl,
@@ -1523,9 +1533,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             sl.psel = 0x0c0c0000u | ((conv & 2u) ? 0x0300u : 0x0700u) | ((conv & 1u) ? 0x01u : 0x05u);
             sl.psel_raw = 0x0c0c0000u | ((conv & 2u) ? 0x0100u : 0x0700u) | ((conv & 1u) ? 0x00u : 0x05u);
         }
-        St3<D0, LEAN> st[NS];
+        St3<D0, LEAN, KA> st[NS];
         __syncthreads();   // prologue 1b: the memory wave's first gathers landed
-        PreIn<D0> in;
+        PreIn<D0, KA> in;
         // records of the next pre's window, read a period ahead (!KEEP_AD: read
         // by the pre's period itself -- the VGPRs go to the window states)
         Rec<D0> rcn = sl.read_rec(1 % a.nw);
@@ -1562,8 +1572,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             if (STAMP) tx = stampL();
             const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
             const bool fast = !GU && uA != a.tail && uB != a.tail;
-            PreIn<D0> in;
-            St3<D0, LEAN> &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
+            PreIn<D0, KA> in;
+            St3<D0, LEAN, KA> &sp = st[(s + NS - 1) % NS], &sn = st[(s + 1) % NS];
             unsigned long long t1 = 0, t2 = 0, t3 = 0;
             // pre first only at plan distance 2 (same box, r05u: slab waves 1 ..
             // of the distance-1 kernels pre first -- r2/3 39.48 vs 38.98 ms, r1/2
@@ -1581,12 +1591,12 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 // there, and wave 0 keeps posting first)
                 uint2 xe = make_uint2(0, 0);
                 if (LDPC_C3_XEARLY) xe = sl.read_x_raw(p - 1, sp);   // x issued first: it lands with the pre's inputs
-                sl.read_pre((s + 1) % NI, GG::KEEP_AD ? rcn : sl.read_rec(p + 1), in);
-                if constexpr (GG::KEEP_AD) rcn = sl.read_rec(p + 2);   // (the next period's pre, either order)
+                sl.read_pre((s + 1) % NI, KA ? rcn : sl.read_rec(p + 1), in);
+                if constexpr (KA) rcn = sl.read_rec(p + 2);   // (the next period's pre, either order)
                 sl.template pre<false, ET>(p + 1, in, sn);
                 if (STAMP) t1 = stampL();
                 if (stag && fair) __builtin_amdgcn_s_setprio(P1);
-                const uint32_t xr = LDPC_C3_XEARLY ? Slab3<D0, WS, R, NMS, LEAN>::x_of(xe) : sl.read_x(p - 1, sp);
+                const uint32_t xr = LDPC_C3_XEARLY ? Slab3<D0, WS, R, NMS, LEAN, KA>::x_of(xe) : sl.read_x(p - 1, sp);
                 if (STAMP) {
                     asm volatile("" ::"v"(xr));
                     t2 = stampL();
@@ -1604,9 +1614,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                         t2 = stampL();
                     }
                     sl.template post<false, ET, MP1>(p - 1, xr, sp);
-                    sl.read_pre((s + 1) % NI, GG::KEEP_AD ? rcn : sl.read_rec(p + 1), in);
+                    sl.read_pre((s + 1) % NI, KA ? rcn : sl.read_rec(p + 1), in);
                 }
-                if constexpr (GG::KEEP_AD) rcn = sl.read_rec(p + 2);
+                if constexpr (KA) rcn = sl.read_rec(p + 2);
                 if (STAMP) t1 = stampL();
                 if (fair) __builtin_amdgcn_s_setprio(P1);
                 sl.template pre<false, ET, MP2>(p + 1, in, sn);
@@ -1620,8 +1630,8 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                         sl.template post<false, ET>(p - 1, xr, sp);
                 }
                 if (STAMP) t1 = t2 = t3 = stampL();
-                if (dpr) sl.read_pre((s + 1) % NI, GG::KEEP_AD ? rcn : sl.read_rec(p + 1), in);
-                if constexpr (GG::KEEP_AD) rcn = sl.read_rec(p + 2);
+                if (dpr) sl.read_pre((s + 1) % NI, KA ? rcn : sl.read_rec(p + 1), in);
+                if constexpr (KA) rcn = sl.read_rec(p + 2);
                 if (dpr) {
                     if (uB == a.tail)
                         sl.template pre<true, ET>(p + 1, in, sn);
