@@ -237,12 +237,6 @@ static void coop3_records(const Coop3Host &ho, const LcPlan &lp, int k, std::vec
             rec[W_X] = (src[X] - (uint32_t)k) | xi << 16;
             rec[W_O] = (src[D0 - 1] - (uint32_t)k) | (step * 2 * NP * 16) << 16;              // + cst offset
             rec[W_META] = src[D0];
-            if (kk == 0) {   // slot 0: the window's trailing pass-through chain steps (<= 7; LDPC_C3_CHAIN_SKIP)
-                int act = 0;
-                for (int k2 = 0; k2 < S; k2++)
-                    act += (ho.pl.tab[((size_t)u * S + k2) * RECW + D0] & COOP_M_ACT) ? 1 : 0;
-                if (S - act <= 7 && act > 0) rec[W_META] |= (uint32_t)(S - act) << 28;
-            }
             // lane group kk's line ops (LcPlan::ops, S NLD per period: op sub * S + kk)
             for (int sub = 0; sub < NLD; sub++) {
                 const size_t o = (size_t)u * S * NLD + (size_t)sub * S + kk;

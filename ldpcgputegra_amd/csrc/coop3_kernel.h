@@ -186,10 +186,6 @@ struct G3 {
                                  // the post-first waves 1, 2 issuing their pre's reads beside the x read
                                  // 34.40, the memory wave's gather-index reads before its loads 34.06)
 #endif
-#ifndef LDPC_C3_CHAIN_SKIP
-#define LDPC_C3_CHAIN_SKIP 0     // the chain skips a window's trailing pass-through steps (inactive slots: the
-                                 // plan fills ~44.9 of r1/2's 48), their count in slot 0's meta bits 28..30
-#endif
 #ifndef LDPC_C3_HALF_KA
 #define LDPC_C3_HALF_KA 1        // HALF, fixed iterations: info offsets kept pre -> post, records read a period ahead
 #endif
@@ -842,7 +838,7 @@ struct Slab3 {
 // its output goes to position k+1, so after step 8j+6 positions 0..7 hold the
 // inputs of steps 8j .. 8j+7: the x inputs post needs, stored as one uint4.
 template <int WS, int R, int B0, int B1, bool NMS = false, typename SMT>
-LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4], uint32_t npv = 0)
+LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
 {
     const uint4 *cp = &sm.cst[buf][0][c & 1][c >> 1];
     constexpr int KST = 2 * NP;       // uint4 between steps
@@ -853,27 +849,6 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4], uint32_t 
     };
 #pragma unroll
     for (int i = 0; i < 8; i++) kq[B0 & 1][i] = cp[(B0 * 8 + i) * KST];
-    // step J of a block (position J -> J + 1)
-    auto step = [&](auto jc, const uint4 (&kb)[8]) __attribute__((always_inline)) {
-        constexpr int J = decltype(jc)::value;
-        uint32_t tmp;
-        if constexpr (J % 2 == 0) {
-            if constexpr (NMS) C3_STEP_SAME_NMS(w[J / 2], kb[J]);
-            else C3_STEP_SAME(w[J / 2], kb[J]);
-        } else {
-            if constexpr (NMS) C3_STEP_CROSS_NMS(w[J / 2], w[(J / 2 + 1) & 3], kb[J]);
-            else C3_STEP_CROSS(w[J / 2], w[(J / 2 + 1) & 3], kb[J]);
-        }
-    };
-    // LDPC_C3_CHAIN_SKIP: the last block of a window with RR real steps (the
-    // rest pass-through: Y' = Y): their x inputs, then the last output
-    // (position RR) moved to position 0, the next window's first input
-    auto partial = [&](auto rc, int b, const uint4 (&kb)[8]) __attribute__((always_inline)) {
-        constexpr int RR = decltype(rc)::value;
-        static_for<0, RR>([&](auto jc) __attribute__((always_inline)) { step(jc, kb); });
-        put_x(b, w);
-        w[0] = (RR & 1) ? w[RR >> 1] >> 16 : w[RR >> 1];
-    };
 #pragma unroll
     for (int b = B0; b < B1; b++) {
         if (b + 1 < B1) {
@@ -881,21 +856,6 @@ LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4], uint32_t 
             for (int i = 0; i < 8; i++) kq[(b + 1) & 1][i] = cp[((b + 1) * 8 + i) * KST];
         }
         uint32_t tmp;
-        if (LDPC_C3_CHAIN_SKIP && b == B1 - 1) {
-            const uint32_t np = __builtin_amdgcn_readfirstlane(npv >> 28) & 7u;   // trailing pass-through steps
-            if (np != 0) {
-                switch (np) {
-                case 1: partial(std::integral_constant<int, 7>{}, b, kq[b & 1]); break;
-                case 2: partial(std::integral_constant<int, 6>{}, b, kq[b & 1]); break;
-                case 3: partial(std::integral_constant<int, 5>{}, b, kq[b & 1]); break;
-                case 4: partial(std::integral_constant<int, 4>{}, b, kq[b & 1]); break;
-                case 5: partial(std::integral_constant<int, 3>{}, b, kq[b & 1]); break;
-                case 6: partial(std::integral_constant<int, 2>{}, b, kq[b & 1]); break;
-                default: partial(std::integral_constant<int, 1>{}, b, kq[b & 1]); break;
-                }
-                continue;
-            }
-        }
         if constexpr (NMS) {
             C3_STEP_SAME_NMS(w[0], kq[b & 1][0]);
             C3_STEP_CROSS_NMS(w[0], w[1], kq[b & 1][1]);
@@ -1196,9 +1156,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             if (STAMP && it == 0) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
                 if (STAMP) tx = stamp3();
-                if (p < G && cl)
-                    chain_window3<WS, R, 0, NB, NMS>(sm, p & 1, c, w4,
-                                                      LDPC_C3_CHAIN_SKIP ? sm.tab[p & (TQ - 1)][0][GG::W_META] : 0u);
+                // (skipping a window's trailing pass-through steps -- the plan
+                // fills ~44.9 of r1/2's 48 slots -- measured -0.3 % on one box
+                // and +0.1 % on another, r06c / r06g: not kept)
+                if (p < G && cl) chain_window3<WS, R, 0, NB, NMS>(sm, p & 1, c, w4);
                 if (STAMP) sP[0] += stamp3() - tx;
                 stage(un, (p + KAHEAD) & (TQ - 1));
                 un = (un + 1 == a.nw) ? 0 : un + 1;
@@ -1580,6 +1541,9 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             // 36.79 vs 35.14: a wave that waits for its chain inputs late keeps
             // the partner SIMD's chain / memory wave waiting on the barrier)
             const bool stag = LDPC_C3_STAGGER && WS == 6 && wave > CHW;
+            // (WS = 4 at plan distance 1, r2/3 and the shaped r3/4: slab waves 1
+            // .. 3 -- no distance-2 pair -- pre first with the x read early
+            // measured 2.4 % slower, r06k)
             const bool prefirst = fast && (GG::DIST == 2 || stag);
             if (prefirst) {
                 if (stag && fair) __builtin_amdgcn_s_setprio(P0);
