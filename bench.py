@@ -34,7 +34,9 @@ def source_hash():
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 10; f32: 400 -- a 0.05 ms step, so that the host's fixed "
+                         "synchronisation cost around the timed region stays below 1 %%)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--dtype", default="i8", choices=("i8", "f32"),
                     help="i8: configs[2] (default); f32: configs[1], float min-sum (defaults 648x324, batch 1024, 20 it)")
@@ -60,6 +62,8 @@ def parse():
         a.batch = 1024 if f32 else 4096
     if a.iters is None:
         a.iters = 20 if f32 else 50
+    if a.steps is None:
+        a.steps = 400 if f32 and not a.mixed else 10
     return a
 
 
@@ -515,20 +519,33 @@ def main():
         step()
     torch.cuda.synchronize()
     counts.zero_()
-    dec.profile(True)
+    # The kernel's average launch duration, from HIP events over the timed
+    # region.  When a step is ONE launch (the float edge-parallel kernel, error
+    # count fused into its epilogue) a single event pair brackets the whole
+    # region: per-launch event pairs cost ~7.5 us of GPU time per 46 us step
+    # (profiles/r06l_f32_events.txt), which would inflate the step they time.
+    # Otherwise (int8: decode + count launches) an event pair per decode launch.
+    region = f32 and dec.last_kernel == "ldsep"
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    dec.profile(not region)
     dec.kernel_time(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(a.steps):
         step()
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = el_local = time.perf_counter() - t0
     kms, launches = dec.kernel_time(reset=True)
     dec.profile(False)
+    if region:
+        kms, launches = ev0.elapsed_time(ev1), a.steps
 
     be_l, fe_l = counts.tolist()
     el, be, fe, _ = reduce_results(el, be_l, fe_l, B * a.steps, device="cuda")
@@ -623,6 +640,8 @@ def main():
                 "frac": round(achieved / lds_peak, 4), "traffic": traffic, "traffic_source": traffic_note,
                 "hbm_achieved": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic else None,
                 "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": alg_bytes,
+                "kernel_ms_source": ("one HIP event pair over the timed region / launches (one launch per step)"
+                                     if region else "HIP event pair per decode launch, averaged"),
                 "note": ("algorithmic bytes are on-chip traffic (V in LDS, messages in VGPRs: neither leaves the CU); "
                          "bound in practice: VALU issue at one wave per SIMD (DPP butterflies per check, DESIGN.md)"
                          if dec.last_kernel == "ldsep" else

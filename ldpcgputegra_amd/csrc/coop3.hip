@@ -47,11 +47,12 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
             fprintf(stderr, "  chain %d: busy %.0f steps %.0f | ET round 0 %.1f, full syndromes %.1f (%.4f per period)\n",
                     w, x[0], x[1], x[2], x[3], x[6]);
         else if (w == WS + 1)
-            fprintf(stderr, "  memory %d: busy %.0f | issue %.0f vmcnt %.0f\n", w, x[0], x[2], x[0] - x[2]);
+            fprintf(stderr, "  memory %d: busy %.0f | issue %.0f vmcnt %.0f | last barrier arrival per period %.0f\n", w,
+                    x[0], x[2], x[0] - x[2], x[6]);
         else   // fast periods: x-input wait, post, pre; rest = guarded periods' share and the stamps
-            fprintf(stderr, "  slab %d: busy %.0f | x wait %.0f post %.0f pre %.0f rest %.0f | ET segment prologue %.1f "
-                            "epilogue + syndrome %.1f\n", w, x[0], x[1], x[2], x[3], x[0] - x[1] - x[2] - x[3], x[4],
-                    x[6]);
+            fprintf(stderr, "  slab %d: busy %.0f | x wait %.0f post %.0f pre %.0f rest %.0f | LDS drain at the barrier "
+                            "%.0f | segment prologue + epilogue (+ ET syndrome) %.1f\n", w, x[0], x[1], x[2], x[3],
+                    x[0] - x[1] - x[2] - x[3], x[6], x[4]);
     }
 }
 
@@ -95,6 +96,18 @@ static_assert(SmemOf<7>::v + 512 <= 160 * 1024 && SmemOf<10>::v + 512 <= 160 * 1
                   SmemOf<30>::v + 512 <= 160 * 1024,
               "LDS: the workgroup's Smem3 plus the ET kernel's static words fit 160 KB");
 int g3_lcs(int d0) { return g3_at<LcsOf>(d0); }
+
+// The chain wave's priority (s_setprio level; LDPC_COOP3_PRIO overrides).
+// r1/2 (WS = 6): the chain shares its SIMD with the memory wave only and is
+// the critical wave: 3.  WS = 4 (every other degree): the chain shares SIMD 0
+// with slab wave 0, and at level 3 it took that wave's VALU during its post
+// (r06l stamps, r2/3: slab 0 busy 2397 of a 2615-cycle period, slabs 2 / 3
+// ~1915).  The chain has slack there; levels 0 / 1 / 2 / 3, same box, ms
+// (r06n, profiles/r06n_ab_chain_prio.txt): r1/2 34.76 / 34.77 / 33.16 / 33.18;
+// r2/3 37.29 / 36.24 / 37.86 / 37.87; shaped r3/4 29.42 / 29.50 / 31.78 /
+// 31.81; shaped r5/6 37.53 / 37.85 / 37.85 / 37.86; r8/9 and r9/10 flat
+// (within 0.3 %).
+int coop3_chain_prio(int d0) { return d0 == 10 ? 1 : d0 == 14 || d0 == 22 ? 0 : 3; }
 
 }  // namespace
 
@@ -491,7 +504,7 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.coff = nms ? 0u : (uint32_t)(L.param * 256 + 255) * 0x00010001u;
     a.offp = nms ? 0u : (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
     a.nmsf = nms ? (uint32_t)(L.param & 0xFFFF) * 0x00010001u : 0u;
-    a.prio = env_int3("LDPC_COOP3_PRIO", 1);
+    a.prio = std::min(3, std::max(0, env_int3("LDPC_COOP3_PRIO", coop3_chain_prio(cc.d0))));
     a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 0 none, 1 static (second waves), 2 fair by phase
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups

@@ -963,9 +963,19 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         __syncthreads();
         if (et_sh[0] == 0) return;   // padding columns only
     }
-    // ET (slab waves): sP[3] = segment prologues, sD = epilogues + syndromes;
+    // slab waves: sP[3] = segment prologues + epilogues (+ ET syndromes), sD =
+    // LDS drain at the period barrier;
     // elapsed from the first segment's start, G x segments periods
     unsigned long long sA = 0, sP[4] = {0, 0, 0, 0}, sD = 0, t0 = 0, tx = 0, tseg = 0;
+    // stamps: every wave's barrier arrival per period (double-buffered by
+    // period parity); the memory wave sums the per-period LAST arrival (sD)
+    // (not degrees 10 / 14 nor ET kernels: their stamped waves would spill)
+    constexpr bool ARR = STAMP && !ET && D0 != 10 && D0 != 14;
+    __shared__ uint32_t st_arr[ARR ? 16 : 1];
+    auto arrive = [&](int p, unsigned long long t) __attribute__((always_inline)) {
+        if (ARR) st_arr[(p & 1) * 8 + wave] = (uint32_t)t;   // every lane (same value): no branch before
+                                                               // the barrier (tools/check_vmcnt.py)
+    };
     int nseg = 1;
     // after iteration `it` (ET): syndrome and decision -- every thread,
     // uniform result (true: decode another iteration).  Codewords converged
@@ -1129,7 +1139,14 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 
     if (wave == CHW) {
         // ------------------------------------------------------------ chain wave
-        if (a.prio) __builtin_amdgcn_s_setprio(3);
+        // the chain's wave priority (a.prio, coop3_chain_prio): s_setprio
+        // takes an immediate
+        if (a.prio == 3)
+            __builtin_amdgcn_s_setprio(3);
+        else if (a.prio == 2)
+            __builtin_amdgcn_s_setprio(2);
+        else if (a.prio == 1)
+            __builtin_amdgcn_s_setprio(1);
         constexpr int TABW = S * GG::RECW;   // words per window table
         constexpr int NCH = TABW / 4;   // 16-B chunks per window table
         constexpr int CPL = (NCH + 63) / 64;
@@ -1164,7 +1181,11 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 stage(un, (p + KAHEAD) & (TQ - 1));
                 un = (un + 1 == a.nw) ? 0 : un + 1;
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPL * DPER) : "memory");
-                if (STAMP) sA += stamp3() - tx;
+                if (STAMP) {
+                    const unsigned long long t = stamp3();
+                    sA += t - tx;
+                    arrive(p, t);
+                }
                 __syncthreads();
             }
             __syncthreads();   // epilogue: the slab waves' line writebacks read the cache
@@ -1305,9 +1326,21 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             // tools/check_vmcnt.py (run by __graft_entry__.build) checks the
             // ISA.  The compiler's own waits for the line loads it tracks (it
             // does not see the LDS-DMA gathers) are stricter than needed.
+            unsigned long long txp = 0;   // (stamps) the previous period's start
             auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
                 constexpr int s = decltype(sc_)::value;   // p % NPD
                 if (STAMP) tx = stampL();
+                if (ARR) {   // period p-1's last barrier arrival, from this wave's start of p-1
+                    // one LDS read (lane w: wave w's arrival), a max over lanes
+                    // 0..7 by xor shuffles: no loop or branch, two VGPRs; after
+                    // this period's start stamp, so it is not timed itself
+                    int d = (lane & 7) < WS + 2 ? (int)(st_arr[((p - 1) & 1) * 8 + (lane & 7)] - (uint32_t)txp) : 0;
+                    d = max(d, __shfl_xor(d, 1));
+                    d = max(d, __shfl_xor(d, 2));
+                    d = max(d, __shfl_xor(d, 4));
+                    sD += p >= 1 ? (unsigned long long)max(0, __builtin_amdgcn_readfirstlane(d)) : 0ull;
+                    txp = tx;
+                }
                 uint32_t gix[NST][NGI];
                 uint4 wbd[NST][NLD], std_[NST][NSI];
                 auto loads = [&]() __attribute__((always_inline)) {   // line loads of period p
@@ -1393,7 +1426,11 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 if (STAMP) sP[1] += stampL() - tx;
                 // the gathers of p-1: (NLD + NSI) NST ops of p-1 and (2 NLD + NGI + NSI) NST of p after them
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"((3 * NLD + NGI + 2 * NSI) * NST) : "memory");
-                if (STAMP) sA += stampL() - tx;
+                if (STAMP) {
+                    const unsigned long long t = stampL();
+                    sA += t - tx;
+                    arrive(p, t);
+                }
                 __syncthreads();
                 uS = (uS + 1 == a.nw) ? 0 : uS + 1;
             };
@@ -1605,7 +1642,12 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             }
             if (STAMP) {
                 const unsigned long long t5 = stampL();
+                // the wave's own LDS ops still in flight at its barrier (the
+                // barrier's lgkmcnt(0)): sD
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                sD += stampL() - t5;
                 sA += t5 - tx;
+                arrive(p, t5);
                 if (prefirst) {   // pre first: x wait after it, post, pre
                     sP[0] += t2 - t1;
                     sP[1] += t3 - t2;
@@ -1659,7 +1701,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             }
         }
         const bool more = ET && et_after(it);
-        if (STAMP) sD += stamp3() - tseg;
+        if (STAMP) sP[3] += stamp3() - tseg;
         if (!more) break;
         nseg++;
     }

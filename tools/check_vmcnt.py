@@ -82,7 +82,7 @@ def kind(line):
     return "L"
 
 
-def closes_period(lines, i, reach=8):
+def closes_period(lines, i, reach=12):
     """The wait at line i is followed by an s_barrier within `reach` lines,
     with no vector-memory instruction or branch before it."""
     for l in lines[i + 1:i + 1 + reach]:
