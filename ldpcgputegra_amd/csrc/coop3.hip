@@ -47,8 +47,8 @@ void report_stamps3(const unsigned long long *d, int grid, hipStream_t s)
             fprintf(stderr, "  chain %d: busy %.0f steps %.0f | ET round 0 %.1f, full syndromes %.1f (%.4f per period)\n",
                     w, x[0], x[1], x[2], x[3], x[6]);
         else if (w == WS + 1)
-            fprintf(stderr, "  memory %d: busy %.0f | issue %.0f vmcnt %.0f | last barrier arrival per period %.0f\n", w,
-                    x[0], x[2], x[0] - x[2], x[6]);
+            fprintf(stderr, "  memory %d: busy %.0f | issue %.0f vmcnt %.0f | per period: last wave ready %.0f after the "
+                            "first wave's start, starts spread over %.0f\n", w, x[0], x[2], x[0] - x[2], x[6], x[3]);
         else   // fast periods: x-input wait, post, pre; rest = guarded periods' share and the stamps
             fprintf(stderr, "  slab %d: busy %.0f | x wait %.0f post %.0f pre %.0f rest %.0f | LDS drain at the barrier "
                             "%.0f | segment prologue + epilogue (+ ET syndrome) %.1f\n", w, x[0], x[1], x[2], x[3],
@@ -108,6 +108,16 @@ int g3_lcs(int d0) { return g3_at<LcsOf>(d0); }
 // 31.81; shaped r5/6 37.53 / 37.85 / 37.85 / 37.86; r8/9 and r9/10 flat
 // (within 0.3 %).
 int coop3_chain_prio(int d0) { return d0 == 10 ? 1 : d0 == 14 || d0 == 22 ? 0 : 3; }
+
+// The memory wave's priority (LDPC_COOP3_MPRIO overrides).  r1/2: 2 (r04j:
+// 0.35 % over 0; r06t flat).  WS = 4: it shares SIMD 2 with slab wave 1 and
+// only issues memory ops and LDS copies -- at level 2 it held that slab wave
+// back.  Levels 0 / 1 / 2 / 3, same box, ms (r06t,
+// profiles/r06t_ab_mem_prio.txt): r2/3 36.43 / 36.42 / 36.67 / 36.69; shaped
+// r3/4 29.47 / 29.69 / 29.75 / 29.74; shaped r5/6 35.47 / 37.82 / 37.82 /
+// 37.84; r8/9 31.21 / 31.99 / 31.96 / 31.95; r9/10 27.75 / 28.55 / 28.45 /
+// 28.55.
+int coop3_mem_prio(int d0) { return d0 == 7 ? 2 : 0; }
 
 }  // namespace
 
@@ -505,6 +515,7 @@ int launch_coop3(const DecodeLaunch &L, const CoopCode &cc, hipStream_t s)
     a.offp = nms ? 0u : (uint32_t)(L.param & 0xFFFF) * 0x00010001u;
     a.nmsf = nms ? (uint32_t)(L.param & 0xFFFF) * 0x00010001u : 0u;
     a.prio = std::min(3, std::max(0, env_int3("LDPC_COOP3_PRIO", coop3_chain_prio(cc.d0))));
+    a.mprio = std::min(3, std::max(0, env_int3("LDPC_COOP3_MPRIO", coop3_mem_prio(cc.d0))));
     a.slab_prio = env_int3("LDPC_COOP3_SLAB_PRIO", 2);   // 0 none, 1 static (second waves), 2 fair by phase
     const int grid = L.stride / CW;
     a.remap = (grid % 8) == 0 && env_int3("LDPC_COOP3_REMAP", 1) != 0;   // XCD-aware codeword groups

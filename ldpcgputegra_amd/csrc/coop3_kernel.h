@@ -168,9 +168,6 @@ struct G3 {
 #ifndef LDPC_C3_MSLEEP
 #define LDPC_C3_MSLEEP 4      // memory wave: s_sleep (x 64 cycles) after its line loads, before its LDS burst
 #endif
-#ifndef LDPC_C3_MPRIO
-#define LDPC_C3_MPRIO 2        // memory wave priority (chain wave: 3; same-box A/B: 2 vs 0 -0.35 %)
-#endif
 #ifndef LDPC_C3_STAGGER
 #define LDPC_C3_STAGGER 1        // WS = 6: the second-dispatched slab waves (3 .. 5, beside waves 0 .. 2 on the
                                  // same SIMDs) run the pre of window p+1 before the post of window p-1: the two
@@ -253,7 +250,7 @@ struct Coop3Args {
     // stage's codeword count) when batch_dev is set
     int iter_base, fill;
     const int *batch_dev;
-    int G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio;
+    int G, nw, tail, mrows, n, m, k, x0, remap, prio, slab_prio, mprio;
     uint32_t nmsf;                    // NMS factor per half (value form)
     size_t gstride;                   // bytes between two codeword groups' V
     uint32_t rmm, coff, offp;         // R(msg_max), C(offset) + 255 (R - coff: C form), offset per half (value form)
@@ -971,7 +968,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
     // period parity); the memory wave sums the per-period LAST arrival (sD)
     // (not degrees 10 / 14 nor ET kernels: their stamped waves would spill)
     constexpr bool ARR = STAMP && !ET && D0 != 10 && D0 != 14;
-    __shared__ uint32_t st_arr[ARR ? 16 : 1];
+    __shared__ uint32_t st_arr[ARR ? 16 : 1], st_beg[ARR ? 16 : 1];
+    auto begin = [&](int p, unsigned long long t) __attribute__((always_inline)) {
+        if (ARR) st_beg[(p & 1) * 8 + wave] = (uint32_t)t;
+    };
     auto arrive = [&](int p, unsigned long long t) __attribute__((always_inline)) {
         if (ARR) st_arr[(p & 1) * 8 + wave] = (uint32_t)t;   // every lane (same value): no branch before
                                                                // the barrier (tools/check_vmcnt.py)
@@ -1172,7 +1172,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             __syncthreads();   // prologue 2: constants of window 0 in LDS
             if (STAMP && it == 0) t0 = stamp3();
             for (int p = 0; p <= G; p++) {
-                if (STAMP) tx = stamp3();
+                if (STAMP) {
+                    tx = stamp3();
+                    begin(p, tx);
+                }
                 // (skipping a window's trailing pass-through steps -- the plan
                 // fills ~44.9 of r1/2's 48 slots -- measured -0.3 % on one box
                 // and +0.1 % on another, r06c / r06g: not kept)
@@ -1203,7 +1206,13 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
 
     if (wave == MW) {
         constexpr int NST = GG::NSET;   // the 8-slot sets (= WS but for HALF: 4 slab waves of 4 slots)
-        if (LDPC_C3_MPRIO > 0) __builtin_amdgcn_s_setprio(LDPC_C3_MPRIO);
+        // memory wave priority (a.mprio; r1/2 same-box A/B: 2 vs 0 -0.35 %)
+        if (a.mprio == 3)
+            __builtin_amdgcn_s_setprio(3);
+        else if (a.mprio == 2)
+            __builtin_amdgcn_s_setprio(2);
+        else if (a.mprio == 1)
+            __builtin_amdgcn_s_setprio(1);
         // ------------------------------------------------------------ memory wave
         // Every vector-memory operation of the workgroup, per period p for each
         // slab wave's set of 8 slots (w = 0..NST-1), in this order: the line
@@ -1330,15 +1339,30 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
             auto mperiod = [&](auto sc_, int p) __attribute__((always_inline)) {
                 constexpr int s = decltype(sc_)::value;   // p % NPD
                 if (STAMP) tx = stampL();
-                if (ARR) {   // period p-1's last barrier arrival, from this wave's start of p-1
-                    // one LDS read (lane w: wave w's arrival), a max over lanes
-                    // 0..7 by xor shuffles: no loop or branch, two VGPRs; after
-                    // this period's start stamp, so it is not timed itself
-                    int d = (lane & 7) < WS + 2 ? (int)(st_arr[((p - 1) & 1) * 8 + (lane & 7)] - (uint32_t)txp) : 0;
-                    d = max(d, __shfl_xor(d, 1));
-                    d = max(d, __shfl_xor(d, 2));
-                    d = max(d, __shfl_xor(d, 4));
-                    sD += p >= 1 ? (unsigned long long)max(0, __builtin_amdgcn_readfirstlane(d)) : 0ull;
+                if (ARR) {
+                    // period p-1: the last wave's barrier arrival (ready: its
+                    // LDS ops done) after the first wave's start -> sD, the
+                    // spread of the waves' starts -> sP[2].  Lane w reads wave
+                    // w's stamps; min / max over lanes 0..7 by xor shuffles (no
+                    // loop or branch); after this period's start stamp, so it
+                    // is not timed itself
+                    begin(p, tx);
+                    const bool wl = (lane & 7) < WS + 2;
+                    const uint32_t b0 = st_beg[((p - 1) & 1) * 8 + (lane & 7)];
+                    const uint32_t a0 = st_arr[((p - 1) & 1) * 8 + (lane & 7)];
+                    int e = wl ? (int)(a0 - (uint32_t)txp) : -(1 << 30);   // relative to this wave's start of p-1
+                    int b = wl ? (int)(b0 - (uint32_t)txp) : (1 << 30);
+                    int bm = wl ? b : -(1 << 30);
+#pragma unroll
+                    for (int o = 1; o < 8; o <<= 1) {
+                        e = max(e, __shfl_xor(e, o));
+                        b = min(b, __shfl_xor(b, o));
+                        bm = max(bm, __shfl_xor(bm, o));
+                    }
+                    const int last = __builtin_amdgcn_readfirstlane(e), first = __builtin_amdgcn_readfirstlane(b),
+                              spread = __builtin_amdgcn_readfirstlane(bm) - first;
+                    sD += p >= 1 ? (unsigned long long)max(0, last - first) : 0ull;
+                    sP[2] += p >= 1 ? (unsigned long long)max(0, spread) : 0ull;
                     txp = tx;
                 }
                 uint32_t gix[NST][NGI];
@@ -1427,6 +1451,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 // the gathers of p-1: (NLD + NSI) NST ops of p-1 and (2 NLD + NGI + NSI) NST of p after them
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"((3 * NLD + NGI + 2 * NSI) * NST) : "memory");
                 if (STAMP) {
+                    if (ARR) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // arrival = ready, as the slab waves'
                     const unsigned long long t = stampL();
                     sA += t - tx;
                     arrive(p, t);
@@ -1567,7 +1592,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
         auto period = [&](auto sc_, auto guarded_, int p) __attribute__((always_inline)) {
             constexpr int s = decltype(sc_)::value;   // p % U
             constexpr bool GU = decltype(guarded_)::value;
-            if (STAMP) tx = stampL();
+            if (STAMP) {
+                tx = stampL();
+                begin(p, tx);
+            }
             const bool dpo = p >= 1 && p <= G, dpr = p + 1 < G;
             const bool fast = !GU && uA != a.tail && uB != a.tail;
             PreIn<D0, KA> in;
@@ -1645,9 +1673,10 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 // the wave's own LDS ops still in flight at its barrier (the
                 // barrier's lgkmcnt(0)): sD
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                sD += stampL() - t5;
+                const unsigned long long t6 = stampL();
+                sD += t6 - t5;
                 sA += t5 - tx;
-                arrive(p, t5);
+                arrive(p, t6);   // ready for the barrier: own LDS ops done
                 if (prefirst) {   // pre first: x wait after it, post, pre
                     sP[0] += t2 - t1;
                     sP[1] += t3 - t2;
