@@ -106,8 +106,11 @@ int g3_lcs(int d0) { return g3_at<LcsOf>(d0); }
 // (r06n, profiles/r06n_ab_chain_prio.txt): r1/2 34.76 / 34.77 / 33.16 / 33.18;
 // r2/3 37.29 / 36.24 / 37.86 / 37.87; shaped r3/4 29.42 / 29.50 / 31.78 /
 // 31.81; shaped r5/6 37.53 / 37.85 / 37.85 / 37.86; r8/9 and r9/10 flat
-// (within 0.3 %).
-int coop3_chain_prio(int d0) { return d0 == 10 ? 1 : d0 == 14 || d0 == 22 ? 0 : 3; }
+// (within 0.3 %).  With the memory wave at level 0 (below), levels 0 / 1 / 3
+// (r06u, profiles/r06u_ab_chain_prio.txt): r2/3 36.48 / 36.47 / 38.31; r3/4
+// 29.39 / 29.42 / 32.15; r5/6 35.48 / 37.00 / 37.00; r8/9 31.17 / 31.20 /
+// 31.19; r9/10 27.70 / 27.76 / 27.77 -- level 0 at every WS = 4 degree.
+int coop3_chain_prio(int d0) { return g3_ws(d0) == 6 ? 3 : 0; }
 
 // The memory wave's priority (LDPC_COOP3_MPRIO overrides).  r1/2: 2 (r04j:
 // 0.35 % over 0; r06t flat).  WS = 4: it shares SIMD 2 with slab wave 1 and
@@ -117,7 +120,7 @@ int coop3_chain_prio(int d0) { return d0 == 10 ? 1 : d0 == 14 || d0 == 22 ? 0 : 
 // r3/4 29.47 / 29.69 / 29.75 / 29.74; shaped r5/6 35.47 / 37.82 / 37.82 /
 // 37.84; r8/9 31.21 / 31.99 / 31.96 / 31.95; r9/10 27.75 / 28.55 / 28.45 /
 // 28.55.
-int coop3_mem_prio(int d0) { return d0 == 7 ? 2 : 0; }
+int coop3_mem_prio(int d0) { return g3_ws(d0) == 6 ? 2 : 0; }
 
 }  // namespace
 
