@@ -5,10 +5,11 @@ over windows of <= 32 checks, 8 / 12 information edges per check, two 16-bit
 edge-code words per codeword (96-B message records), 1 / 2 line loads per lane
 group and period -- and first-group degree 22, 27, 30 (the shaped r5/6 of
 configs[4], the reference's r8/9 and r9/10, code/x86/Constantes/64800x7200 /
-64800x6480) -- coop3_decode<22 | 27 | 30, 2, 2>: 2 slab waves over windows of
-16 checks at plan distance 2, 20 / 25 / 28 information edges per check, 3 / 4
-edge-code words (128 / 160-B records), gathers and stores in two instructions
-per slot set, 3 / 4 line loads per lane group and period -- against the oracle
+64800x6480) -- coop3_decode<22 | 27 | 30, 4, 2>: two lanes per check (4 slab
+waves of 4 slots over windows of 16 checks, each lane reducing half of the 20 /
+25 / 28 information edges, a DPP min / sign merge), 160-B message records,
+gathers and stores in two instructions per slot set, 3 / 4 line loads per lane
+group and period -- against the oracle
 (the reference's recurrence, CDecoder_OMS_fixed_SSE.cpp:172-546; NMS
 CDecoder_NMS_fixed_SSE.cpp:188-240; early termination per codeword on the
 posterior hard-decision syndrome after each iteration, SURVEY.md §8(f) row 2 --
@@ -129,3 +130,23 @@ def test_r23_full_batch_fixed_50_sampled_vs_oracle(CODE):
     eh, es, _ = O.decode_i8(t, llr[sel], iters, return_soft=True, threads=O.host_threads())
     assert np.array_equal(s[sel], es)
     assert np.array_equal(h[sel], eh)
+
+
+@pytest.mark.parametrize("CODE", ["dvbs2_r1_2", "dvbs2_r2_3", "dvbs2shape_r5_6"])
+def test_wave_priorities_do_not_change_results(CODE, monkeypatch):
+    """The chain / memory wave priorities (coop3_chain_prio / coop3_mem_prio,
+    overridden by LDPC_COOP3_PRIO / LDPC_COOP3_MPRIO per launch) only reorder
+    issue: every level gives the oracle's soft output, fixed iterations and
+    early termination alike."""
+    t = load_table(CODE)
+    ebn0 = {"dvbs2_r1_2": 1.0}.get(CODE) or EBN0[CODE][0]
+    llr = _llr(CODE, 37, ebn0, 23)
+    eh, es, _ = O.decode_i8(t, llr, 10, return_soft=True, threads=O.host_threads())
+    _, ees, eit = O.decode_i8(t, llr, 30, early_term=True, return_soft=True, threads=O.host_threads())
+    for chain, mem in [(0, 0), (3, 2), (1, 3)]:
+        monkeypatch.setenv("LDPC_COOP3_PRIO", str(chain))
+        monkeypatch.setenv("LDPC_COOP3_MPRIO", str(mem))
+        h, s, _, _ = _run(CODE, llr, 10, default_params())
+        assert np.array_equal(s, es) and np.array_equal(h, eh), (chain, mem)
+        _, s2, its, _ = _run(CODE, llr, 30, default_params(early_term=1))
+        assert np.array_equal(s2, ees) and np.array_equal(its, eit), (chain, mem)
