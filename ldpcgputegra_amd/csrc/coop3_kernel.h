@@ -834,45 +834,89 @@ struct Slab3 {
 // sits at position k % 8 of w (w[i] low / high half = positions 2i, 2i+1) and
 // its output goes to position k+1, so after step 8j+6 positions 0..7 hold the
 // inputs of steps 8j .. 8j+7: the x inputs post needs, stored as one uint4.
-template <int WS, int R, int B0, int B1, bool NMS = false, typename SMT>
+// PF2: the constants read two blocks of 8 steps ahead instead of one (degree
+// 10 only: r2/3 36.38 -> 35.79 ms same box; r1/2 +0.6 %, degrees 14 .. 30
+// within 0.5 %, r06ac / r06ad)
+template <int WS, int R, int B0, int B1, bool NMS = false, bool PF2 = false, typename SMT>
 LDPC_DEV void chain_window3(SMT &sm, int buf, int c, uint32_t (&w)[4])
 {
     const uint4 *cp = &sm.cst[buf][0][c & 1][c >> 1];
     constexpr int KST = 2 * NP;       // uint4 between steps
-    uint4 kq[2][8];
-    // the x inputs of steps 8b .. 8b+7 (positions 0..7 of w) -> xo
-    auto put_x = [&](int b, const uint32_t (&v)[4]) __attribute__((always_inline)) {
-        sm.xo[buf][b][c] = make_uint4(v[0], v[1], v[2], v[3]);
-    };
+    if constexpr (PF2) {
+        uint4 kq[3][8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) kq[B0 & 1][i] = cp[(B0 * 8 + i) * KST];
+        for (int i = 0; i < 8; i++) kq[B0 % 3][i] = cp[(B0 * 8 + i) * KST];
+        if (B0 + 1 < B1)
 #pragma unroll
-    for (int b = B0; b < B1; b++) {
-        if (b + 1 < B1) {
+            for (int i = 0; i < 8; i++) kq[(B0 + 1) % 3][i] = cp[((B0 + 1) * 8 + i) * KST];
+        auto put_x = [&](int b, const uint32_t (&v)[4]) __attribute__((always_inline)) {
+            sm.xo[buf][b][c] = make_uint4(v[0], v[1], v[2], v[3]);
+        };
 #pragma unroll
-            for (int i = 0; i < 8; i++) kq[(b + 1) & 1][i] = cp[((b + 1) * 8 + i) * KST];
+        for (int b = B0; b < B1; b++) {
+            if (b + 2 < B1) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) kq[(b + 2) % 3][i] = cp[((b + 2) * 8 + i) * KST];
+            }
+            uint32_t tmp;
+            if constexpr (NMS) {
+                C3_STEP_SAME_NMS(w[0], kq[b % 3][0]);
+                C3_STEP_CROSS_NMS(w[0], w[1], kq[b % 3][1]);
+                C3_STEP_SAME_NMS(w[1], kq[b % 3][2]);
+                C3_STEP_CROSS_NMS(w[1], w[2], kq[b % 3][3]);
+                C3_STEP_SAME_NMS(w[2], kq[b % 3][4]);
+                C3_STEP_CROSS_NMS(w[2], w[3], kq[b % 3][5]);
+                C3_STEP_SAME_NMS(w[3], kq[b % 3][6]);
+                put_x(b, w);
+                C3_STEP_CROSS_NMS(w[3], w[0], kq[b % 3][7]);
+            } else {
+                C3_STEP_SAME(w[0], kq[b % 3][0]);
+                C3_STEP_CROSS(w[0], w[1], kq[b % 3][1]);
+                C3_STEP_SAME(w[1], kq[b % 3][2]);
+                C3_STEP_CROSS(w[1], w[2], kq[b % 3][3]);
+                C3_STEP_SAME(w[2], kq[b % 3][4]);
+                C3_STEP_CROSS(w[2], w[3], kq[b % 3][5]);
+                C3_STEP_SAME(w[3], kq[b % 3][6]);
+                put_x(b, w);
+                C3_STEP_CROSS(w[3], w[0], kq[b % 3][7]);
+            }
         }
-        uint32_t tmp;
-        if constexpr (NMS) {
-            C3_STEP_SAME_NMS(w[0], kq[b & 1][0]);
-            C3_STEP_CROSS_NMS(w[0], w[1], kq[b & 1][1]);
-            C3_STEP_SAME_NMS(w[1], kq[b & 1][2]);
-            C3_STEP_CROSS_NMS(w[1], w[2], kq[b & 1][3]);
-            C3_STEP_SAME_NMS(w[2], kq[b & 1][4]);
-            C3_STEP_CROSS_NMS(w[2], w[3], kq[b & 1][5]);
-            C3_STEP_SAME_NMS(w[3], kq[b & 1][6]);
-            put_x(b, w);
-            C3_STEP_CROSS_NMS(w[3], w[0], kq[b & 1][7]);
-        } else {
-            C3_STEP_SAME(w[0], kq[b & 1][0]);          // pos 0 -> 1
-            C3_STEP_CROSS(w[0], w[1], kq[b & 1][1]);   // pos 1 -> 2
-            C3_STEP_SAME(w[1], kq[b & 1][2]);          // 2 -> 3
-            C3_STEP_CROSS(w[1], w[2], kq[b & 1][3]);   // 3 -> 4
-            C3_STEP_SAME(w[2], kq[b & 1][4]);          // 4 -> 5
-            C3_STEP_CROSS(w[2], w[3], kq[b & 1][5]);   // 5 -> 6
-            C3_STEP_SAME(w[3], kq[b & 1][6]);          // 6 -> 7
-            put_x(b, w);
-            C3_STEP_CROSS(w[3], w[0], kq[b & 1][7]);   // 7 -> 0 (the next block's first input)
+    } else {
+        uint4 kq[2][8];
+        // the x inputs of steps 8b .. 8b+7 (positions 0..7 of w) -> xo
+        auto put_x = [&](int b, const uint32_t (&v)[4]) __attribute__((always_inline)) {
+            sm.xo[buf][b][c] = make_uint4(v[0], v[1], v[2], v[3]);
+        };
+#pragma unroll
+        for (int i = 0; i < 8; i++) kq[B0 & 1][i] = cp[(B0 * 8 + i) * KST];
+#pragma unroll
+        for (int b = B0; b < B1; b++) {
+            if (b + 1 < B1) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) kq[(b + 1) & 1][i] = cp[((b + 1) * 8 + i) * KST];
+            }
+            uint32_t tmp;
+            if constexpr (NMS) {
+                C3_STEP_SAME_NMS(w[0], kq[b & 1][0]);
+                C3_STEP_CROSS_NMS(w[0], w[1], kq[b & 1][1]);
+                C3_STEP_SAME_NMS(w[1], kq[b & 1][2]);
+                C3_STEP_CROSS_NMS(w[1], w[2], kq[b & 1][3]);
+                C3_STEP_SAME_NMS(w[2], kq[b & 1][4]);
+                C3_STEP_CROSS_NMS(w[2], w[3], kq[b & 1][5]);
+                C3_STEP_SAME_NMS(w[3], kq[b & 1][6]);
+                put_x(b, w);
+                C3_STEP_CROSS_NMS(w[3], w[0], kq[b & 1][7]);
+            } else {
+                C3_STEP_SAME(w[0], kq[b & 1][0]);          // pos 0 -> 1
+                C3_STEP_CROSS(w[0], w[1], kq[b & 1][1]);   // pos 1 -> 2
+                C3_STEP_SAME(w[1], kq[b & 1][2]);          // 2 -> 3
+                C3_STEP_CROSS(w[1], w[2], kq[b & 1][3]);   // 3 -> 4
+                C3_STEP_SAME(w[2], kq[b & 1][4]);          // 4 -> 5
+                C3_STEP_CROSS(w[2], w[3], kq[b & 1][5]);   // 5 -> 6
+                C3_STEP_SAME(w[3], kq[b & 1][6]);          // 6 -> 7
+                put_x(b, w);
+                C3_STEP_CROSS(w[3], w[0], kq[b & 1][7]);   // 7 -> 0 (the next block's first input)
+            }
         }
     }
 }
@@ -1179,7 +1223,7 @@ __global__ void __launch_bounds__(64 * (WS + 2)) coop3_decode(Coop3Args a)
                 // (skipping a window's trailing pass-through steps -- the plan
                 // fills ~44.9 of r1/2's 48 slots -- measured -0.3 % on one box
                 // and +0.1 % on another, r06c / r06g: not kept)
-                if (p < G && cl) chain_window3<WS, R, 0, NB, NMS>(sm, p & 1, c, w4);
+                if (p < G && cl) chain_window3<WS, R, 0, NB, NMS, D0 == 10>(sm, p & 1, c, w4);
                 if (STAMP) sP[0] += stamp3() - tx;
                 stage(un, (p + KAHEAD) & (TQ - 1));
                 un = (un + 1 == a.nw) ? 0 : un + 1;
